@@ -1,0 +1,100 @@
+"""In-tree native build (no cmake/ninja, no JIT cache): explicit g++/gcc/hipcc lines.
+
+Outputs (git-ignored, travel to the GPU box with the gpurun snapshot):
+  gp1_raytracer_2223_amd/lib/librtx_host.so   C++ host scene layer (g++)
+  gp1_raytracer_2223_amd/lib/librtx_hip.so    HIP render path for gfx950 (hipcc)
+  oracle/_build/librtx_oracle.so              C restatement (test infrastructure)
+  oracle/_ref/ref_harness                     the reference's own sources (test infra,
+                                              only when /root/reference exists)
+
+Every float-producing compile uses -ffp-contract=off and no fast-math: the reference is
+MSVC /fp:precise x64 (no FMA contraction) and parity is bit-level.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+REPO = PKG.parent
+LIB = PKG / "lib"
+CSRC = PKG / "csrc"
+INC = REPO / "include"
+ORACLE = REPO / "oracle"
+REFERENCE = Path("/root/reference")
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("RTX_OFFLOAD_ARCH", "gfx950")
+
+
+def _run(cmd: list[str], cwd: Path | None = None) -> None:
+    print("+", " ".join(str(c) for c in cmd), flush=True)
+    subprocess.run([str(c) for c in cmd], check=True, cwd=cwd)
+
+
+def _stale(out: Path, deps: list[Path]) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps if d.exists())
+
+
+def build_host(force: bool = False) -> Path:
+    LIB.mkdir(exist_ok=True)
+    out = LIB / "librtx_host.so"
+    srcs = [CSRC / "host" / "scene.cpp", CSRC / "host" / "host_api.cpp"]
+    deps = srcs + list((CSRC / "host").glob("*.h")) + [INC / "rtx.h", INC / "rtx_host.h"]
+    if force or _stale(out, deps):
+        _run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
+              "-Wall", "-Wextra", f"-I{INC}", *srcs, "-o", out])
+    return out
+
+
+def build_hip(force: bool = False) -> Path:
+    LIB.mkdir(exist_ok=True)
+    out = LIB / "librtx_hip.so"
+    srcs = [CSRC / "rtx_hip.hip"]
+    deps = srcs + list(CSRC.glob("*.h")) + [INC / "rtx.h"]
+    if force or _stale(out, deps):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-O3", "-ffp-contract=off",
+              "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fPIC", "-shared",
+              "-Wall", f"-I{INC}", f"-I{CSRC}", *srcs, "-o", out])
+    return out
+
+
+def build_oracle(force: bool = False) -> Path:
+    """Test infrastructure: the C restatement used only by tests/, smoke() and bench's
+    cpu_baseline leg."""
+    bdir = ORACLE / "_build"
+    bdir.mkdir(exist_ok=True)
+    out = bdir / "librtx_oracle.so"
+    src = ORACLE / "rtx_oracle.c"
+    if force or _stale(out, [src, INC / "rtx.h"]):
+        _run(["gcc", "-std=c11", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
+              "-Wall", "-Wextra", f"-I{INC}", src, "-o", out, "-lm", "-lpthread"])
+    return out
+
+
+def build_reference(force: bool = False) -> Path | None:
+    """Test infrastructure: the reference's own sources compiled in place (oracle/ref)."""
+    out = ORACLE / "_ref" / "ref_harness"
+    if not (REFERENCE / "source" / "Scene.cpp").exists():
+        return out if out.exists() else None
+    if force and (ORACLE / "_ref").exists():
+        shutil.rmtree(ORACLE / "_ref")
+    _run(["make", "-s", "-C", ORACLE / "ref", "-j8"])
+    return out
+
+
+def build_all(force: bool = False) -> None:
+    build_host(force)
+    build_oracle(force)
+    build_reference(force)
+    build_hip(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

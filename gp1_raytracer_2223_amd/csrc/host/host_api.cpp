@@ -1,0 +1,101 @@
+// host_api.cpp — extern "C" wrappers of the host scene model (include/rtx_host.h).
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "rtx_host.h"
+#include "scene.h"
+
+struct rtx_host_scene {
+    std::unique_ptr<rtx::Scene> scene;
+};
+
+static void set_err(char* err, size_t len, const std::string& msg) {
+    if (err && len) {
+        std::strncpy(err, msg.c_str(), len - 1);
+        err[len - 1] = 0;
+    }
+}
+
+extern "C" int rtx_host_scene_create(const char* name, const char* asset_dir, rtx_host_scene** out, char* err,
+                                     size_t err_len) {
+    if (!name || !out) return RTX_E_INVALID;
+    *out = nullptr;
+    try {
+        auto s = rtx::MakeScene(name, asset_dir ? asset_dir : "");
+        if (!s) { set_err(err, err_len, std::string("unknown scene: ") + name); return RTX_E_INVALID; }
+        if (!s->Initialize()) { set_err(err, err_len, s->Error()); return RTX_E_UNSUPPORTED; }
+        auto* h = new rtx_host_scene;
+        h->scene = std::move(s);
+        *out = h;
+        return RTX_OK;
+    } catch (const std::bad_alloc&) {
+        set_err(err, err_len, "out of memory");
+        return RTX_E_NOMEM;
+    } catch (const std::exception& e) {
+        set_err(err, err_len, e.what());
+        return RTX_E_INVALID;
+    }
+}
+
+extern "C" void rtx_host_scene_destroy(rtx_host_scene* s) { delete s; }
+
+extern "C" int rtx_host_scene_update(rtx_host_scene* s, float total_time) {
+    if (!s) return RTX_E_INVALID;
+    s->scene->Update(total_time);
+    return RTX_OK;
+}
+
+extern "C" int rtx_host_scene_view(rtx_host_scene* s, rtx_scene* out_scene, rtx_camera* out_camera) {
+    if (!s) return RTX_E_INVALID;
+    rtx::Camera& cam = s->scene->GetCamera();
+    cam.CalculateCameraToWorld();   // Renderer.cpp:40
+    if (out_scene) *out_scene = s->scene->View();
+    if (out_camera) *out_camera = cam.View();
+    return RTX_OK;
+}
+
+extern "C" int rtx_host_camera_set(rtx_host_scene* s, const float origin[3], float fov_degrees, float pitch,
+                                   float yaw) {
+    if (!s || !origin) return RTX_E_INVALID;
+    rtx::Camera& cam = s->scene->GetCamera();
+    cam.origin = {origin[0], origin[1], origin[2]};
+    cam.SetCameraFOV(fov_degrees);
+    cam.totalPitch = pitch;
+    cam.totalYaw = yaw;
+    cam.CalculateForwardVector();
+    cam.CalculateCameraToWorld();
+    return RTX_OK;
+}
+
+extern "C" int rtx_host_parse_obj(const char* path, float* positions, uint32_t* n_positions, float* normals,
+                                  int32_t* indices, uint32_t* n_indices, uint32_t cap_pos, uint32_t cap_idx) {
+    if (!path || !n_positions || !n_indices) return RTX_E_INVALID;
+    std::vector<rtx::Vec3> p, n;
+    std::vector<int32_t> idx;
+    try {
+        if (!rtx::ParseOBJ(path, p, n, idx)) return RTX_E_INVALID;
+    } catch (const std::exception&) {
+        return RTX_E_INVALID;
+    }
+    *n_positions = static_cast<uint32_t>(p.size());
+    *n_indices = static_cast<uint32_t>(idx.size());
+    if (positions && p.size() <= cap_pos)
+        for (size_t k = 0; k < p.size(); ++k) { positions[3 * k] = p[k].x; positions[3 * k + 1] = p[k].y; positions[3 * k + 2] = p[k].z; }
+    if (normals && n.size() * 3 <= static_cast<size_t>(cap_idx))
+        for (size_t k = 0; k < n.size(); ++k) { normals[3 * k] = n[k].x; normals[3 * k + 1] = n[k].y; normals[3 * k + 2] = n[k].z; }
+    if (indices && idx.size() <= cap_idx) std::memcpy(indices, idx.data(), idx.size() * 4);
+    return RTX_OK;
+}
+
+extern "C" int rtx_host_obj_to_asset(const char* obj_path, const char* asset_path) {
+    if (!obj_path || !asset_path) return RTX_E_INVALID;
+    std::vector<rtx::Vec3> p, n;
+    std::vector<int32_t> idx;
+    try {
+        if (!rtx::ParseOBJ(obj_path, p, n, idx)) return RTX_E_INVALID;
+    } catch (const std::exception&) {
+        return RTX_E_INVALID;
+    }
+    return rtx::SaveMeshAsset(asset_path, p, idx) ? RTX_OK : RTX_E_INVALID;
+}

@@ -1,0 +1,690 @@
+// scene.cpp — host scene model (see scene.h).  Build with -ffp-contract=off.
+#include "scene.h"
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <random>
+#include <utility>
+
+namespace rtx {
+
+// ---------------------------------------------------------------- TriangleMesh
+void TriangleMesh::AppendTriangle(const Vec3& v0, const Vec3& v1, const Vec3& v2) {
+    // dae::Triangle(v0, v1, v2) computes its normal (DataTypes.h:85-91), then
+    // AppendTriangle pushes 3 fresh vertices + 3 indices + the normal (:158-176).
+    const Vec3 normal = Vec3::Cross(v1 - v0, v2 - v0).Normalized();
+    int32_t start = static_cast<int32_t>(positions.size());
+    positions.push_back(v0); positions.push_back(v1); positions.push_back(v2);
+    indices.push_back(start); indices.push_back(start + 1); indices.push_back(start + 2);
+    normals.push_back(normal);
+}
+
+void TriangleMesh::CalculateNormals() {
+    normals.reserve(indices.size() / 3);
+    for (size_t idx = 0; idx + 2 < indices.size(); idx += 3) {
+        const Vec3& v0 = positions[static_cast<size_t>(indices[idx])];
+        const Vec3& v1 = positions[static_cast<size_t>(indices[idx + 1])];
+        const Vec3& v2 = positions[static_cast<size_t>(indices[idx + 2])];
+        normals.push_back(Vec3::Cross(v1 - v0, v2 - v0).Normalized());
+    }
+}
+
+void TriangleMesh::UpdateAABB() {
+    if (!positions.empty()) {
+        minAABB = positions[0]; maxAABB = positions[0];
+        for (const auto& p : positions) { minAABB = Vec3::Min(p, minAABB); maxAABB = Vec3::Max(p, maxAABB); }
+    }
+}
+
+void TriangleMesh::UpdateTransforms() {
+    const Mat4 finalTransform = scaleTransform * rotationTransform * translationTransform;
+    transformedPositions.clear();
+    transformedPositions.reserve(positions.size());
+    for (const auto& p : positions) transformedPositions.push_back(finalTransform.TransformPoint(p));
+    transformedNormals.clear();
+    transformedNormals.reserve(normals.size());
+    for (const auto& n : normals) transformedNormals.push_back(finalTransform.TransformVector(n).Normalized());
+    BuildBVH();
+}
+
+void TriangleMesh::BuildBVH() {
+    if (nodes.empty() || indices.empty()) return;   // reference: UB / crash (see Scene_W4_TestScene)
+    BVHNode& root = nodes[0];
+    root.leftNode = 0;
+    root.firstIdx = 0;
+    root.idxCount = static_cast<uint32_t>(indices.size());
+    nodesUsed = 1;
+    UpdateNodeBounds(0);
+    Subdivide(0);
+}
+
+void TriangleMesh::UpdateNodeBounds(uint32_t nodeIdx) {
+    BVHNode& node = nodes[nodeIdx];
+    node.minAABB = kMaxVector;
+    node.maxAABB = kMinVector;
+    for (uint32_t i = node.firstIdx; i < node.firstIdx + node.idxCount; ++i) {
+        node.minAABB = Vec3::Min(node.minAABB, transformedPositions[indices[i]]);
+        node.maxAABB = Vec3::Max(node.maxAABB, transformedPositions[indices[i]]);
+    }
+}
+
+float TriangleMesh::CalculateNodeCost(const BVHNode& node) {
+    const Vec3 e = node.maxAABB - node.minAABB;
+    const float area = e.x * e.y + e.y * e.z + e.z * e.x;
+    return static_cast<float>(node.idxCount) * area;
+}
+
+// Binned SAH, 8 bins (DataTypes.h:378-456), including the reference's quirks: centroid
+// scale 0.3333f, centroid bounds starting at {FLT_MAX, FLT_MIN}, and 0*inf = NaN costs
+// for empty sides (never accepted by the strict < comparison).
+float TriangleMesh::FindBestSplitPlane(const BVHNode& node, int& axis, float& splitPos) const {
+    float bestCost = FLT_MAX;
+    for (int axisIdx = 0; axisIdx < 3; ++axisIdx) {
+        float minBounds = FLT_MAX;
+        float maxBounds = FLT_MIN;
+        for (uint32_t idx = 0; idx < node.idxCount; idx += 3) {
+            const Vec3 c = Centroid(node.firstIdx + idx);
+            minBounds = fmin_ref(minBounds, c[axisIdx]);
+            maxBounds = fmax_ref(maxBounds, c[axisIdx]);
+        }
+        const float boundsDifference = maxBounds - minBounds;
+        if (fabsf(boundsDifference) < FLT_EPSILON) continue;
+
+        constexpr int kBins = 8, kPlanes = kBins - 1;
+        AABB binBounds[kBins];
+        uint32_t binCount[kBins] = {0, 0, 0, 0, 0, 0, 0, 0};
+        float scale = kBins / boundsDifference;
+        for (uint32_t idx = 0; idx < node.idxCount; idx += 3) {
+            const uint32_t off = node.firstIdx + idx;
+            const Vec3& v0 = transformedPositions[indices[off]];
+            const Vec3& v1 = transformedPositions[indices[off + 1]];
+            const Vec3& v2 = transformedPositions[indices[off + 2]];
+            const Vec3 c = (v0 + v1 + v2) * 0.3333f;
+            int b = static_cast<int>((c[axisIdx] - minBounds) * scale);
+            if (kPlanes < b) b = kPlanes;   // std::min(amountOfPlaneBins, b)
+            binCount[b] += 3;
+            binBounds[b].Grow(v0); binBounds[b].Grow(v1); binBounds[b].Grow(v2);
+        }
+        float leftArea[kPlanes]{}, rightArea[kPlanes]{};
+        int leftCount[kPlanes]{}, rightCount[kPlanes]{};
+        int leftSum = 0, rightSum = 0;
+        AABB leftBox, rightBox;
+        for (int i = 0; i < kPlanes; ++i) {
+            leftSum += binCount[i];
+            leftCount[i] = leftSum;
+            leftBox.Grow(binBounds[i]);
+            leftArea[i] = leftBox.Area();
+            rightSum += binCount[kPlanes - i];
+            rightCount[kPlanes - i - 1] = rightSum;
+            rightBox.Grow(binBounds[kPlanes - i]);
+            rightArea[kPlanes - i - 1] = rightBox.Area();
+        }
+        scale = boundsDifference / kBins;
+        for (int i = 0; i < kPlanes; ++i) {
+            const float planeCost = static_cast<float>(leftCount[i]) * leftArea[i] +
+                                    static_cast<float>(rightCount[i]) * rightArea[i];
+            if (planeCost < bestCost) {
+                axis = axisIdx;
+                splitPos = minBounds + scale * static_cast<float>(i + 1);
+                bestCost = planeCost;
+            }
+        }
+    }
+    return bestCost;
+}
+
+void TriangleMesh::Subdivide(uint32_t nodeIdx) {
+    if (nodes[nodeIdx].idxCount <= 8) return;
+    int axis = 0;
+    float splitPos = 0.f;
+    const float splitCost = FindBestSplitPlane(nodes[nodeIdx], axis, splitPos);
+    const float noSplitCost = CalculateNodeCost(nodes[nodeIdx]);
+    if (splitCost >= noSplitCost) return;
+
+    // In-place partition (DataTypes.h:335-363): permutes indices, normals and
+    // transformedNormals together.
+    const BVHNode node = nodes[nodeIdx];
+    int i = static_cast<int>(node.firstIdx);
+    int j = i + static_cast<int>(node.idxCount) - 1;
+    while (i <= j) {
+        const Vec3 c = Centroid(static_cast<uint32_t>(i));
+        if (c[axis] < splitPos) {
+            i += 3;
+        } else {
+            std::swap(normals[i / 3], normals[(j - 2) / 3]);
+            std::swap(transformedNormals[i / 3], transformedNormals[(j - 2) / 3]);
+            std::swap(indices[i], indices[j - 2]);
+            std::swap(indices[i + 1], indices[j - 1]);
+            std::swap(indices[i + 2], indices[j]);
+            j -= 3;
+        }
+    }
+    const int leftCount = i - static_cast<int>(node.firstIdx);
+    if (leftCount == 0 || static_cast<uint32_t>(leftCount) == node.idxCount) return;
+
+    const uint32_t leftNodeIdx = nodesUsed++;
+    const uint32_t rightNodeIdx = nodesUsed++;
+    nodes[nodeIdx].leftNode = leftNodeIdx;
+    nodes[leftNodeIdx].firstIdx = node.firstIdx;
+    nodes[leftNodeIdx].idxCount = static_cast<uint32_t>(leftCount);
+    nodes[rightNodeIdx].firstIdx = static_cast<uint32_t>(i);
+    nodes[rightNodeIdx].idxCount = node.idxCount - static_cast<uint32_t>(leftCount);
+    nodes[nodeIdx].idxCount = 0;
+
+    UpdateNodeBounds(leftNodeIdx);
+    UpdateNodeBounds(rightNodeIdx);
+    Subdivide(leftNodeIdx);
+    Subdivide(rightNodeIdx);
+}
+
+// ---------------------------------------------------------------- Camera
+void Camera::SetCameraFOV(float degrees) {
+    fovAngle = fmax_ref(10.f, fmin_ref(degrees, 175.f));
+    fov = tanf(fovAngle * kToRadians / 2.f);
+}
+
+void Camera::CalculateCameraToWorld() {
+    if (forwardChanged) {
+        right = Vec3::Cross(kUnitY, forward).Normalized();
+        up = Vec3::Cross(forward, right).Normalized();
+        forwardChanged = false;
+    }
+}
+
+void Camera::CalculateForwardVector() {
+    const Mat4 finalRotation = Mat4::Rotation({totalPitch, totalYaw, 0.f});
+    forward = finalRotation.TransformVector(kUnitZ);
+    forwardChanged = true;
+}
+
+rtx_camera Camera::View() const {
+    rtx_camera c;
+    const Vec3* v[4] = {&origin, &right, &up, &forward};
+    float* dst[4] = {c.origin, c.right, c.up, c.forward};
+    for (int k = 0; k < 4; ++k) { dst[k][0] = v[k]->x; dst[k][1] = v[k]->y; dst[k][2] = v[k]->z; }
+    c.fov = fov;
+    return c;
+}
+
+// ---------------------------------------------------------------- OBJ
+static void FaceNormals(const std::vector<Vec3>& positions, const std::vector<int32_t>& indices,
+                        std::vector<Vec3>& normals) {
+    // Utils.h:426-448: Cross(v1 - v0, v2 - v0), Normalize()
+    for (uint64_t index = 0; index + 2 < indices.size(); index += 3) {
+        const uint32_t i0 = static_cast<uint32_t>(indices[index]);
+        const uint32_t i1 = static_cast<uint32_t>(indices[index + 1]);
+        const uint32_t i2 = static_cast<uint32_t>(indices[index + 2]);
+        Vec3 n = Vec3::Cross(positions[i1] - positions[i0], positions[i2] - positions[i0]);
+        n.Normalize();
+        normals.push_back(n);
+    }
+}
+
+bool ParseOBJ(const std::string& path, std::vector<Vec3>& positions, std::vector<Vec3>& normals,
+              std::vector<int32_t>& indices) {
+    // Token stream semantics of Utils.h:377-424: first token of a line selects the
+    // command, `f` keeps only the text before the first '/', everything after the
+    // three consumed fields is skipped.
+    std::ifstream file(path);
+    if (!file) return false;
+    std::string cmd;
+    while (!file.eof()) {
+        file >> cmd;
+        if (cmd == "v") {
+            float x, y, z;
+            file >> x >> y >> z;
+            positions.push_back({x, y, z});
+        } else if (cmd == "f") {
+            std::string s0, s1, s2;
+            file >> s0 >> s1 >> s2;
+            if (s0.empty() || s1.empty() || s2.empty()) continue;
+            const float i0 = std::stof(s0.substr(0, s0.find('/')));
+            const float i1 = std::stof(s1.substr(0, s1.find('/')));
+            const float i2 = std::stof(s2.substr(0, s2.find('/')));
+            indices.push_back(static_cast<int32_t>(i0) - 1);
+            indices.push_back(static_cast<int32_t>(i1) - 1);
+            indices.push_back(static_cast<int32_t>(i2) - 1);
+        }
+        file.ignore(1000, '\n');
+        if (file.eof()) break;
+    }
+    FaceNormals(positions, indices, normals);
+    return true;
+}
+
+bool LoadMeshAsset(const std::string& path, std::vector<Vec3>& positions, std::vector<Vec3>& normals,
+                   std::vector<int32_t>& indices) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    char magic[4];
+    uint32_t nv = 0, ni = 0;
+    bool ok = std::fread(magic, 1, 4, f) == 4 && std::memcmp(magic, "RTXM", 4) == 0 &&
+              std::fread(&nv, 4, 1, f) == 1 && std::fread(&ni, 4, 1, f) == 1;
+    if (ok) {
+        std::vector<float> p(3ull * nv);
+        std::vector<int32_t> idx(ni);
+        ok = std::fread(p.data(), 4, p.size(), f) == p.size() && std::fread(idx.data(), 4, idx.size(), f) == idx.size();
+        if (ok) {
+            for (uint32_t k = 0; k < nv; ++k) positions.push_back({p[3 * k], p[3 * k + 1], p[3 * k + 2]});
+            for (uint32_t k = 0; k < ni; ++k) {
+                if (idx[k] < 0 || static_cast<uint32_t>(idx[k]) >= nv) ok = false;
+                indices.push_back(idx[k]);
+            }
+        }
+    }
+    std::fclose(f);
+    if (ok) FaceNormals(positions, indices, normals);
+    return ok;
+}
+
+bool SaveMeshAsset(const std::string& path, const std::vector<Vec3>& positions, const std::vector<int32_t>& indices) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    const uint32_t nv = static_cast<uint32_t>(positions.size()), ni = static_cast<uint32_t>(indices.size());
+    bool ok = std::fwrite("RTXM", 1, 4, f) == 4 && std::fwrite(&nv, 4, 1, f) == 1 && std::fwrite(&ni, 4, 1, f) == 1;
+    for (const auto& p : positions) ok = ok && std::fwrite(&p.x, 4, 3, f) == 3;
+    ok = ok && std::fwrite(indices.data(), 4, indices.size(), f) == indices.size();
+    std::fclose(f);
+    return ok;
+}
+
+// ---------------------------------------------------------------- Scene
+rtx_material SolidColor(const Color& c) {
+    rtx_material m{}; m.kind = RTX_MAT_SOLID_COLOR; m.color[0] = c.r; m.color[1] = c.g; m.color[2] = c.b; return m;
+}
+rtx_material Lambert(const Color& c, float kd) {
+    rtx_material m = SolidColor(c); m.kind = RTX_MAT_LAMBERT; m.kd = kd; return m;
+}
+rtx_material LambertPhong(const Color& c, float kd, float ks, float exponent) {
+    rtx_material m = SolidColor(c); m.kind = RTX_MAT_LAMBERT_PHONG; m.kd = kd; m.ks = ks; m.exponent = exponent; return m;
+}
+rtx_material CookTorrance(const Color& albedo, float metalness, float roughness) {
+    rtx_material m = SolidColor(albedo); m.kind = RTX_MAT_COOK_TORRANCE; m.metalness = metalness; m.roughness = roughness; return m;
+}
+
+namespace colors {
+const Color Red{1, 0, 0}, Blue{0, 0, 1}, Green{0, 1, 0}, Yellow{1, 1, 0}, Magenta{1, 0, 1}, White{1, 1, 1};
+}
+
+Scene::Scene(std::string assetDir) : m_AssetDir(std::move(assetDir)) {
+    m_Materials.push_back(SolidColor({1, 0, 0}));   // Scene.cpp:9-10 default RED
+}
+
+uint8_t Scene::AddSphere(const Vec3& o, float radius, uint8_t mat) {
+    rtx_sphere s{}; s.origin[0] = o.x; s.origin[1] = o.y; s.origin[2] = o.z; s.radius = radius; s.material = mat;
+    m_Spheres.push_back(s);
+    return mat;
+}
+uint8_t Scene::AddPlane(const Vec3& o, const Vec3& n, uint8_t mat) {
+    rtx_plane p{};
+    p.origin[0] = o.x; p.origin[1] = o.y; p.origin[2] = o.z;
+    p.normal[0] = n.x; p.normal[1] = n.y; p.normal[2] = n.z;
+    p.material = mat;
+    m_Planes.push_back(p);
+    return mat;
+}
+TriangleMesh* Scene::AddTriangleMesh(int32_t cullMode, uint8_t mat) {
+    auto m = std::make_unique<TriangleMesh>();
+    m->cullMode = cullMode; m->materialIndex = mat;
+    m_Meshes.push_back(std::move(m));
+    return m_Meshes.back().get();
+}
+void Scene::AddPointLight(const Vec3& o, float intensity, const Color& c) {
+    rtx_light l{};
+    l.origin[0] = o.x; l.origin[1] = o.y; l.origin[2] = o.z;
+    l.color[0] = c.r; l.color[1] = c.g; l.color[2] = c.b;
+    l.intensity = intensity; l.type = RTX_LIGHT_POINT;
+    m_Lights.push_back(l);
+}
+void Scene::AddDirectionalLight(const Vec3& d, float intensity, const Color& c) {
+    rtx_light l{};
+    l.direction[0] = d.x; l.direction[1] = d.y; l.direction[2] = d.z;
+    l.color[0] = c.r; l.color[1] = c.g; l.color[2] = c.b;
+    l.intensity = intensity; l.type = RTX_LIGHT_DIRECTIONAL;
+    m_Lights.push_back(l);
+}
+uint8_t Scene::AddMaterial(const rtx_material& m) {
+    m_Materials.push_back(m);
+    return static_cast<uint8_t>(m_Materials.size() - 1);
+}
+
+bool Scene::LoadMesh(TriangleMesh* m, const std::string& stem) {
+    // Prefer the committed pre-tokenised asset; fall back to an .obj of the same stem.
+    const std::string base = m_AssetDir.empty() ? stem : m_AssetDir + "/" + stem;
+    if (LoadMeshAsset(base + ".rtxmesh", m->positions, m->normals, m->indices)) return true;
+    if (ParseOBJ(base + ".obj", m->positions, m->normals, m->indices)) return true;
+    m_Error = "mesh asset not found: " + base + ".rtxmesh / .obj";
+    return false;
+}
+
+rtx_scene Scene::View() {
+    m_MeshViews.clear();
+    for (auto& m : m_Meshes) {
+        rtx_mesh v{};
+        v.positions = m->transformedPositions.empty() ? nullptr : &m->transformedPositions[0].x;
+        v.n_positions = static_cast<uint32_t>(m->transformedPositions.size());
+        v.indices = m->indices.data();
+        v.n_indices = static_cast<uint32_t>(m->indices.size());
+        v.normals = m->transformedNormals.empty() ? nullptr : &m->transformedNormals[0].x;
+        v.nodes = reinterpret_cast<const rtx_bvh_node*>(m->nodes.data());
+        v.n_nodes = m->nodes.empty() ? 0 : m->nodesUsed;
+        v.cull_mode = m->cullMode;
+        v.material = m->materialIndex;
+        m_MeshViews.push_back(v);
+    }
+    rtx_scene s{};
+    s.spheres = m_Spheres.data(); s.n_spheres = static_cast<uint32_t>(m_Spheres.size());
+    s.planes = m_Planes.data(); s.n_planes = static_cast<uint32_t>(m_Planes.size());
+    s.meshes = m_MeshViews.data(); s.n_meshes = static_cast<uint32_t>(m_MeshViews.size());
+    s.lights = m_Lights.data(); s.n_lights = static_cast<uint32_t>(m_Lights.size());
+    s.materials = m_Materials.data(); s.n_materials = static_cast<uint32_t>(m_Materials.size());
+    return s;
+}
+
+// ---------------------------------------------------------------- catalogue
+namespace {
+
+// Scene.cpp:164-184
+class SceneW1 final : public Scene {
+public:
+    using Scene::Scene;
+    bool Initialize() override {
+        sceneName = "W1";
+        constexpr uint8_t red = 0;
+        const uint8_t blue = AddMaterial(SolidColor(colors::Blue));
+        const uint8_t yellow = AddMaterial(SolidColor(colors::Yellow));
+        const uint8_t green = AddMaterial(SolidColor(colors::Green));
+        const uint8_t magenta = AddMaterial(SolidColor(colors::Magenta));
+        AddSphere({-25.f, 0.f, 100.f}, 50.f, red);
+        AddSphere({25.f, 0.f, 100.f}, 50.f, blue);
+        AddPlane({-75.f, 0.f, 0.f}, {1.f, 0.f, 0.f}, green);
+        AddPlane({75.f, 0.f, 0.f}, {-1.f, 0.f, 0.f}, green);
+        AddPlane({0.f, -75.f, 0.f}, {0.f, 1.f, 0.f}, yellow);
+        AddPlane({0.f, 75.f, 0.f}, {0.f, -1.f, 0.f}, yellow);
+        AddPlane({0.f, 0.f, 125.f}, {0.f, 0.f, -1.f}, magenta);
+        return true;
+    }
+};
+
+// Scene.cpp:188-218
+class SceneW2 final : public Scene {
+public:
+    using Scene::Scene;
+    bool Initialize() override {
+        sceneName = "W2";
+        m_Camera.origin = {0.f, 3.f, -9.f};
+        m_Camera.SetCameraFOV(45.f);
+        constexpr uint8_t red = 0;
+        const uint8_t blue = AddMaterial(SolidColor(colors::Blue));
+        const uint8_t yellow = AddMaterial(SolidColor(colors::Yellow));
+        const uint8_t green = AddMaterial(SolidColor(colors::Green));
+        const uint8_t magenta = AddMaterial(SolidColor(colors::Magenta));
+        AddPlane({-5.f, 0.f, 0.f}, {1.f, 0.f, 0.f}, green);
+        AddPlane({5.f, 0.f, 0.f}, {-1.f, 0.f, 0.f}, green);
+        AddPlane({0.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, yellow);
+        AddPlane({0.f, 10.f, 0.f}, {0.f, -1.f, 0.f}, yellow);
+        AddPlane({0.f, 0.f, 10.f}, {0.f, 0.f, -1.f}, magenta);
+        AddSphere({-1.75f, 1.f, 0.f}, 0.75f, red);
+        AddSphere({0.f, 1.f, 0.f}, 0.75f, blue);
+        AddSphere({1.75f, 1.f, 0.f}, 0.75f, red);
+        AddSphere({-1.75f, 3.f, 0.f}, 0.75f, blue);
+        AddSphere({0.f, 3.f, 0.f}, 0.75f, red);
+        AddSphere({1.75f, 3.f, 0.f}, 0.75f, blue);
+        AddPointLight({0.f, 5.f, -5.f}, 70.f, colors::White);
+        return true;
+    }
+};
+
+// Scene.cpp:223-243
+class SceneW3Test final : public Scene {
+public:
+    using Scene::Scene;
+    bool Initialize() override {
+        sceneName = "W3_Test";
+        m_Camera.origin = {0.f, 1.f, -5.f};
+        m_Camera.SetCameraFOV(45.f);
+        const uint8_t red = AddMaterial(Lambert(colors::Red, 1.f));
+        const uint8_t bluePhong = AddMaterial(LambertPhong(colors::Blue, 1.f, 1.f, 60.f));
+        const uint8_t yellow = AddMaterial(Lambert(colors::Yellow, 1.f));
+        AddPlane({0.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, yellow);
+        AddSphere({-0.75f, 1.f, 0.f}, 1.f, red);
+        AddSphere({0.75f, 1.f, 0.f}, 1.f, bluePhong);
+        AddPointLight({0.f, 5.f, 5.f}, 25.f, colors::White);
+        AddPointLight({0.f, 2.5f, -5.f}, 25.f, colors::White);
+        return true;
+    }
+};
+
+class CatalogueScene : public Scene {
+public:
+    using Scene::Scene;
+protected:
+    uint8_t Mat(const rtx_material& m) { return AddMaterial(m); }
+    void RoomPlanes(uint8_t mat) {   // the 5 planes shared by W3/W4 (e.g. Scene.cpp:263-267)
+        AddPlane({0.f, 0.f, 10.f}, {0.f, 0.f, -1.f}, mat);
+        AddPlane({0.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, mat);
+        AddPlane({0.f, 10.f, 0.f}, {0.f, -1.f, 0.f}, mat);
+        AddPlane({5.f, 0.f, 0.f}, {-1.f, 0.f, 0.f}, mat);
+        AddPlane({-5.f, 0.f, 0.f}, {1.f, 0.f, 0.f}, mat);
+    }
+    void CtMaterials(uint8_t out[6]) {
+        const Color metal{0.972f, 0.960f, 0.915f}, plastic{0.75f, 0.75f, 0.75f};
+        out[0] = Mat(CookTorrance(metal, 1.f, 1.f));
+        out[1] = Mat(CookTorrance(metal, 1.f, 0.6f));
+        out[2] = Mat(CookTorrance(metal, 1.f, 0.1f));
+        out[3] = Mat(CookTorrance(plastic, 0.f, 1.f));
+        out[4] = Mat(CookTorrance(plastic, 0.f, 0.6f));
+        out[5] = Mat(CookTorrance(plastic, 0.f, 0.1f));
+    }
+    void SixSpheres(const uint8_t m[6]) {   // Scene.cpp:273-278
+        AddSphere({-1.75f, 1.f, 0.f}, 0.75f, m[0]);
+        AddSphere({0.f, 1.f, 0.f}, 0.75f, m[1]);
+        AddSphere({1.75f, 1.f, 0.f}, 0.75f, m[2]);
+        AddSphere({-1.75f, 3.f, 0.f}, 0.75f, m[3]);
+        AddSphere({0.f, 3.f, 0.f}, 0.75f, m[4]);
+        AddSphere({1.75f, 3.f, 0.f}, 0.75f, m[5]);
+    }
+    void ThreeLights() {                    // Scene.cpp:282-284
+        AddPointLight({0.f, 5.f, 5.f}, 50.f, Color{1.f, 0.61f, 0.45f});
+        AddPointLight({-2.5f, 5.f, -5.f}, 70.f, Color{1.f, 0.8f, 0.45f});
+        AddPointLight({2.5f, 2.5f, -5.f}, 50.f, Color{0.34f, 0.47f, 0.68f});
+    }
+    static float Yaw(float t) { return (cosf(t) + 1.f) / 2.f * kPi2; }   // Scene.cpp:394
+};
+
+// Scene.cpp:245-286
+class SceneW3 final : public CatalogueScene {
+public:
+    using CatalogueScene::CatalogueScene;
+    bool Initialize() override {
+        sceneName = "W3";
+        m_Camera.origin = {0.f, 3.f, -9.f};
+        m_Camera.SetCameraFOV(45.f);
+        uint8_t ct[6];
+        CtMaterials(ct);
+        const uint8_t grayBlue = Mat(Lambert({0.49f, 0.57f, 0.57f}, 1.f));
+        Mat(LambertPhong(colors::Blue, 0.5f, 0.5f, 3.f));
+        Mat(LambertPhong(colors::Blue, 0.5f, 0.5f, 15.f));
+        Mat(LambertPhong(colors::Blue, 0.5f, 0.5f, 30.f));
+        RoomPlanes(grayBlue);
+        SixSpheres(ct);
+        ThreeLights();
+        return true;
+    }
+};
+
+// Scene.cpp:289-328 — the reference never allocates pBVHNodes for this scene and
+// crashes in BuildBVH (segfault); we refuse it with an error instead.
+class SceneW4Test final : public CatalogueScene {
+public:
+    using CatalogueScene::CatalogueScene;
+    bool Initialize() override {
+        sceneName = "W4_Test";
+        m_Error = "Scene_W4_TestScene is not renderable: the reference never allocates its BVH nodes "
+                  "(Scene.cpp:306-310 vs DataTypes.h:231-232) and crashes";
+        return false;
+    }
+};
+
+// Scene.cpp:330-400
+class SceneW4Reference final : public CatalogueScene {
+public:
+    using CatalogueScene::CatalogueScene;
+    bool Initialize() override {
+        sceneName = "W4_Reference";
+        m_Camera.origin = {0.f, 3.f, -9.f};
+        m_Camera.SetCameraFOV(45.f);
+        uint8_t ct[6];
+        CtMaterials(ct);
+        const uint8_t grayBlue = Mat(Lambert({0.49f, 0.57f, 0.57f}, 1.f));
+        const uint8_t white = Mat(Lambert(colors::White, 1.f));
+        RoomPlanes(grayBlue);
+        SixSpheres(ct);
+        const Vec3 a{-0.75f, 1.5f, 0.f}, b{0.75f, 0.f, 0.f}, c{-0.75f, 0.f, 0.f};
+        const int32_t culls[3] = {RTX_CULL_BACK, RTX_CULL_FRONT, RTX_CULL_NONE};
+        const float xs[3] = {-1.75f, 0.f, 1.75f};
+        for (int k = 0; k < 3; ++k) {
+            TriangleMesh* m = AddTriangleMesh(culls[k], white);
+            m->AppendTriangle(a, b, c);
+            m->Translate({xs[k], 4.5f, 0.f});
+            m->AllocateNodes();
+            m->UpdateAABB();
+            m->UpdateTransforms();
+        }
+        ThreeLights();
+        return true;
+    }
+    void Update(float t) override {
+        const float yaw = Yaw(t);
+        for (auto& m : m_Meshes) { m->RotateY(yaw); m->UpdateTransforms(); }
+    }
+};
+
+// Scene.cpp:402-437
+class SceneW4Bunny : public CatalogueScene {
+public:
+    using CatalogueScene::CatalogueScene;
+    bool Initialize() override {
+        sceneName = "W4_Bunny";
+        m_Camera.origin = {0.f, 3.f, -9.f};
+        m_Camera.SetCameraFOV(45.f);
+        const uint8_t grayBlue = Mat(Lambert({0.49f, 0.57f, 0.57f}, 1.f));
+        const uint8_t white = Mat(Lambert(colors::White, 1.f));
+        TriangleMesh* m = AddTriangleMesh(RTX_CULL_BACK, white);
+        if (!LoadMesh(m, "lowpoly_bunny2")) return false;
+        m->Scale({2.f, 2.f, 2.f});
+        m->AllocateNodes();
+        m->UpdateAABB();
+        m->UpdateTransforms();
+        RoomPlanes(grayBlue);
+        ThreeLights();
+        return true;
+    }
+    void Update(float t) override {
+        m_Meshes[0]->RotateY(Yaw(t));
+        m_Meshes[0]->UpdateTransforms();
+    }
+};
+
+// Bunny + 5 lights at (3.5cos θk, 5.5, 3.5 sin θk − 2), θk = 2πk/5,
+// intensity 40, colours cycling the reference trio.
+class SceneBunny8Lights final : public SceneW4Bunny {
+public:
+    using SceneW4Bunny::SceneW4Bunny;
+    bool Initialize() override {
+        if (!SceneW4Bunny::Initialize()) return false;
+        sceneName = "Bunny8Lights";
+        const Color trio[3] = {{1.f, 0.61f, 0.45f}, {1.f, 0.8f, 0.45f}, {0.34f, 0.47f, 0.68f}};
+        for (int k = 0; k < 5; ++k) {
+            const float theta = kPi2 * static_cast<float>(k) / 5.f;
+            AddPointLight({3.5f * cosf(theta), 5.5f, 3.5f * sinf(theta) - 2.f}, 40.f, trio[k % 3]);
+        }
+        return true;
+    }
+};
+
+// Scene.cpp:439-474
+class SceneW4Optional final : public CatalogueScene {
+public:
+    using CatalogueScene::CatalogueScene;
+    bool Initialize() override {
+        sceneName = "W4_Optional";
+        m_Camera.origin = {0.f, 2.f, -9.f};
+        m_Camera.SetCameraFOV(45.f);
+        const uint8_t grayBlue = Mat(Lambert({0.49f, 0.57f, 0.57f}, 1.f));
+        const uint8_t copper = Mat(CookTorrance({0.72f, 0.254f, 0.055f}, 1.0f, 0.7f));
+        TriangleMesh* m = AddTriangleMesh(RTX_CULL_BACK, copper);
+        if (!LoadMesh(m, "Assignment3D1")) return false;
+        m->Scale({0.03f, 0.03f, 0.03f});
+        m->AllocateNodes();
+        m->UpdateAABB();
+        m->UpdateTransforms();
+        RoomPlanes(grayBlue);
+        ThreeLights();
+        return true;
+    }
+    void Update(float t) override {
+        m_Meshes[0]->RotateY(Yaw(t));
+        m_Meshes[0]->UpdateTransforms();
+    }
+};
+
+// 250 x 200-quad height field = 100,000 triangles over
+// x in [-3,3], z in [-1,3], y = 0.3 + 0.5 u, u = (mt19937(42)() >> 8) * 2^-24 per vertex
+// (z outer, x inner); back-face culled, Lambert white; Bunny-scene planes and lights.
+class SceneSynthetic100k final : public CatalogueScene {
+public:
+    using CatalogueScene::CatalogueScene;
+    bool Initialize() override {
+        sceneName = "Synthetic100k";
+        m_Camera.origin = {0.f, 3.f, -9.f};
+        m_Camera.SetCameraFOV(45.f);
+        const uint8_t grayBlue = Mat(Lambert({0.49f, 0.57f, 0.57f}, 1.f));
+        const uint8_t white = Mat(Lambert(colors::White, 1.f));
+        TriangleMesh* m = AddTriangleMesh(RTX_CULL_BACK, white);
+        const int NX = 250, NZ = 200;
+        std::mt19937 rng(42);
+        for (int j = 0; j <= NZ; ++j) {
+            for (int i = 0; i <= NX; ++i) {
+                const float u = static_cast<float>(rng() >> 8) * (1.0f / 16777216.0f);
+                const float x = -3.0f + (6.0f * static_cast<float>(i)) / 250.0f;
+                const float z = -1.0f + (4.0f * static_cast<float>(j)) / 200.0f;
+                m->positions.push_back({x, 0.3f + 0.5f * u, z});
+            }
+        }
+        for (int j = 0; j < NZ; ++j) {
+            for (int i = 0; i < NX; ++i) {
+                const int32_t v00 = j * (NX + 1) + i, v10 = v00 + 1, v01 = v00 + (NX + 1), v11 = v01 + 1;
+                const int32_t tri[6] = {v00, v01, v10, v10, v01, v11};
+                for (int32_t k : tri) m->indices.push_back(k);
+            }
+        }
+        m->CalculateNormals();
+        m->AllocateNodes();
+        m->UpdateAABB();
+        m->UpdateTransforms();
+        RoomPlanes(grayBlue);
+        ThreeLights();
+        return true;
+    }
+};
+
+}  // namespace
+
+std::unique_ptr<Scene> MakeScene(const std::string& name, const std::string& assetDir) {
+    std::unique_ptr<Scene> s;
+    if (name == "W1") s = std::make_unique<SceneW1>(assetDir);
+    else if (name == "W2") s = std::make_unique<SceneW2>(assetDir);
+    else if (name == "W3") s = std::make_unique<SceneW3>(assetDir);
+    else if (name == "W3_Test") s = std::make_unique<SceneW3Test>(assetDir);
+    else if (name == "W4_Test") s = std::make_unique<SceneW4Test>(assetDir);
+    else if (name == "W4_Reference") s = std::make_unique<SceneW4Reference>(assetDir);
+    else if (name == "W4_Bunny") s = std::make_unique<SceneW4Bunny>(assetDir);
+    else if (name == "Bunny8Lights") s = std::make_unique<SceneBunny8Lights>(assetDir);
+    else if (name == "W4_Optional") s = std::make_unique<SceneW4Optional>(assetDir);
+    else if (name == "Synthetic100k") s = std::make_unique<SceneSynthetic100k>(assetDir);
+    return s;
+}
+
+}  // namespace rtx

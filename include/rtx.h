@@ -1,0 +1,207 @@
+/*
+ * rtx.h — C-ABI drop-in boundary for the per-pixel render loop of
+ * JonathanMenschaert/GP1_Raytracer_2223 (`Renderer::Render` → `RenderPixel`).
+ *
+ * The reference has no plugin API; its seam is `Renderer::Render(Scene*) const`
+ * (source/Renderer.h:28, called once per frame from source/main.cpp:91) with the
+ * per-pixel body `Renderer::RenderPixel` (source/Renderer.cpp:100-182).  This header
+ * replaces that seam with plain C: the caller flattens its Scene into `rtx_scene`
+ * (plain pointers + sizes, no C++ or torch types), uploads it once to HBM with
+ * `rtx_upload_scene`, then calls `rtx_render` once per frame.
+ *
+ * Scene records are laid out byte-for-byte like the reference's own value types so a
+ * reference Scene can hand its std::vector storage over without repacking:
+ *   rtx_sphere   == dae::Sphere   (source/DataTypes.h:13-19,  20 B)
+ *   rtx_plane    == dae::Plane    (source/DataTypes.h:21-27,  28 B)
+ *   rtx_bvh_node == dae::BVHNode  (source/DataTypes.h:43-54,  36 B)
+ *   rtx_light    == dae::Light    (source/DataTypes.h:528-536, 44 B)
+ * Materials are polymorphic in the reference (source/Material.h) and are flattened
+ * into the tagged `rtx_material`.
+ *
+ * Error convention: every entry point returns RTX_OK (0) or a negative RTX_E_* code and
+ * never throws across the ABI; `rtx_last_error` gives a human-readable reason.  (The
+ * reference itself has no error channel: Renderer::Render returns void.)
+ *
+ * Threading: like Renderer::Render (called only from the main thread), one caller
+ * thread per rtx_ctx.  Different contexts (one per GPU) may be driven concurrently.
+ */
+#ifndef RTX_H_
+#define RTX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTX_ABI_VERSION 1
+
+enum {
+    RTX_OK = 0,
+    RTX_E_INVALID = -1,   /* bad argument / malformed scene                          */
+    RTX_E_DEVICE = -2,    /* HIP runtime error (message in rtx_last_error)           */
+    RTX_E_NOMEM = -3,     /* host or device allocation failed                       */
+    RTX_E_STATE = -4,     /* e.g. rtx_render before rtx_upload_scene                 */
+    RTX_E_UNSUPPORTED = -5
+};
+
+/* dae::TriangleCullMode (source/DataTypes.h:29-34), same enumerator order */
+enum { RTX_CULL_FRONT = 0, RTX_CULL_BACK = 1, RTX_CULL_NONE = 2 };
+/* dae::LightType (source/DataTypes.h:522-526) */
+enum { RTX_LIGHT_POINT = 0, RTX_LIGHT_DIRECTIONAL = 1 };
+/* Renderer::LightingMode (source/Renderer.h:40-48), same enumerator order */
+enum {
+    RTX_MODE_OBSERVED_AREA = 0,
+    RTX_MODE_RADIANCE = 1,
+    RTX_MODE_BRDF = 2,
+    RTX_MODE_COMBINED = 3,
+    RTX_MODE_COUNT = 4
+};
+/* Material subclasses of source/Material.h */
+enum {
+    RTX_MAT_SOLID_COLOR = 0,   /* Material_SolidColor    Material.h:34-48   */
+    RTX_MAT_LAMBERT = 1,       /* Material_Lambert       Material.h:54-68   */
+    RTX_MAT_LAMBERT_PHONG = 2, /* Material_LambertPhong  Material.h:74-94   */
+    RTX_MAT_COOK_TORRANCE = 3  /* Material_CookTorrence  Material.h:99-129  */
+};
+
+typedef struct rtx_sphere {
+    float origin[3];
+    float radius;
+    uint8_t material;
+    uint8_t _pad[3];
+} rtx_sphere;
+
+typedef struct rtx_plane {
+    float origin[3];
+    float normal[3];
+    uint8_t material;
+    uint8_t _pad[3];
+} rtx_plane;
+
+/* One node of the reference's binned-SAH BVH.  `idx_count` and `first_idx` count
+ * INDICES (3 per triangle), leaf iff idx_count > 0, right child = left_node + 1. */
+typedef struct rtx_bvh_node {
+    float min[3];
+    float max[3];
+    uint32_t first_idx;
+    uint32_t idx_count;
+    uint32_t left_node;
+} rtx_bvh_node;
+
+/* A TriangleMesh after UpdateTransforms()/BuildBVH() (source/DataTypes.h:109-236):
+ * world-space positions, the BVH-permuted index array, per-triangle world normals
+ * (transformedNormals, indexed by index/3) and the node array (nodesUsed entries). */
+typedef struct rtx_mesh {
+    const float* positions;   /* 3 * n_positions floats (transformedPositions) */
+    uint32_t n_positions;
+    const int32_t* indices;   /* n_indices = 3 * triangles                    */
+    uint32_t n_indices;
+    const float* normals;     /* 3 * (n_indices / 3) floats (transformedNormals) */
+    const rtx_bvh_node* nodes;
+    uint32_t n_nodes;
+    int32_t cull_mode;        /* RTX_CULL_*                                   */
+    uint8_t material;
+    uint8_t _pad[3];
+} rtx_mesh;
+
+typedef struct rtx_light {
+    float origin[3];
+    float direction[3];
+    float color[3];
+    float intensity;
+    int32_t type;             /* RTX_LIGHT_* */
+} rtx_light;
+
+/* Flattened Material.  Field use per kind:
+ *   SOLID_COLOR   : color
+ *   LAMBERT       : color (diffuse colour), kd
+ *   LAMBERT_PHONG : color, kd, ks, exponent
+ *   COOK_TORRANCE : color (albedo), metalness, roughness                         */
+typedef struct rtx_material {
+    int32_t kind;
+    float color[3];
+    float kd;
+    float ks;
+    float exponent;
+    float metalness;
+    float roughness;
+} rtx_material;
+
+typedef struct rtx_scene {
+    const rtx_sphere* spheres;     uint32_t n_spheres;
+    const rtx_plane* planes;       uint32_t n_planes;
+    const rtx_mesh* meshes;        uint32_t n_meshes;
+    const rtx_light* lights;       uint32_t n_lights;
+    const rtx_material* materials; uint32_t n_materials;
+} rtx_scene;
+
+/* Camera after Camera::CalculateCameraToWorld() (source/Camera.h:43-53): the rows of
+ * cameraToWorld, the ray origin and fov = tanf(fovAngle*TO_RADIANS/2) (Camera.h:55-59). */
+typedef struct rtx_camera {
+    float origin[3];
+    float right[3];
+    float up[3];
+    float forward[3];
+    float fov;
+} rtx_camera;
+
+/* SDL_MapRGB for a palette-less 8-bit-per-channel surface:
+ * pixel = r<<rshift | g<<gshift | b<<bshift | amask.  XRGB8888 = {16, 8, 0, 0}. */
+typedef struct rtx_pixel_format {
+    uint32_t rshift, gshift, bshift, amask;
+} rtx_pixel_format;
+
+/* Per-frame parameters (the Renderer's state: m_Width/m_Height, m_CurrentLightingMode,
+ * m_ShadowsEnabled — source/Renderer.h:40-61) plus the image partition for multi-GPU:
+ * rows are grouped in stripes of `stripe_rows`; this call renders stripe s iff
+ * s % stripe_step == stripe_first.  stripe_rows = 0 means "the whole image". */
+typedef struct rtx_render_params {
+    uint32_t width, height;
+    int32_t lighting_mode;        /* RTX_MODE_* (default RTX_MODE_COMBINED) */
+    int32_t shadows_enabled;      /* 0/1 (default 1)                         */
+    rtx_pixel_format format;
+    uint32_t stripe_rows;
+    uint32_t stripe_first;
+    uint32_t stripe_step;
+} rtx_render_params;
+
+typedef struct rtx_ctx rtx_ctx;
+
+/* ---- device context (librtx_hip.so) ------------------------------------------- */
+int rtx_abi_version(void);
+/* Bind a context to HIP device `device_id` (one context per GPU; one process per GPU
+ * is the supported multi-GPU model).  Creates its own non-blocking stream. */
+int rtx_create(rtx_ctx** out, int device_id);
+void rtx_destroy(rtx_ctx* ctx);
+const char* rtx_last_error(const rtx_ctx* ctx);
+/* Copy the caller-owned scene into HBM (device layout of DESIGN.md §3).  The caller
+ * may free its arrays afterwards.  Re-call after an animated Scene::Update. */
+int rtx_upload_scene(rtx_ctx* ctx, const rtx_scene* scene);
+/* Blocking frame render, like Renderer::Render: renders the rows selected by
+ * `params` and writes them into the caller's host buffers (row-major, pitch = width
+ * pixels; rows this call does not own are left untouched).  out_rgb (3 floats per
+ * pixel, post-MaxToOne colour) may be NULL. */
+int rtx_render(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
+               uint32_t* out_pixels, float* out_rgb);
+/* Asynchronous variant for device-resident pipelines: renders into the context's HBM
+ * frame buffer on the context stream and returns immediately. */
+int rtx_render_async(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
+                     int want_rgb);
+int rtx_synchronize(rtx_ctx* ctx);
+/* Copy the context's frame buffer (rows owned by the last render) to host memory. */
+int rtx_download(rtx_ctx* ctx, uint32_t* out_pixels, float* out_rgb);
+/* Device pointers of the HBM frame buffer (width*height uint32 / 3*width*height f32). */
+int rtx_device_buffers(rtx_ctx* ctx, void** d_pixels, void** d_rgb);
+/* Time `iters` back-to-back launches of the render kernel(s) with HIP events recorded
+ * on the context stream; writes the mean per-frame device time in ms. */
+int rtx_time_frames(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
+                    int iters, float* mean_ms);
+/* Work counters of the last uploaded scene (device bytes resident). */
+int rtx_scene_bytes(const rtx_ctx* ctx, uint64_t* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTX_H_ */

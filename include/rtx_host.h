@@ -1,0 +1,47 @@
+/*
+ * rtx_host.h — C-ABI of the host scene library (librtx_host.so, C++): the Scene layer
+ * that sits ABOVE the render boundary of rtx.h.  It mirrors the reference's
+ * Scene::Initialize / Scene::Update / Scene::GetCamera (source/Scene.h:30-43) for the
+ * scene catalogue of source/Scene.cpp:163-474 and flattens a scene into the rtx_scene
+ * view that rtx_upload_scene() consumes.
+ */
+#ifndef RTX_HOST_H_
+#define RTX_HOST_H_
+
+#include "rtx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rtx_host_scene rtx_host_scene;
+
+/* Build a catalogue scene (W1, W2, W3, W3_Test, W4_Test, W4_Reference, W4_Bunny,
+ * W4_Optional, Synthetic100k, Bunny8Lights) — Scene_*::Initialize().  Mesh assets are
+ * looked up in `asset_dir` as <stem>.rtxmesh, then <stem>.obj.  On failure returns an
+ * error code and, if err/err_len are given, the reason. */
+int rtx_host_scene_create(const char* name, const char* asset_dir, rtx_host_scene** out, char* err,
+                          size_t err_len);
+void rtx_host_scene_destroy(rtx_host_scene* s);
+/* Scene_W4_*::Update minus the SDL camera input: yaw = (cos t + 1)/2 * 2pi on every
+ * animated mesh, transforms + BVH rebuilt (source/Scene.cpp:391-400, 431-437, 468-474). */
+int rtx_host_scene_update(rtx_host_scene* s, float total_time);
+/* Flat view (pointers into the scene; valid until the next update/destroy) and the
+ * camera after CalculateCameraToWorld(). */
+int rtx_host_scene_view(rtx_host_scene* s, rtx_scene* out_scene, rtx_camera* out_camera);
+/* Camera controls (Camera.h): origin, fov in degrees (SetCameraFOV), pitch/yaw in
+ * radians (CalculateForwardVector). */
+int rtx_host_camera_set(rtx_host_scene* s, const float origin[3], float fov_degrees, float pitch, float yaw);
+
+/* Utils::ParseOBJ (source/Utils.h:377-451).  Fills caller buffers when non-NULL and
+ * always reports the counts; returns RTX_OK or RTX_E_INVALID (unreadable file). */
+int rtx_host_parse_obj(const char* path, float* positions, uint32_t* n_positions, float* normals,
+                       int32_t* indices, uint32_t* n_indices, uint32_t capacity_positions,
+                       uint32_t capacity_indices);
+/* Convert an .obj into the pre-tokenised .rtxmesh asset format. */
+int rtx_host_obj_to_asset(const char* obj_path, const char* asset_path);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTX_HOST_H_ */
