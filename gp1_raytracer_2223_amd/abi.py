@@ -133,7 +133,8 @@ def load_host() -> C.CDLL:
 
 HIP_SYMBOLS = ["rtx_abi_version", "rtx_create", "rtx_destroy", "rtx_last_error", "rtx_upload_scene",
                "rtx_render", "rtx_render_async", "rtx_synchronize", "rtx_download", "rtx_device_buffers",
-               "rtx_time_frames", "rtx_scene_bytes", "rtx_count_work"]
+               "rtx_time_frames", "rtx_scene_bytes", "rtx_count_work",
+               "rtx_render_views_async", "rtx_time_views"]
 
 
 def load_hip() -> C.CDLL:
@@ -161,6 +162,11 @@ def load_hip() -> C.CDLL:
         lib.rtx_render.restype = C.c_int
         lib.rtx_render_async.argtypes = [VP, C.POINTER(Camera), C.POINTER(RenderParams), C.c_int]
         lib.rtx_render_async.restype = C.c_int
+        lib.rtx_render_views_async.argtypes = [VP, C.POINTER(Camera), C.c_int, C.POINTER(RenderParams), C.c_int]
+        lib.rtx_render_views_async.restype = C.c_int
+        lib.rtx_time_views.argtypes = [VP, C.POINTER(Camera), C.c_int, C.POINTER(RenderParams), C.c_int,
+                                       C.POINTER(C.c_float)]
+        lib.rtx_time_views.restype = C.c_int
         lib.rtx_synchronize.argtypes = [VP]
         lib.rtx_synchronize.restype = C.c_int
         lib.rtx_download.argtypes = [VP, C.POINTER(C.c_uint32), C.POINTER(C.c_float)]

@@ -1,0 +1,890 @@
+// rtx_hip.hip — MI355X (gfx950) render path behind the C-ABI of include/rtx.h.
+//
+// One HIP thread per pixel; one wave64 = an 8x8 pixel tile; one 256-thread workgroup =
+// 16x16 pixels.  The BVH is traversed by the WAVE, not by the lane: a wave-uniform DFS
+// stack of (node, 64-bit lane mask) lives in LDS, node/triangle/sphere/plane/light
+// records are fetched once per wave through the scalar unit (s_load into SGPRs: the
+// address is wave-uniform), and each lane evaluates its own ray against them under its
+// mask bit.  A lane takes part in a node exactly when the reference's per-ray
+// recursive DFS (source/Utils.h:246-288) would visit that node for its ray, in the same
+// left-then-right order, so closest-hit tie-breaking (strict <) is the reference's.
+// Shadow rays use the same packet traversal with __ballot early-out: a lane leaves the
+// mask at its first occluder and the wave stops when every lane is occluded.
+//
+// Numerics: every float operation restates the reference in IEEE binary32 in the same
+// order (built with -ffp-contract=off, correctly rounded div/sqrt); powf (Phong,
+// Fresnel) is the device libm's and may differ from the host's by an ulp.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rtx.h"
+#include "rtx_kernels.h"
+
+using namespace rtxd;
+
+#define RTX_PI 3.14159265358979323846f   // MathHelpers.h:7
+
+// ====================================================================== device code
+namespace {
+
+__device__ __forceinline__ float smin(float a, float b) { return (b < a) ? b : a; }  // std::min
+__device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a; }  // std::max
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ unsigned long long uni64(unsigned long long x) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32));
+    return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+
+struct Ray {
+    float ox, oy, oz, dx, dy, dz, ix, iy, iz, tmin, tmax;
+};
+
+// dae::Ray constructor (DataTypes.h:549-564): inversedDir = 1 / dir
+__device__ __forceinline__ Ray make_ray(float ox, float oy, float oz, float dx, float dy, float dz, float tmin,
+                                        float tmax) {
+    Ray r;
+    r.ox = ox; r.oy = oy; r.oz = oz; r.dx = dx; r.dy = dy; r.dz = dz;
+    r.ix = 1.f / dx; r.iy = 1.f / dy; r.iz = 1.f / dz;
+    r.tmin = tmin; r.tmax = tmax;
+    return r;
+}
+
+// HitTest_Sphere (Utils.h:52-66) — t and the accept test; hit data is rebuilt later.
+__device__ __forceinline__ bool sphere_t(const float4 s, const Ray& r, float& t) {
+    const float ovx = s.x - r.ox, ovy = s.y - r.oy, ovz = s.z - r.oz;
+    const float ovs = ovx * ovx + ovy * ovy + ovz * ovz;
+    const float proj = r.dx * ovx + r.dy * ovy + r.dz * ovz;
+    const float perp = ovs - proj * proj;
+    if (s.w < perp) return false;
+    const float dist = sqrtf(s.w - perp);
+    t = proj - dist;
+    return !(t < r.tmin || t > r.tmax);
+}
+
+// HitTest_Plane (Utils.h:84-97)
+__device__ __forceinline__ bool plane_t(const float4 p0, const float4 p1, const Ray& r, float& t) {
+    t = ((p0.x - r.ox) * p1.x + (p0.y - r.oy) * p1.y + (p0.z - r.oz) * p1.z) /
+        (r.dx * p1.x + r.dy * p1.y + r.dz * p1.z);
+    return t >= r.tmin && t < r.tmax;
+}
+
+// HitTest_Triangle (Utils.h:109-184), Möller–Trumbore with the reference's cull rules;
+// SHADOW swaps front/back culling (:114-127).  Cross products are written in their
+// reduced form {a, -b, c}: identical to Vector3::Cross's UnitX*a - UnitY*b + UnitZ*c
+// for finite inputs up to the sign of a zero, which no comparison below can observe.
+template <bool SHADOW>
+__device__ __forceinline__ bool tri_t(const float4 A, const float4 B, const float4 C, int cull, const Ray& r,
+                                      float& t) {
+    const float cullDot = A.w * r.dx + B.w * r.dy + C.w * r.dz;
+    if (fabsf(cullDot) < FLT_EPSILON) return false;
+    if (SHADOW) cull = (cull == RTX_CULL_FRONT) ? RTX_CULL_BACK : (cull == RTX_CULL_BACK ? RTX_CULL_FRONT : cull);
+    if (cull == RTX_CULL_FRONT && cullDot < 0) return false;
+    if (cull == RTX_CULL_BACK && cullDot > 0) return false;
+    const float hx = r.dy * C.z - r.dz * C.y;
+    const float hy = -(r.dx * C.z - r.dz * C.x);
+    const float hz = r.dx * C.y - r.dy * C.x;
+    const float a = B.x * hx + B.y * hy + B.z * hz;
+    if (fabsf(a) < FLT_EPSILON) return false;
+    const float ai = 1.f / a;
+    const float sx = r.ox - A.x, sy = r.oy - A.y, sz = r.oz - A.z;
+    const float u = ai * (sx * hx + sy * hy + sz * hz);
+    if (u < 0.f || u > 1.f) return false;
+    const float qx = sy * B.z - sz * B.y;
+    const float qy = -(sx * B.z - sz * B.x);
+    const float qz = sx * B.y - sy * B.x;
+    const float v = ai * (r.dx * qx + r.dy * qy + r.dz * qz);
+    if (v < 0.f || (u + v) > 1.f) return false;
+    t = ai * (C.x * qx + C.y * qy + C.z * qz);
+    return !(t < r.tmin || t >= r.tmax);
+}
+
+// SlabTest_BVH (Utils.h:221-243)
+__device__ __forceinline__ bool slab(const float4 mn, const float4 mx, const Ray& r) {
+    const float tx1 = (mn.x - r.ox) * r.ix, tx2 = (mx.x - r.ox) * r.ix;
+    float tMin = smin(tx1, tx2), tMax = smax(tx1, tx2);
+    const float ty1 = (mn.y - r.oy) * r.iy, ty2 = (mx.y - r.oy) * r.iy;
+    tMin = smax(tMin, smin(ty1, ty2));
+    tMax = smin(tMax, smax(ty1, ty2));
+    const float tz1 = (mn.z - r.oz) * r.iz, tz2 = (mx.z - r.oz) * r.iz;
+    tMin = smax(tMin, smin(tz1, tz2));
+    tMax = smin(tMax, smax(tz1, tz2));
+    return tMax > 0 && tMax >= tMin;
+}
+
+struct Counts {
+    uint32_t c[kNumCounters];
+};
+
+// Closest-hit packet traversal of one mesh.  `sc_t` is the reference's shared scratch
+// HitRecord t (Scene.cpp:31, Utils.h:270-273): a triangle replaces it iff t < sc_t.
+template <bool COUNT>
+__device__ void mesh_closest(const DevScene& S, const int4 M, const Ray& r, unsigned long long mask, uint32_t lane,
+                             uint32_t* sN, unsigned long long* sM, float& sc_t, uint32_t& sc_tri, Counts& cnt) {
+    if (M.y == 0 || mask == 0) return;
+    int sp = 0;
+    uint32_t node = static_cast<uint32_t>(M.x);
+    unsigned long long m = mask;
+    for (;;) {
+        const float4 b0 = S.nodes[2 * node], b1 = S.nodes[2 * node + 1];
+        const bool in = (m >> lane) & 1ull;
+        if (COUNT && in) cnt.c[kSlab]++;
+        const bool pass = in && slab(b0, b1, r);
+        const unsigned long long pm = ballot(pass);
+        if (pm) {
+            const uint32_t link = __float_as_uint(b0.w);
+            const uint32_t ntri = __float_as_uint(b1.w);
+            if (ntri) {
+                for (uint32_t k = 0; k < ntri; ++k) {
+                    const uint32_t ti = link + k;
+                    const float4 A = S.tris[3 * ti], B = S.tris[3 * ti + 1], C = S.tris[3 * ti + 2];
+                    if (pass) {
+                        if (COUNT) cnt.c[kTri]++;
+                        float t;
+                        if (tri_t<false>(A, B, C, M.z, r, t) && t < sc_t) { sc_t = t; sc_tri = ti; }
+                    }
+                }
+            } else {
+                sN[sp] = link + 1;   // right child after the whole left subtree
+                sM[sp] = pm;
+                ++sp;
+                node = link;
+                m = pm;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        node = uni(sN[sp]);
+        m = uni64(sM[sp]);
+    }
+}
+
+// Any-hit packet traversal (shadow rays, Scene::DoesHit → HitTest_TriangleMesh with
+// ignoreHitRecord).  Lanes leave at their first occluder; the wave leaves when all did.
+template <bool COUNT>
+__device__ void mesh_any(const DevScene& S, const int4 M, const Ray& r, unsigned long long mask, uint32_t lane,
+                         uint32_t* sN, unsigned long long* sM, bool& occ, Counts& cnt) {
+    if (M.y == 0) return;
+    unsigned long long m = mask & ballot(!occ);
+    if (m == 0) return;
+    int sp = 0;
+    uint32_t node = static_cast<uint32_t>(M.x);
+    for (;;) {
+        m &= ballot(!occ);
+        if (m) {
+            const float4 b0 = S.nodes[2 * node], b1 = S.nodes[2 * node + 1];
+            const bool in = (m >> lane) & 1ull;
+            if (COUNT && in) cnt.c[kSlab]++;
+            const bool pass = in && slab(b0, b1, r);
+            const unsigned long long pm = ballot(pass);
+            if (pm) {
+                const uint32_t link = __float_as_uint(b0.w);
+                const uint32_t ntri = __float_as_uint(b1.w);
+                if (ntri) {
+                    for (uint32_t k = 0; k < ntri; ++k) {
+                        const uint32_t ti = link + k;
+                        const float4 A = S.tris[3 * ti], B = S.tris[3 * ti + 1], C = S.tris[3 * ti + 2];
+                        if (pass && !occ) {
+                            if (COUNT) cnt.c[kTri]++;
+                            float t;
+                            if (tri_t<true>(A, B, C, M.z, r, t)) occ = true;
+                        }
+                    }
+                    if ((ballot(!occ) & mask) == 0) break;
+                } else {
+                    sN[sp] = link + 1;
+                    sM[sp] = pm;
+                    ++sp;
+                    node = link;
+                    m = pm;
+                    continue;
+                }
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        node = uni(sN[sp]);
+        m = uni64(sM[sp]);
+    }
+}
+
+struct RGB {
+    float r, g, b;
+};
+
+// Material::Shade (Material.h:41-123) via BRDFs.h; m2.yzw holds (rgb*kd)/PI computed on
+// the host with the same binary32 operations (BRDF::Lambert, BRDFs.h:14-17).
+__device__ __forceinline__ RGB shade(const DevScene& S, uint32_t mi, float nx, float ny, float nz, float lx, float ly,
+                                     float lz, float vx, float vy, float vz, Counts& cnt, bool count) {
+    const float4 m0 = S.materials[3 * mi], m1 = S.materials[3 * mi + 1], m2 = S.materials[3 * mi + 2];
+    const int kind = __float_as_int(m0.x);
+    RGB c{0.f, 0.f, 0.f};
+    if (kind == RTX_MAT_SOLID_COLOR) {
+        c = {m0.y, m0.z, m0.w};
+    } else if (kind == RTX_MAT_LAMBERT) {
+        if (count) cnt.c[kShadeLambert]++;
+        c = {m2.y, m2.z, m2.w};
+    } else if (kind == RTX_MAT_LAMBERT_PHONG) {
+        if (count) { cnt.c[kShadeLambert]++; cnt.c[kShadePhong]++; }
+        // BRDF::Phong (BRDFs.h:33-40)
+        const float s2 = 2.f * smax(nx * lx + ny * ly + nz * lz, 0.f);
+        const float rx = lx - nx * s2, ry = ly - ny * s2, rz = lz - nz * s2;
+        const float cosa = smax(rx * vx + ry * vy + rz * vz, 0.f);
+        const float spec = m1.y * powf(cosa, m1.z);
+        c = {m2.y + spec, m2.z + spec, m2.w + spec};
+    } else if (kind == RTX_MAT_COOK_TORRANCE) {
+        if (count) cnt.c[kShadeCT]++;
+        float hx = vx + lx, hy = vy + ly, hz = vz + lz;
+        const float hm = sqrtf(hx * hx + hy * hy + hz * hz);
+        hx = hx / hm; hy = hy / hm; hz = hz / hm;
+        const bool dielectric = (m1.w == 0.f);
+        const float f0r = dielectric ? 0.04f : m0.y, f0g = dielectric ? 0.04f : m0.z, f0b = dielectric ? 0.04f : m0.w;
+        const float p = powf(1.f - smax(hx * vx + hy * vy + hz * vz, 0.f), 5.f);
+        const float Fr = f0r + ((1.f - f0r) * p), Fg = f0g + ((1.f - f0g) * p), Fb = f0b + ((1.f - f0b) * p);
+        const float rough = m2.x;
+        const float a = rough * rough;
+        const float sqrA = a * a;
+        const float ndh = smax(nx * hx + ny * hy + nz * hz, 0.f);
+        const float in = (ndh * ndh) * ((a * a) - 1.f) + 1.f;
+        const float D = sqrA / (RTX_PI * (in * in));
+        const float k = ((a + 1.f) * (a + 1.f)) / 8.f;
+        const float cv = smax(nx * vx + ny * vy + nz * vz, 0.f);
+        const float cl = smax(nx * lx + ny * ly + nz * lz, 0.f);
+        const float G = (cv / ((cv * (1.f - k)) + k)) * (cl / ((cl * (1.f - k)) + k));
+        const float den = (4.f * smax(vx * nx + vy * ny + vz * nz, 0.0001f)) * smax(lx * nx + ly * ny + lz * nz, 0.0001f);
+        const float kr = dielectric ? 1.f - Fr : 0.f, kg = dielectric ? 1.f - Fg : 0.f, kb = dielectric ? 1.f - Fb : 0.f;
+        c.r = (m0.y * kr) / RTX_PI + ((Fr * D) * G) / den;
+        c.g = (m0.z * kg) / RTX_PI + ((Fg * D) * G) / den;
+        c.b = (m0.w * kb) / RTX_PI + ((Fb * D) * G) / den;
+    }
+    return c;
+}
+
+__device__ __forceinline__ uint32_t q8(float c) {
+    // static_cast<uint8_t>(c * 255) as x86 compiles it: cvttss2si then the low byte
+    // (NaN and out-of-int32-range values give 0x80000000 -> 0).
+    const float x = c * 255;
+    if (!(x > -2147483648.f && x < 2147483648.f)) return 0u;
+    return static_cast<uint32_t>(static_cast<int32_t>(x)) & 0xffu;
+}
+
+}  // namespace
+
+// Renderer::RenderPixel (source/Renderer.cpp:100-182) for a 16x16 tile per workgroup.
+template <bool COUNT>
+__global__ void __launch_bounds__(kBlockThreads) rtx_render_kernel(const DevScene S, const FrameArgs F) {
+    __shared__ uint32_t stkN[kBlockThreads / 64][kStackDepth];
+    __shared__ unsigned long long stkM[kBlockThreads / 64][kStackDepth];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t* sN = stkN[wave];
+    unsigned long long* sM = stkM[wave];
+
+    const uint32_t view = blockIdx.z;
+    const ViewCam& V = F.cam[view];
+    uint32_t gy = blockIdx.y;
+    if (F.groups_per_stripe) {
+        // view v owns the stripes s with s % step == (first - v) mod step (rtx.h)
+        const uint32_t first = (F.stripe_first + F.stripe_step - view % F.stripe_step) % F.stripe_step;
+        const uint32_t k = gy / F.groups_per_stripe, sub = gy % F.groups_per_stripe;
+        gy = (first + k * F.stripe_step) * F.groups_per_stripe + sub;
+    }
+    const int px = static_cast<int>(blockIdx.x * kTile + (wave & 1u) * 8u + (lane & 7u));
+    const int py = static_cast<int>(gy * kTile + (wave >> 1) * 8u + (lane >> 3));
+    const bool valid = px < static_cast<int>(F.width) && py < static_cast<int>(F.height);
+    Counts cnt;
+    if (COUNT) for (int k = 0; k < kNumCounters; ++k) cnt.c[k] = 0;
+    if (COUNT && valid) cnt.c[kPixels] = 1;
+
+    // ---- primary ray (Renderer.cpp:104-114; Matrix::TransformVector Matrix.cpp:35-42)
+    const int W = static_cast<int>(F.width), H = static_cast<int>(F.height);
+    const float cx = (2.f * ((px + 0.5f) / W) - 1) * F.aspect * V.fov;
+    const float cy = (1.f - (2.f * (py + 0.5f) / H)) * V.fov;
+    float dx = V.right[0] * cx + V.up[0] * cy + V.forward[0] * 1.f;
+    float dy = V.right[1] * cx + V.up[1] * cy + V.forward[1] * 1.f;
+    float dz = V.right[2] * cx + V.up[2] * cy + V.forward[2] * 1.f;
+    const float dm = sqrtf(dx * dx + dy * dy + dz * dz);
+    dx /= dm; dy /= dm; dz /= dm;
+    const Ray vr = make_ray(V.origin[0], V.origin[1], V.origin[2], dx, dy, dz, 0.0001f, FLT_MAX);
+    const unsigned long long active = ballot(valid);
+
+    // ---- Scene::GetClosestHit (Scene.cpp:29-66)
+    float best_t = FLT_MAX, sc_t = FLT_MAX;
+    uint32_t best_kind = 0, best_idx = 0;   // kind: 0 none, 1 sphere, 2 plane, 3 triangle
+    for (uint32_t i = 0; i < S.n_spheres; ++i) {
+        const float4 s = S.spheres[i];
+        if (valid) {
+            if (COUNT) cnt.c[kSphere]++;
+            float t;
+            if (sphere_t(s, vr, t)) {
+                sc_t = t;
+                if (t < best_t) { best_t = t; best_kind = 1; best_idx = i; }
+            }
+        }
+    }
+    for (uint32_t i = 0; i < S.n_planes; ++i) {
+        const float4 p0 = S.planes[2 * i], p1 = S.planes[2 * i + 1];
+        if (valid) {
+            if (COUNT) cnt.c[kPlane]++;
+            float t;
+            if (plane_t(p0, p1, vr, t)) {
+                sc_t = t;
+                if (t < best_t) { best_t = t; best_kind = 2; best_idx = i; }
+            }
+        }
+    }
+    for (uint32_t mi = 0; mi < S.n_meshes; ++mi) {
+        const int4 M = S.meshes[mi];
+        uint32_t sc_tri = 0;
+        mesh_closest<COUNT>(S, M, vr, active, lane, sN, sM, sc_t, sc_tri, cnt);
+        if (sc_t < best_t) { best_t = sc_t; best_kind = 3; best_idx = sc_tri; }
+    }
+
+    // ---- hit record (rebuilt from t: ray.origin + t * ray.direction, Utils.h:62-64)
+    const bool did = best_kind != 0;
+    float hx = 0.f, hy = 0.f, hz = 0.f, nx = 0.f, ny = 0.f, nz = 0.f;
+    uint32_t mat = 0;
+    if (did) {
+        hx = vr.ox + vr.dx * best_t; hy = vr.oy + vr.dy * best_t; hz = vr.oz + vr.dz * best_t;
+        if (best_kind == 1) {
+            const float4 s = S.spheres[best_idx];
+            nx = hx - s.x; ny = hy - s.y; nz = hz - s.z;
+            const float m = sqrtf(nx * nx + ny * ny + nz * nz);   // closestHit.normal.Normalize()
+            nx /= m; ny /= m; nz /= m;
+            mat = S.sphere_mat[best_idx];
+        } else if (best_kind == 2) {
+            const float4 p0 = S.planes[2 * best_idx], p1 = S.planes[2 * best_idx + 1];
+            nx = p1.x; ny = p1.y; nz = p1.z;
+            mat = __float_as_uint(p0.w);
+        } else {
+            const float4 A = S.tris[3 * best_idx], B = S.tris[3 * best_idx + 1], C = S.tris[3 * best_idx + 2];
+            nx = A.w; ny = B.w; nz = C.w;
+            mat = S.tri_mat[best_idx];
+        }
+    }
+    if (COUNT && did) cnt.c[kHit]++;
+
+    float shadowFactor = 1.f;
+    float fr = 0.f, fg = 0.f, fb = 0.f;
+    const unsigned long long hitmask = ballot(did);
+    if (hitmask) {
+        // originOffset = hit.origin + hit.normal * 0.0001f (Renderer.cpp:126)
+        const float oox = hx + nx * 0.0001f, ooy = hy + ny * 0.0001f, ooz = hz + nz * 0.0001f;
+        const float vx = -dx, vy = -dy, vz = -dz;
+        for (uint32_t li = 0; li < S.n_lights; ++li) {
+            const float4 L0 = S.lights[2 * li], L1 = S.lights[2 * li + 1];
+            const int ltype = __float_as_int(L0.w);
+            const bool known = (ltype == RTX_LIGHT_POINT || ltype == RTX_LIGHT_DIRECTIONAL);
+            float lx = known ? L0.x - oox : 0.f, ly = known ? L0.y - ooy : 0.f, lz = known ? L0.z - ooz : 0.f;
+            const float mag = sqrtf(lx * lx + ly * ly + lz * lz);
+            lx /= mag; ly /= mag; lz /= mag;
+            bool occ = false;
+            if (F.shadows) {
+                // Scene::DoesHit (Scene.cpp:68-96) on Ray{originOffset, l, 1e-4, |l|}
+                const Ray sr = make_ray(oox, ooy, ooz, lx, ly, lz, 0.0001f, mag);
+                if (COUNT && did) cnt.c[kShadow]++;
+                for (uint32_t i = 0; i < S.n_spheres; ++i) {
+                    if ((ballot(did && !occ)) == 0) break;
+                    const float4 s = S.spheres[i];
+                    if (did && !occ) {
+                        if (COUNT) cnt.c[kSphere]++;
+                        float t;
+                        occ = sphere_t(s, sr, t);
+                    }
+                }
+                for (uint32_t i = 0; i < S.n_planes; ++i) {
+                    if ((ballot(did && !occ)) == 0) break;
+                    const float4 p0 = S.planes[2 * i], p1 = S.planes[2 * i + 1];
+                    if (did && !occ) {
+                        if (COUNT) cnt.c[kPlane]++;
+                        float t;
+                        occ = plane_t(p0, p1, sr, t);
+                    }
+                }
+                for (uint32_t mi = 0; mi < S.n_meshes; ++mi) {
+                    const unsigned long long live = ballot(did && !occ);
+                    if (live == 0) break;
+                    mesh_any<COUNT>(S, S.meshes[mi], sr, live, lane, sN, sM, occ, cnt);
+                }
+            }
+            if (!did) continue;
+            if (occ) {
+                if (COUNT) cnt.c[kOccluded]++;
+                shadowFactor *= 0.95f;
+                continue;
+            }
+            if (COUNT) cnt.c[kShadeBase]++;
+            if (F.mode == RTX_MODE_COMBINED || F.mode == RTX_MODE_RADIANCE) {
+                // LightUtils::GetRadiance (Utils.h:355-369) at hit.origin
+                float s = 0.f;
+                bool any = true;
+                if (ltype == RTX_LIGHT_POINT) {
+                    const float ex = L0.x - hx, ey = L0.y - hy, ez = L0.z - hz;
+                    s = L1.w / (ex * ex + ey * ey + ez * ez);
+                } else if (ltype == RTX_LIGHT_DIRECTIONAL) {
+                    s = L1.w;
+                } else {
+                    any = false;
+                }
+                const float rr = any ? L1.x * s : 0.f, rg = any ? L1.y * s : 0.f, rb = any ? L1.z * s : 0.f;
+                if (F.mode == RTX_MODE_RADIANCE) {
+                    fr += rr; fg += rg; fb += rb;
+                } else {
+                    const float oa = smax(nx * lx + ny * ly + nz * lz, 0.f);
+                    const RGB br = shade(S, mat, nx, ny, nz, lx, ly, lz, vx, vy, vz, cnt, COUNT);
+                    fr += (rr * oa) * br.r; fg += (rg * oa) * br.g; fb += (rb * oa) * br.b;
+                }
+            } else if (F.mode == RTX_MODE_OBSERVED_AREA) {
+                const float oa = smax(nx * lx + ny * ly + nz * lz, 0.f);
+                fr += oa; fg += oa; fb += oa;
+            } else if (F.mode == RTX_MODE_BRDF) {
+                const RGB br = shade(S, mat, nx, ny, nz, lx, ly, lz, vx, vy, vz, cnt, COUNT);
+                fr += br.r; fg += br.g; fb += br.b;
+            }
+        }
+        if (did) { fr *= shadowFactor; fg *= shadowFactor; fb *= shadowFactor; }
+    }
+    // ColorRGB::MaxToOne (ColorRGB.h:12-17)
+    const float mv = smax(fr, smax(fg, fb));
+    if (mv > 1.f) { fr /= mv; fg /= mv; fb /= mv; }
+    if (valid) {
+        const size_t o = static_cast<size_t>(view) * F.width * F.height + static_cast<size_t>(py) * F.width +
+                         static_cast<size_t>(px);
+        F.out_px[o] = (q8(fr) << F.rshift) | (q8(fg) << F.gshift) | (q8(fb) << F.bshift) | F.amask;
+        if (F.out_rgb) {
+            F.out_rgb[3 * o] = fr; F.out_rgb[3 * o + 1] = fg; F.out_rgb[3 * o + 2] = fb;
+        }
+    }
+    if (COUNT) {
+        for (int k = 0; k < kNumCounters; ++k)
+            if (cnt.c[k]) atomicAdd(&F.counters[k], static_cast<unsigned long long>(cnt.c[k]));
+    }
+}
+
+template __global__ void rtx_render_kernel<false>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<true>(const DevScene, const FrameArgs);
+
+// ====================================================================== host side
+struct rtx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    // scene image in HBM (one allocation, 256-B aligned sections)
+    char* d_scene = nullptr;
+    size_t scene_bytes = 0;
+    DevScene dev{};
+    bool has_scene = false;
+    // frame buffer in HBM
+    uint32_t* d_px = nullptr;
+    float* d_rgb = nullptr;
+    size_t px_cap = 0, rgb_cap = 0;
+    unsigned long long* d_counters = nullptr;
+    // last render
+    rtx_render_params last{};
+    int last_views = 1;
+    bool last_valid = false, last_rgb = false;
+};
+
+namespace {
+
+int fail(rtx_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIP_TRY(ctx, call)                                                                  \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail((ctx), RTX_E_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+inline float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
+inline float bits(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+inline float bitsi(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// Deepest DFS stack a wave can need for this BVH (pending right siblings on a path).
+bool bvh_depth_ok(const rtx_mesh& m, std::string& why) {
+    std::vector<std::pair<uint32_t, int>> st{{0u, 0}};
+    int maxd = 0;
+    size_t visited = 0;
+    while (!st.empty()) {
+        auto [n, d] = st.back();
+        st.pop_back();
+        if (++visited > 4ull * m.n_nodes + 4) { why = "BVH has a cycle"; return false; }
+        maxd = d > maxd ? d : maxd;
+        const rtx_bvh_node& nd = m.nodes[n];
+        if (nd.idx_count == 0) {
+            if (nd.left_node + 1 >= m.n_nodes || nd.left_node == 0) { why = "BVH child index out of range"; return false; }
+            st.push_back({nd.left_node + 1, d + 1});
+            st.push_back({nd.left_node, d + 1});
+        }
+    }
+    if (maxd >= kStackDepth) { why = "BVH deeper than the device stack (" + std::to_string(maxd) + ")"; return false; }
+    return true;
+}
+
+}  // namespace
+
+extern "C" int rtx_abi_version(void) { return RTX_ABI_VERSION; }
+
+extern "C" int rtx_create(rtx_ctx** out, int device_id) {
+    if (!out) return RTX_E_INVALID;
+    *out = nullptr;
+    rtx_ctx* c = new (std::nothrow) rtx_ctx;
+    if (!c) return RTX_E_NOMEM;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) { delete c; return RTX_E_DEVICE; }
+    if (device_id < 0 || device_id >= n) { delete c; return RTX_E_INVALID; }
+    c->device = device_id;
+    if (hipSetDevice(device_id) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc(&c->d_counters, sizeof(unsigned long long) * kNumCounters) != hipSuccess) {
+        delete c;
+        return RTX_E_DEVICE;
+    }
+    *out = c;
+    return RTX_OK;
+}
+
+extern "C" void rtx_destroy(rtx_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->d_scene);
+    (void)hipFree(c->d_px);
+    (void)hipFree(c->d_rgb);
+    (void)hipFree(c->d_counters);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" const char* rtx_last_error(const rtx_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+extern "C" int rtx_scene_bytes(const rtx_ctx* c, uint64_t* bytes) {
+    if (!c || !bytes) return RTX_E_INVALID;
+    *bytes = c->scene_bytes;
+    return RTX_OK;
+}
+
+extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
+    if (!c || !s) return RTX_E_INVALID;
+    if ((s->n_spheres && !s->spheres) || (s->n_planes && !s->planes) || (s->n_meshes && !s->meshes) ||
+        (s->n_lights && !s->lights) || (s->n_materials && !s->materials))
+        return fail(c, RTX_E_INVALID, "null array with non-zero count");
+    if (s->n_materials == 0 || s->n_materials > 256) return fail(c, RTX_E_INVALID, "need 1..256 materials");
+    const uint32_t nm = s->n_materials;
+    std::vector<float4> sph, pl, tri, nodes, lights, mats;
+    std::vector<uint32_t> sph_mat, tri_mat;
+    std::vector<int4> meshes;
+    for (uint32_t i = 0; i < s->n_spheres; ++i) {
+        const rtx_sphere& p = s->spheres[i];
+        if (p.material >= nm) return fail(c, RTX_E_INVALID, "sphere material out of range");
+        sph.push_back(f4(p.origin[0], p.origin[1], p.origin[2], p.radius * p.radius));   // Square(radius)
+        sph_mat.push_back(p.material);
+    }
+    for (uint32_t i = 0; i < s->n_planes; ++i) {
+        const rtx_plane& p = s->planes[i];
+        if (p.material >= nm) return fail(c, RTX_E_INVALID, "plane material out of range");
+        pl.push_back(f4(p.origin[0], p.origin[1], p.origin[2], bits(p.material)));
+        pl.push_back(f4(p.normal[0], p.normal[1], p.normal[2], 0.f));
+    }
+    for (uint32_t mi = 0; mi < s->n_meshes; ++mi) {
+        const rtx_mesh& m = s->meshes[mi];
+        if (m.material >= nm) return fail(c, RTX_E_INVALID, "mesh material out of range");
+        if (m.cull_mode < RTX_CULL_FRONT || m.cull_mode > RTX_CULL_NONE) return fail(c, RTX_E_INVALID, "bad cull mode");
+        if (m.n_indices % 3) return fail(c, RTX_E_INVALID, "mesh index count not a multiple of 3");
+        const uint32_t tri0 = static_cast<uint32_t>(tri.size() / 3), node0 = static_cast<uint32_t>(nodes.size() / 2);
+        const uint32_t ntri = m.n_indices / 3;
+        if (ntri && (!m.positions || !m.indices || !m.normals)) return fail(c, RTX_E_INVALID, "mesh arrays missing");
+        for (uint32_t k = 0; k < ntri; ++k) {
+            const int32_t i0 = m.indices[3 * k], i1 = m.indices[3 * k + 1], i2 = m.indices[3 * k + 2];
+            if (i0 < 0 || i1 < 0 || i2 < 0 || static_cast<uint32_t>(i0) >= m.n_positions ||
+                static_cast<uint32_t>(i1) >= m.n_positions || static_cast<uint32_t>(i2) >= m.n_positions)
+                return fail(c, RTX_E_INVALID, "mesh index out of range");
+            const float* v0 = m.positions + 3 * i0;
+            const float* v1 = m.positions + 3 * i1;
+            const float* v2 = m.positions + 3 * i2;
+            const float* n = m.normals + 3 * k;
+            // edge1 = v1 - v0, edge2 = v2 - v0 (Utils.h:139-140), same binary32 ops as on device
+            tri.push_back(f4(v0[0], v0[1], v0[2], n[0]));
+            tri.push_back(f4(v1[0] - v0[0], v1[1] - v0[1], v1[2] - v0[2], n[1]));
+            tri.push_back(f4(v2[0] - v0[0], v2[1] - v0[1], v2[2] - v0[2], n[2]));
+            tri_mat.push_back(m.material);
+        }
+        if (m.n_nodes) {
+            if (!m.nodes) return fail(c, RTX_E_INVALID, "mesh nodes missing");
+            std::string why;
+            if (!bvh_depth_ok(m, why)) return fail(c, RTX_E_INVALID, why);
+            for (uint32_t k = 0; k < m.n_nodes; ++k) {
+                const rtx_bvh_node& nd = m.nodes[k];
+                uint32_t link, cnt;
+                if (nd.idx_count > 0) {
+                    if (nd.first_idx % 3 || nd.idx_count % 3 || nd.first_idx + nd.idx_count > m.n_indices)
+                        return fail(c, RTX_E_INVALID, "BVH leaf range invalid");
+                    link = tri0 + nd.first_idx / 3;
+                    cnt = nd.idx_count / 3;
+                } else {
+                    link = node0 + nd.left_node;
+                    cnt = 0;
+                }
+                nodes.push_back(f4(nd.min[0], nd.min[1], nd.min[2], bits(link)));
+                nodes.push_back(f4(nd.max[0], nd.max[1], nd.max[2], bits(cnt)));
+            }
+        }
+        meshes.push_back(make_int4(static_cast<int>(node0), static_cast<int>(m.n_nodes), m.cull_mode, m.material));
+    }
+    for (uint32_t i = 0; i < s->n_lights; ++i) {
+        const rtx_light& l = s->lights[i];
+        lights.push_back(f4(l.origin[0], l.origin[1], l.origin[2], bitsi(l.type)));
+        lights.push_back(f4(l.color[0], l.color[1], l.color[2], l.intensity));
+    }
+    for (uint32_t i = 0; i < nm; ++i) {
+        const rtx_material& m = s->materials[i];
+        // BRDF::Lambert(kd, cd) = (cd * kd) / PI (BRDFs.h:14-17), exact binary32 on host
+        const float lr = (m.color[0] * m.kd) / RTX_PI, lg = (m.color[1] * m.kd) / RTX_PI, lb = (m.color[2] * m.kd) / RTX_PI;
+        mats.push_back(f4(bitsi(m.kind), m.color[0], m.color[1], m.color[2]));
+        mats.push_back(f4(m.kd, m.ks, m.exponent, m.metalness));
+        mats.push_back(f4(m.roughness, lr, lg, lb));
+    }
+
+    struct Sec { const void* p; size_t n; size_t off; };
+    Sec secs[] = {{sph.data(), sph.size() * 16, 0},       {sph_mat.data(), sph_mat.size() * 4, 0},
+                  {pl.data(), pl.size() * 16, 0},         {tri.data(), tri.size() * 16, 0},
+                  {tri_mat.data(), tri_mat.size() * 4, 0}, {nodes.data(), nodes.size() * 16, 0},
+                  {meshes.data(), meshes.size() * 16, 0}, {lights.data(), lights.size() * 16, 0},
+                  {mats.data(), mats.size() * 16, 0}};
+    size_t total = 0;
+    for (auto& x : secs) { x.off = total; total += align256(x.n ? x.n : 16); }
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (total > c->scene_bytes || !c->d_scene) {
+        (void)hipFree(c->d_scene);
+        c->d_scene = nullptr;
+        c->scene_bytes = 0;
+        HIP_TRY(c, hipMalloc(&c->d_scene, total));
+    }
+    c->scene_bytes = total;
+    for (auto& x : secs)
+        if (x.n) HIP_TRY(c, hipMemcpyAsync(c->d_scene + x.off, x.p, x.n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    DevScene d{};
+    d.spheres = reinterpret_cast<const float4*>(c->d_scene + secs[0].off);
+    d.sphere_mat = reinterpret_cast<const uint32_t*>(c->d_scene + secs[1].off);
+    d.planes = reinterpret_cast<const float4*>(c->d_scene + secs[2].off);
+    d.tris = reinterpret_cast<const float4*>(c->d_scene + secs[3].off);
+    d.tri_mat = reinterpret_cast<const uint32_t*>(c->d_scene + secs[4].off);
+    d.nodes = reinterpret_cast<const float4*>(c->d_scene + secs[5].off);
+    d.meshes = reinterpret_cast<const int4*>(c->d_scene + secs[6].off);
+    d.lights = reinterpret_cast<const float4*>(c->d_scene + secs[7].off);
+    d.materials = reinterpret_cast<const float4*>(c->d_scene + secs[8].off);
+    d.n_spheres = s->n_spheres; d.n_planes = s->n_planes; d.n_meshes = s->n_meshes;
+    d.n_lights = s->n_lights; d.n_materials = nm;
+    d.n_tris = static_cast<uint32_t>(tri.size() / 3); d.n_nodes = static_cast<uint32_t>(nodes.size() / 2);
+    c->dev = d;
+    c->has_scene = true;
+    return RTX_OK;
+}
+
+namespace {
+
+int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_params* p, bool want_rgb, FrameArgs& F,
+            dim3& grid) {
+    if (!c || !cams || !p) return RTX_E_INVALID;
+    if (n_views < 1 || n_views > kMaxViews) return fail(c, RTX_E_INVALID, "n_views must be 1..8");
+    if (!c->has_scene) return fail(c, RTX_E_STATE, "no scene uploaded");
+    if (p->width == 0 || p->height == 0 || p->width > 65536 || p->height > 65536)
+        return fail(c, RTX_E_INVALID, "bad image size");
+    if (p->lighting_mode < 0 || p->lighting_mode >= RTX_MODE_COUNT) return fail(c, RTX_E_INVALID, "bad lighting mode");
+    if (p->format.rshift > 24 || p->format.gshift > 24 || p->format.bshift > 24)
+        return fail(c, RTX_E_INVALID, "bad pixel format");
+    const bool striped = p->stripe_rows != 0 && p->stripe_step > 1;
+    if (striped && (p->stripe_rows % kTile != 0 || p->stripe_first >= p->stripe_step))
+        return fail(c, RTX_E_INVALID, "stripe_rows must be a multiple of 16 and stripe_first < stripe_step");
+    const size_t npx = static_cast<size_t>(p->width) * p->height * static_cast<size_t>(n_views);
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (npx > c->px_cap) {
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_px);
+        c->d_px = nullptr;
+        c->px_cap = 0;
+        HIP_TRY(c, hipMalloc(&c->d_px, npx * 4));
+        c->px_cap = npx;
+    }
+    if (want_rgb && npx > c->rgb_cap) {
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_rgb);
+        c->d_rgb = nullptr;
+        c->rgb_cap = 0;
+        HIP_TRY(c, hipMalloc(&c->d_rgb, npx * 12));
+        c->rgb_cap = npx;
+    }
+    std::memset(&F, 0, sizeof F);
+    for (int v = 0; v < n_views; ++v) {
+        for (int k = 0; k < 3; ++k) {
+            F.cam[v].origin[k] = cams[v].origin[k]; F.cam[v].right[k] = cams[v].right[k];
+            F.cam[v].up[k] = cams[v].up[k]; F.cam[v].forward[k] = cams[v].forward[k];
+        }
+        F.cam[v].fov = cams[v].fov;
+    }
+    F.aspect = static_cast<int>(p->width) / static_cast<float>(static_cast<int>(p->height));  // Renderer.cpp:30
+    F.width = p->width; F.height = p->height;
+    F.mode = p->lighting_mode; F.shadows = p->shadows_enabled ? 1 : 0;
+    F.rshift = p->format.rshift; F.gshift = p->format.gshift; F.bshift = p->format.bshift; F.amask = p->format.amask;
+    const uint32_t groups = (p->height + kTile - 1) / kTile;
+    uint32_t gy = groups;
+    if (striped) {
+        // every view owns the same number of stripes only if the stripe count divides
+        // evenly; size the grid for the largest owner and let the kernel skip the rest
+        const uint32_t gps = p->stripe_rows / kTile;
+        const uint32_t nstripes = (groups + gps - 1) / gps;
+        const uint32_t owned = (nstripes + p->stripe_step - 1) / p->stripe_step;
+        F.groups_per_stripe = gps; F.stripe_first = p->stripe_first; F.stripe_step = p->stripe_step;
+        gy = owned * gps;
+    }
+    F.tiles_x = (p->width + kTile - 1) / kTile;
+    F.out_px = c->d_px;
+    F.out_rgb = want_rgb ? c->d_rgb : nullptr;
+    F.counters = c->d_counters;
+    grid = dim3(F.tiles_x, gy, static_cast<uint32_t>(n_views));
+    return RTX_OK;
+}
+
+int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
+    if (grid.x == 0 || grid.y == 0) return RTX_OK;
+    if (count)
+        hipLaunchKernelGGL(rtx_render_kernel<true>, grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
+    else
+        hipLaunchKernelGGL(rtx_render_kernel<false>, grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
+    HIP_TRY(c, hipGetLastError());
+    return RTX_OK;
+}
+
+void remember(rtx_ctx* c, const rtx_render_params* p, int n_views, bool rgb) {
+    c->last = *p;
+    c->last_views = n_views;
+    c->last_valid = true;
+    c->last_rgb = rgb;
+}
+
+}  // namespace
+
+extern "C" int rtx_render_views_async(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_params* p,
+                                      int want_rgb) {
+    FrameArgs F;
+    dim3 grid;
+    int rc = prepare(c, cams, n_views, p, want_rgb != 0, F, grid);
+    if (rc != RTX_OK) return rc;
+    rc = launch(c, F, grid, false);
+    if (rc != RTX_OK) return rc;
+    remember(c, p, n_views, want_rgb != 0);
+    return RTX_OK;
+}
+
+extern "C" int rtx_render_async(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, int want_rgb) {
+    return rtx_render_views_async(c, cam, 1, p, want_rgb);
+}
+
+extern "C" int rtx_synchronize(rtx_ctx* c) {
+    if (!c) return RTX_E_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return RTX_OK;
+}
+
+extern "C" int rtx_download(rtx_ctx* c, uint32_t* out_px, float* out_rgb) {
+    if (!c || !out_px) return RTX_E_INVALID;
+    if (!c->last_valid) return fail(c, RTX_E_STATE, "nothing rendered yet");
+    if (out_rgb && !c->last_rgb) return fail(c, RTX_E_STATE, "last render did not produce colours");
+    const rtx_render_params& p = c->last;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t W = p.width, H = p.height;
+    const bool striped = p.stripe_rows != 0 && p.stripe_step > 1;
+    const uint32_t rows_per = striped ? p.stripe_rows : static_cast<uint32_t>(H);
+    const uint32_t step = striped ? p.stripe_step : 1;
+    for (int v = 0; v < c->last_views; ++v) {
+        const uint32_t first = striped ? (p.stripe_first + step - static_cast<uint32_t>(v) % step) % step : 0;
+        const size_t base = static_cast<size_t>(v) * W * H;
+        for (size_t s = first; s * rows_per < H; s += step) {
+            const size_t r0 = s * rows_per, r1 = (r0 + rows_per < H) ? r0 + rows_per : H;
+            HIP_TRY(c, hipMemcpyAsync(out_px + base + r0 * W, c->d_px + base + r0 * W, (r1 - r0) * W * 4,
+                                      hipMemcpyDeviceToHost, c->stream));
+            if (out_rgb)
+                HIP_TRY(c, hipMemcpyAsync(out_rgb + 3 * (base + r0 * W), c->d_rgb + 3 * (base + r0 * W),
+                                          (r1 - r0) * W * 12, hipMemcpyDeviceToHost, c->stream));
+        }
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return RTX_OK;
+}
+
+extern "C" int rtx_render(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint32_t* out_px,
+                          float* out_rgb) {
+    if (!out_px) return RTX_E_INVALID;
+    int rc = rtx_render_async(c, cam, p, out_rgb != nullptr);
+    if (rc != RTX_OK) return rc;
+    return rtx_download(c, out_px, out_rgb);
+}
+
+extern "C" int rtx_device_buffers(rtx_ctx* c, void** d_px, void** d_rgb) {
+    if (!c) return RTX_E_INVALID;
+    if (d_px) *d_px = c->d_px;
+    if (d_rgb) *d_rgb = c->d_rgb;
+    return RTX_OK;
+}
+
+extern "C" int rtx_time_views(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_params* p, int iters,
+                              float* mean_ms) {
+    if (!mean_ms || iters <= 0) return RTX_E_INVALID;
+    FrameArgs F;
+    dim3 grid;
+    int rc = prepare(c, cams, n_views, p, false, F, grid);
+    if (rc != RTX_OK) return rc;
+    HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
+    for (int i = 0; i < iters; ++i) {
+        rc = launch(c, F, grid, false);
+        if (rc != RTX_OK) return rc;
+    }
+    HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
+    HIP_TRY(c, hipEventSynchronize(c->ev1));
+    float ms = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    *mean_ms = ms / static_cast<float>(iters);
+    remember(c, p, n_views, false);
+    return RTX_OK;
+}
+
+extern "C" int rtx_time_frames(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, int iters,
+                               float* mean_ms) {
+    return rtx_time_views(c, cam, 1, p, iters, mean_ms);
+}
+
+// Instrumented variant: the same traversal with per-lane work counters.
+extern "C" int rtx_count_work(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* counts) {
+    if (!counts) return RTX_E_INVALID;
+    FrameArgs F;
+    dim3 grid;
+    int rc = prepare(c, cam, 1, p, false, F, grid);
+    if (rc != RTX_OK) return rc;
+    HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long) * kNumCounters, c->stream));
+    rc = launch(c, F, grid, true);
+    if (rc != RTX_OK) return rc;
+    HIP_TRY(c, hipMemcpyAsync(counts, c->d_counters, sizeof(unsigned long long) * kNumCounters,
+                              hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    remember(c, p, 1, false);
+    return RTX_OK;
+}

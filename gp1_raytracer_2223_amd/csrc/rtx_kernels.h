@@ -1,0 +1,67 @@
+// rtx_kernels.h — device layout of the uploaded scene and the per-frame launch record.
+// Shared by the kernels and the host-side upload code in rtx_hip.hip.
+#pragma once
+#include <stdint.h>
+
+namespace rtxd {
+
+// Per-wave DFS stack entries in LDS (node index + 64-bit lane mask).  The host checks
+// every uploaded BVH's depth against this before accepting the scene.
+constexpr int kStackDepth = 64;
+constexpr int kBlockThreads = 256;     // 4 waves = a 16 x 16 pixel tile (8 x 8 per wave)
+constexpr int kTile = 16;
+
+// Work counters (SURVEY §8(d) cost model; same order as the oracle's).
+enum Counter {
+    kPixels = 0, kSphere, kPlane, kSlab, kTri, kHit, kShadow, kOccluded,
+    kShadeBase, kShadeLambert, kShadePhong, kShadeCT, kNumCounters
+};
+
+// HBM scene image, every record 16-byte aligned so a wave-uniform index
+// becomes one s_load_dwordx4/x8 (scalar cache) instead of 64 vector loads:
+//   sphere   1 x float4 {cx, cy, cz, r*r}          + mat u32
+//   plane    2 x float4 {ox, oy, oz, mat}, {nx, ny, nz, 0}
+//   triangle 3 x float4 {v0, n.x}, {v1-v0, n.y}, {v2-v0, n.z}  (BVH leaf order, all meshes)
+//   node     2 x float4 {min, link}, {max, tri_count}  link = first tri (leaf) | left node
+//   mesh     int4 {first node, n nodes, cull, mat}
+//   light    2 x float4 {origin, type}, {color, intensity}
+//   material 3 x float4 {kind, rgb}, {kd, ks, exp, metal}, {rough, (rgb*kd)/PI}
+struct DevScene {
+    const float4* __restrict__ spheres;
+    const uint32_t* __restrict__ sphere_mat;
+    const float4* __restrict__ planes;
+    const float4* __restrict__ tris;
+    const uint32_t* __restrict__ tri_mat;     // material of the owning mesh, per triangle
+    const float4* __restrict__ nodes;
+    const int4* __restrict__ meshes;
+    const float4* __restrict__ lights;
+    const float4* __restrict__ materials;
+    uint32_t n_spheres, n_planes, n_meshes, n_lights, n_materials, n_tris, n_nodes, _pad;
+};
+
+constexpr int kMaxViews = 8;   // views (camera positions) rendered by one launch
+
+struct ViewCam {
+    float origin[3];
+    float right[3];
+    float up[3];
+    float forward[3];
+    float fov;
+    float _pad[3];
+};
+
+struct FrameArgs {
+    ViewCam cam[kMaxViews];       // blockIdx.z selects the view
+    float aspect;                 // (float)W / (float)H  (Renderer.cpp:30)
+    uint32_t width, height;
+    int32_t mode, shadows;
+    uint32_t rshift, gshift, bshift, amask;
+    uint32_t groups_per_stripe;   // stripe_rows / 16 (0 => whole image)
+    uint32_t stripe_first, stripe_step;
+    uint32_t tiles_x;
+    uint32_t* __restrict__ out_px;   // view v at out_px + v * width * height
+    float* __restrict__ out_rgb;     // may be null
+    unsigned long long* __restrict__ counters;  // COUNT variant only
+};
+
+}  // namespace rtxd

@@ -1,0 +1,136 @@
+"""Python mirror of dae::Renderer (source/Renderer.h:17-61) over the HIP C-ABI.
+
+    r = Renderer(1920, 1080)            # Renderer(SDL_Window*): width/height of the surface
+    r.Render(scene)                     # Renderer::Render(Scene*) -> fills r.buffer (uint32 XRGB)
+    r.CycleLightingMode(); r.ToggleShadows(); r.SaveBufferToImage("out.bmp")
+
+Multi-GPU: `Renderer(..., device=rank, stripe=(16, rank, world))` renders only the
+16-row stripes this rank owns (rows of stripe s with s % world == rank); stitching the
+ranks' buffers gives the single-GPU image bit for bit.
+
+There is no CPU fallback: if librtx_hip.so or the GPU is missing this raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import struct
+
+import numpy as np
+
+from . import abi
+from .scene import HostScene
+
+
+class LightingMode:
+    ObservedArea, Radiance, BRDF, Combined, Count = 0, 1, 2, 3, 4
+
+
+class DeviceContext:
+    """Owns one rtx_ctx (one GPU) and its uploaded scene."""
+
+    def __init__(self, device: int = 0):
+        self.lib = abi.load_hip()
+        h = C.c_void_p()
+        rc = self.lib.rtx_create(C.byref(h), int(device))
+        if rc != abi.RTX_OK:
+            raise RuntimeError(f"rtx_create(device={device}) failed with code {rc} (no usable HIP device?)")
+        self.h = h
+        self.device = device
+        self._uploaded = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.rtx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, scene: abi.Scene) -> None:
+        abi.check(self.lib.rtx_upload_scene(self.h, C.byref(scene)), "rtx_upload_scene", self.h)
+
+    def render(self, cam: abi.Camera, params: abi.RenderParams, want_rgb: bool = True):
+        n = params.width * params.height
+        px = np.zeros(n, np.uint32)
+        rgb = np.zeros(3 * n, np.float32) if want_rgb else None
+        rc = self.lib.rtx_render(self.h, C.byref(cam), C.byref(params),
+                                 px.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                 rgb.ctypes.data_as(C.POINTER(C.c_float)) if want_rgb else None)
+        abi.check(rc, "rtx_render", self.h)
+        return px, rgb
+
+    def render_async(self, cam, params, want_rgb=False):
+        abi.check(self.lib.rtx_render_async(self.h, C.byref(cam), C.byref(params), int(want_rgb)),
+                  "rtx_render_async", self.h)
+
+    def synchronize(self):
+        abi.check(self.lib.rtx_synchronize(self.h), "rtx_synchronize", self.h)
+
+    def time_frames(self, cam, params, iters: int) -> float:
+        ms = C.c_float()
+        abi.check(self.lib.rtx_time_frames(self.h, C.byref(cam), C.byref(params), int(iters), C.byref(ms)),
+                  "rtx_time_frames", self.h)
+        return ms.value
+
+    def count_work(self, cam, params) -> np.ndarray:
+        out = (C.c_uint64 * 12)()
+        abi.check(self.lib.rtx_count_work(self.h, C.byref(cam), C.byref(params), out), "rtx_count_work", self.h)
+        return np.array(list(out), dtype=np.uint64)
+
+
+class Renderer:
+    def __init__(self, width: int, height: int, device: int = 0, stripe: tuple[int, int, int] | None = None,
+                 pixel_format=abi.XRGB8888):
+        self.m_Width, self.m_Height = int(width), int(height)
+        self.m_AspectRatio = self.m_Width / float(self.m_Height)
+        self.m_CurrentLightingMode = LightingMode.Combined
+        self.m_ShadowsEnabled = True
+        self.stripe = stripe
+        self.format = pixel_format
+        self.ctx = DeviceContext(device)
+        self._scene_key = None
+        self.buffer = np.zeros(self.m_Width * self.m_Height, np.uint32)
+        self.rgb = None
+
+    def params(self) -> abi.RenderParams:
+        sr, first, step = self.stripe if self.stripe else (0, 0, 1)
+        return abi.make_params(self.m_Width, self.m_Height, self.m_CurrentLightingMode, self.m_ShadowsEnabled,
+                               self.format, sr, first, step)
+
+    def Render(self, scene: HostScene, upload: bool = True, want_rgb: bool = False) -> np.ndarray:
+        """Renderer::Render (Renderer.cpp:34-98): blocking; fills self.buffer."""
+        s, cam = scene.view()
+        if upload or self._scene_key is not id(scene):
+            self.ctx.upload(s)
+            self._scene_key = id(scene)
+        n = self.m_Width * self.m_Height
+        rgb = np.zeros(3 * n, np.float32) if want_rgb else None
+        rc = self.ctx.lib.rtx_render(self.ctx.h, C.byref(cam), C.byref(self.params()),
+                                     self.buffer.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                     rgb.ctypes.data_as(C.POINTER(C.c_float)) if want_rgb else None)
+        abi.check(rc, "rtx_render", self.ctx.h)
+        self.rgb = rgb
+        return self.buffer
+
+    def CycleLightingMode(self) -> None:   # Renderer.cpp:189-193
+        self.m_CurrentLightingMode = (self.m_CurrentLightingMode + 1) % LightingMode.Count
+
+    def ToggleShadows(self) -> None:       # Renderer.h:34-36
+        self.m_ShadowsEnabled = not self.m_ShadowsEnabled
+
+    def SaveBufferToImage(self, path: str = "RayTracing_Buffer.bmp") -> bool:
+        """SDL_SaveBMP of the XRGB8888 surface (Renderer.cpp:184-187): 32-bit BI_RGB BMP."""
+        return save_bmp(path, self.buffer, self.m_Width, self.m_Height)
+
+
+def save_bmp(path: str, pixels: np.ndarray, width: int, height: int) -> bool:
+    img = np.asarray(pixels, dtype=np.uint32).reshape(height, width)[::-1]   # bottom-up rows
+    data = img.astype("<u4").tobytes()
+    header = struct.pack("<2sIHHI", b"BM", 14 + 40 + len(data), 0, 0, 54)
+    info = struct.pack("<IiiHHIIiiII", 40, width, height, 1, 32, 0, len(data), 2835, 2835, 0, 0)
+    with open(path, "wb") as f:
+        f.write(header + info + data)
+    return True

@@ -189,6 +189,13 @@ int rtx_render(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* par
  * frame buffer on the context stream and returns immediately. */
 int rtx_render_async(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
                      int want_rgb);
+/* Multi-view batch (one launch): renders n_views (1..8) cameras of the same scene into
+ * consecutive frame buffers (view v at offset v*width*height).  With stripes, view v
+ * owns the stripes s with s % stripe_step == (stripe_first - v) mod stripe_step, so N
+ * ranks with stripe_first = rank and stripe_step = N cover every view exactly once with
+ * the same number of rows each (the weak-scaling partition of bench.py). */
+int rtx_render_views_async(rtx_ctx* ctx, const rtx_camera* cams, int n_views,
+                           const rtx_render_params* params, int want_rgb);
 int rtx_synchronize(rtx_ctx* ctx);
 /* Copy the context's frame buffer (rows owned by the last render) to host memory. */
 int rtx_download(rtx_ctx* ctx, uint32_t* out_pixels, float* out_rgb);
@@ -198,8 +205,15 @@ int rtx_device_buffers(rtx_ctx* ctx, void** d_pixels, void** d_rgb);
  * on the context stream; writes the mean per-frame device time in ms. */
 int rtx_time_frames(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
                     int iters, float* mean_ms);
-/* Work counters of the last uploaded scene (device bytes resident). */
+int rtx_time_views(rtx_ctx* ctx, const rtx_camera* cams, int n_views, const rtx_render_params* params,
+                   int iters, float* mean_ms);
+/* Bytes of HBM the uploaded scene image occupies. */
 int rtx_scene_bytes(const rtx_ctx* ctx, uint64_t* bytes);
+/* Instrumented render: the same traversal with per-ray work counters (12 x uint64, in
+ * the order pixels, sphere, plane, slab, tri, hit, shadow, occluded, shade_base,
+ * shade_lambert, shade_phong, shade_ct — the SURVEY §8(d) FLOP model).  Not timed. */
+int rtx_count_work(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
+                   uint64_t* counts12);
 
 #ifdef __cplusplus
 }

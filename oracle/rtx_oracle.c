@@ -160,6 +160,10 @@ static int slab(const float* mn, const float* mx, const ray* r) {
 static void bvh_visit(const rtx_mesh* m, uint32_t ni, const ray* r, int* didHit, hitrec* hr,
                       hitrec* cur, int ignore, counters* cnt) {
     const rtx_bvh_node* node = &m->nodes[ni];
+    /* Work accounting stops an any-hit query at its first occluder (the algorithmic
+     * work of DoesHit); the reference keeps visiting the remaining siblings, which does
+     * not change the boolean.  Rendering (cnt == NULL) follows the reference exactly. */
+    if (cnt && ignore && *didHit) return;
     if (cnt) cnt->c[C_SLAB]++;
     if (!slab(node->min, node->max, r)) return;
     if (node->idx_count > 0) {

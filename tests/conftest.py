@@ -1,0 +1,35 @@
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+sys.path.insert(0, str(ROOT / "tests" / "golden"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); run with -m gpu")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _built():
+    """Make sure the native libraries exist (builds in-tree if missing)."""
+    from gp1_raytracer_2223_amd import build
+    lib = ROOT / "gp1_raytracer_2223_amd" / "lib"
+    if not (lib / "librtx_host.so").exists():
+        build.build_host()
+    if not (ROOT / "oracle" / "_build" / "librtx_oracle.so").exists():
+        build.build_oracle()
+    yield
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    from gp1_raytracer_2223_amd.renderer import DeviceContext
+    ctx = DeviceContext(int(os.environ.get("RTX_TEST_DEVICE", "0")))
+    yield ctx
+    ctx.close()

@@ -1,0 +1,89 @@
+"""HIP render path vs the oracle (CPU restatement, pinned to the reference goldens) on
+identical inputs.  Tolerance (BASELINE.json north_star): per-channel max-abs <= 1e-4 on
+the post-MaxToOne float colour, and the uint32 buffer within 1 LSB per channel.  Paths
+without powf (Lambert / SolidColor scenes) are required bit-exact."""
+import numpy as np
+import pytest
+
+import oracle_bind
+from gp1_raytracer_2223_amd import abi
+from gp1_raytracer_2223_amd.scene import HostScene, RENDERABLE
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+POW_FREE = {"W1", "W2", "W4_Bunny", "Synthetic100k", "Bunny8Lights"}
+
+
+def _channels(px):
+    return np.stack([(px >> 16) & 255, (px >> 8) & 255, px & 255], -1).astype(np.int32)
+
+
+def _compare(name, gpu_px, gpu_rgb, ref_px, ref_rgb, exact):
+    d = np.abs(gpu_rgb - ref_rgb)
+    assert not np.isnan(gpu_rgb).any()
+    assert float(d.max(initial=0.0)) <= TOL, f"{name}: max-abs {d.max()} at {np.argmax(d)}"
+    lsb = np.abs(_channels(gpu_px) - _channels(ref_px)).max(initial=0)
+    assert lsb <= 1, f"{name}: {lsb} LSB"
+    if exact:
+        assert np.array_equal(gpu_px, ref_px), f"{name}: {(gpu_px != ref_px).sum()} pixels differ"
+        assert np.array_equal(gpu_rgb.view(np.uint32), ref_rgb.view(np.uint32)), \
+            f"{name}: {(gpu_rgb != ref_rgb).sum()} colour values differ"
+
+
+@pytest.mark.parametrize("name", RENDERABLE)
+@pytest.mark.parametrize("t", [-1.0, 1.3])
+def test_scene_parity(gpu_ctx, name, t):
+    hs = HostScene(name)
+    if t >= 0:
+        hs.update(t)
+    s, cam = hs.view()
+    p = abi.make_params(320, 180)
+    gpu_ctx.upload(s)
+    gpx, grgb = gpu_ctx.render(cam, p)
+    rpx, rrgb = oracle_bind.render(s, cam, p)
+    _compare(name, gpx, grgb, rpx, rrgb, exact=name in POW_FREE)
+
+
+@pytest.mark.parametrize("name", ["W3", "W3_Test", "W4_Reference", "W2"])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("shadows", [0, 1])
+def test_modes(gpu_ctx, name, mode, shadows):
+    hs = HostScene(name)
+    s, cam = hs.view()
+    p = abi.make_params(200, 150, mode, shadows)
+    gpu_ctx.upload(s)
+    gpx, grgb = gpu_ctx.render(cam, p)
+    rpx, rrgb = oracle_bind.render(s, cam, p)
+    _compare(f"{name}/m{mode}/s{shadows}", gpx, grgb, rpx, rrgb, exact=(mode in (0, 1)) or name == "W2")
+
+
+@pytest.mark.parametrize("name", ["W4_Bunny", "W3"])
+def test_stripes_stitch_bit_identical(gpu_ctx, name):
+    """Image tiled over N logical devices (16-row stripes, round robin) == 1 device."""
+    hs = HostScene(name)
+    s, cam = hs.view()
+    W, H = 256, 200
+    gpu_ctx.upload(s)
+    full, _ = gpu_ctx.render(cam, abi.make_params(W, H), want_rgb=False)
+    for n in (2, 3, 4, 8):
+        stitched = np.full(W * H, 0xDEADBEEF, np.uint32)
+        for r in range(n):
+            px, _ = gpu_ctx.render(cam, abi.make_params(W, H, stripe_rows=16, stripe_first=r, stripe_step=n),
+                                   want_rgb=False)
+            rows = np.zeros(H, bool)
+            for y in range(H):
+                rows[y] = (y // 16) % n == r
+            stitched.reshape(H, W)[rows] = px.reshape(H, W)[rows]
+        assert np.array_equal(stitched, full), f"{name} n={n}"
+
+
+@pytest.mark.parametrize("name", ["W4_Bunny", "W3", "W4_Optional", "W4_Reference"])
+def test_work_counters_match_oracle(gpu_ctx, name):
+    hs = HostScene(name)
+    s, cam = hs.view()
+    p = abi.make_params(160, 120)
+    gpu_ctx.upload(s)
+    g = gpu_ctx.count_work(cam, p)
+    o = oracle_bind.count(s, cam, p)
+    assert np.array_equal(g, o), dict(zip(oracle_bind.COUNTER_NAMES, zip(g.tolist(), o.tolist())))
