@@ -1,0 +1,94 @@
+"""Generate the golden fixtures of tests/golden/ from the REFERENCE ITSELF.
+
+Runs only in the build container: needs /root/reference (the reference's sources are
+compiled in place by oracle/ref/Makefile into oracle/_ref/ref_harness; nothing of the
+reference is copied here).  The outputs are data only — inputs and expected outputs of
+the reference's own functions:
+
+  obj_<stem>.npz        Utils::ParseOBJ results for every Resources/*.obj
+  scene_<name>[_t].npz  flattened scenes after Initialize (+ Update(t)): camera, spheres,
+                        planes, lights, materials, mesh world positions / permuted indices /
+                        normals / BVH nodes (large meshes: SHA-256 of each array)
+  frame_<name>_<W>x<H>_m<mode>s<sh>[_t].npz   Renderer::Render output: uint32 pixels and
+                        post-MaxToOne float RGB
+  config_<name>_<W>x<H>.npz   full-resolution BASELINE configs: SHA-256 of the uint32
+                        frame and of the float RGB plane + 4096 seeded sample pixels (index, uint32, rgb)
+  prims.npz             primitive / BRDF known-answer vectors (GeometryUtils, Material::Shade)
+
+Usage:  python tests/golden/make_goldens.py
+"""
+from __future__ import annotations
+
+import hashlib
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parents[1]
+sys.path.insert(0, str(HERE))
+import rtxb  # noqa: E402
+
+HARNESS = ROOT / "oracle" / "_ref" / "ref_harness"
+REF_SRC = Path("/root/reference/source")
+SCENES = ["W1", "W2", "W3", "W3_Test", "W4_Reference", "W4_Bunny", "W4_Optional", "Synthetic100k", "Bunny8Lights"]
+ANIMATED = ["W4_Reference", "W4_Bunny", "W4_Optional", "Bunny8Lights"]
+BIG = {"W4_Optional", "Synthetic100k"}
+CONFIGS = [("W1", 640, 480), ("W3", 1280, 720), ("W4_Bunny", 1920, 1080), ("Synthetic100k", 1920, 1080),
+           ("Bunny8Lights", 3840, 2160)]
+
+
+def run(*args) -> dict:
+    with tempfile.TemporaryDirectory() as td:
+        out = Path(td) / "o.rtxb"
+        subprocess.run([str(HARNESS), *map(str, args), str(out)], cwd=REF_SRC, check=True)
+        return rtxb.read(out)
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def tname(t: float) -> str:
+    return "" if t < 0 else f"_t{t:g}"
+
+
+def main() -> None:
+    assert HARNESS.exists(), "build oracle/_ref first (python -m gp1_raytracer_2223_amd.build)"
+    for obj in sorted(REF_SRC.glob("Resources/*.obj")):
+        d = run("obj", obj.relative_to(REF_SRC))
+        np.savez_compressed(HERE / f"obj_{obj.stem}.npz", **d)
+
+    for name in SCENES:
+        for t in ([-1.0, 1.3] if name in ANIMATED else [-1.0]):
+            d = run("scene", name, t)
+            if name in BIG:
+                d = {k: (np.array([sha(v)]) if k.startswith("mesh") and k != "meshes" else v) for k, v in d.items()}
+            np.savez_compressed(HERE / f"scene_{name}{tname(t)}.npz", **d)
+            d = run("render", name, t, 128, 72, 3, 1, 8)
+            np.savez_compressed(HERE / f"frame_{name}_128x72_m3s1{tname(t)}.npz", pixels=d["pixels"], rgb=d["rgb"])
+
+    for name in ["W3", "W3_Test", "W4_Reference", "W2"]:
+        for mode in range(4):
+            for sh in (0, 1):
+                d = run("render", name, -1, 64, 48, mode, sh, 8)
+                np.savez_compressed(HERE / f"frame_{name}_64x48_m{mode}s{sh}.npz", pixels=d["pixels"], rgb=d["rgb"])
+
+    rng = np.random.default_rng(2223)
+    for name, W, H in CONFIGS:
+        d = run("render", name, -1, W, H, 3, 1, 8)
+        px, rgb = d["pixels"], d["rgb"].reshape(-1, 3)
+        idx = np.sort(rng.choice(W * H, 4096, replace=False)).astype(np.int64)
+        np.savez_compressed(HERE / f"config_{name}_{W}x{H}.npz", sha_pixels=np.array([sha(px)]),
+                            sha_rgb=np.array([sha(rgb)]), idx=idx, pixels=px[idx], rgb=rgb[idx])
+        print(name, W, H, sha(px)[:16], flush=True)
+
+    d = run("prims", 1234, 1500)
+    np.savez_compressed(HERE / "prims.npz", **d)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,77 @@
+"""Multi-rank partition (bench.py / DESIGN.md §6) on CPU with gloo, world_size 2 and 4:
+each rank renders only its 16-row stripes of every view (oracle as the renderer, since
+this container has no GPU); stitching the ranks' stripes must give the single-rank frame
+bit for bit, each rank must get the same number of pixels, and no pixel is rendered twice.
+The transport here (gather to rank 0) is test-only: bench.py moves no data between ranks."""
+import os
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _owned_rows(H, stripe, rank, world, view):
+    first = (rank - view) % world
+    return np.array([(y // stripe) % world == first for y in range(H)])
+
+
+def _worker(rank, world, port, W, H, q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "tests")]
+    import torch
+    import oracle_bind
+    from gp1_raytracer_2223_amd import abi
+    from gp1_raytracer_2223_amd.scene import HostScene
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    hs = HostScene("W4_Bunny")
+    s, cam = hs.view()
+    views = bench.make_views(cam, world)
+    frames = []
+    count = 0
+    for f in range(world):
+        buf = np.zeros(W * H, np.uint32)
+        # rtx_render_views semantics: view f owns stripes s % world == (rank - f) mod world
+        p = abi.make_params(W, H, stripe_rows=16, stripe_first=(rank - f) % world, stripe_step=world)
+        oracle_bind.render(s, views[f], p, threads=2, want_rgb=False, out_px=buf)
+        count += int(_owned_rows(H, 16, rank, world, f).sum()) * W
+        frames.append(torch.from_numpy(buf.view(np.int32)))
+    gathered = [[torch.zeros(W * H, dtype=torch.int32) for _ in range(world)] for _ in range(world)]
+    for f in range(world):
+        dist.all_gather(gathered[f], frames[f])
+    counts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(counts, torch.tensor([count]))
+    if rank == 0:
+        stitched = []
+        for f in range(world):
+            img = np.zeros(W * H, np.uint32)
+            for r in range(world):
+                rows = _owned_rows(H, 16, r, world, f)
+                img.reshape(H, W)[rows] = gathered[f][r].numpy().view(np.uint32).reshape(H, W)[rows]
+            ref, _ = oracle_bind.render(s, views[f], abi.make_params(W, H), threads=2, want_rgb=False)
+            stitched.append(bool(np.array_equal(img, ref)))
+        q.put((stitched, [int(c.item()) for c in counts]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_stripe_partition_gloo(world):
+    W, H = 96, 96
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + world + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    stitched, counts = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(stitched), stitched
+    assert sum(counts) == world * W * H          # every pixel of every view exactly once
+    assert len(set(counts)) == 1                 # weak scaling: equal share per rank

@@ -1,0 +1,71 @@
+"""Pin the oracle (oracle/rtx_oracle.c) to the reference: its frames must equal,
+bit for bit, the frames the reference's own code produced (tests/golden/, generated
+by tests/golden/make_goldens.py from the reference built in place)."""
+import hashlib
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle_bind
+from gp1_raytracer_2223_amd import abi
+from gp1_raytracer_2223_amd.scene import HostScene
+
+G = Path(__file__).resolve().parent / "golden"
+
+
+def _scene(name, t):
+    hs = HostScene(name)
+    if t >= 0:
+        hs.update(t)
+    return hs
+
+
+def _frames():
+    import re
+    out = []
+    pat = re.compile(r"frame_(?P<name>.+)_(?P<w>\d+)x(?P<h>\d+)_m(?P<m>\d)s(?P<s>\d)(?:_t(?P<t>[0-9.]+))?$")
+    for f in sorted(G.glob("frame_*.npz")):
+        mt = pat.match(f.stem)
+        assert mt, f
+        t = float(mt["t"]) if mt["t"] else -1.0
+        out.append(pytest.param(f, mt["name"], t, int(mt["w"]), int(mt["h"]), int(mt["m"]), int(mt["s"]), id=f.stem))
+    return out
+
+
+@pytest.mark.parametrize("path,name,t,W,H,mode,sh", _frames())
+def test_oracle_frame_bit_exact(path, name, t, W, H, mode, sh):
+    g = np.load(path)
+    hs = _scene(name, t)
+    s, cam = hs.view()
+    px, rgb = oracle_bind.render(s, cam, abi.make_params(W, H, mode, sh))
+    assert np.array_equal(px, g["pixels"]), f"{(px != g['pixels']).sum()} pixels differ"
+    assert np.array_equal(rgb.view(np.uint32), g["rgb"].view(np.uint32))
+
+
+@pytest.mark.parametrize("path", sorted(G.glob("config_*.npz")), ids=lambda p: p.stem)
+def test_oracle_config_resolution(path):
+    g = np.load(path)
+    stem = path.stem[len("config_"):]
+    name, wh = stem.rsplit("_", 1)
+    W, H = map(int, wh.split("x"))
+    hs = _scene(name, -1)
+    s, cam = hs.view()
+    px, rgb = oracle_bind.render(s, cam, abi.make_params(W, H))
+    rgb = rgb.reshape(-1, 3)
+    assert np.array_equal(px[g["idx"]], g["pixels"])
+    assert np.array_equal(rgb[g["idx"]].view(np.uint32), g["rgb"].view(np.uint32))
+    assert hashlib.sha256(px.tobytes()).hexdigest() == str(g["sha_pixels"][0])
+    assert hashlib.sha256(rgb.tobytes()).hexdigest() == str(g["sha_rgb"][0])
+
+
+def test_oracle_stripes_cover_frame():
+    hs = _scene("W3", -1)
+    s, cam = hs.view()
+    W, H = 96, 80
+    full, _ = oracle_bind.render(s, cam, abi.make_params(W, H), want_rgb=False)
+    acc = np.zeros_like(full)
+    for r in range(3):
+        oracle_bind.render(s, cam, abi.make_params(W, H, stripe_rows=16, stripe_first=r, stripe_step=3),
+                           want_rgb=False, out_px=acc)
+    assert np.array_equal(acc, full)
