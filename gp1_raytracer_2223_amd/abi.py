@@ -142,7 +142,8 @@ def load_hip() -> C.CDLL:
     missing the product path fails loudly."""
     global _hip
     if _hip is None:
-        path = _lib_path("librtx_hip.so")
+        # RTX_HIP_LIB selects an alternative in-tree build (kernel experiments only)
+        path = Path(os.environ.get("RTX_HIP_LIB", str(_lib_path("librtx_hip.so"))))
         if not path.exists():
             raise RuntimeError(f"{path} is missing: the HIP render path is not built (run __graft_entry__.build())")
         lib = C.CDLL(str(path))

@@ -59,8 +59,11 @@ def build_hip(force: bool = False) -> Path:
     srcs = [CSRC / "rtx_hip.hip"]
     deps = srcs + list(CSRC.glob("*.h")) + [INC / "rtx.h"]
     if force or _stale(out, deps):
+        # -fno-slp-vectorize: the SLP packer turns independent f32 ops into v_pk_* plus
+        # v_mov shuffles; measured 8 % slower on the render kernel (profiles/r01/ablate_*.txt).
         _run([HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-O3", "-ffp-contract=off",
-              "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fPIC", "-shared",
+              "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize",
+              "-DRTX_MIN_WAVES_PER_EU=6", "-fPIC", "-shared",
               "-Wall", f"-I{INC}", f"-I{CSRC}", *srcs, "-o", out])
     return out
 

@@ -59,15 +59,15 @@ __device__ __forceinline__ Ray make_ray(float ox, float oy, float oz, float dx, 
 }
 
 // HitTest_Sphere (Utils.h:52-66) — t and the accept test; hit data is rebuilt later.
+// Branch-free: sqrtf of a negative argument is computed and discarded.
 __device__ __forceinline__ bool sphere_t(const float4 s, const Ray& r, float& t) {
     const float ovx = s.x - r.ox, ovy = s.y - r.oy, ovz = s.z - r.oz;
     const float ovs = ovx * ovx + ovy * ovy + ovz * ovz;
     const float proj = r.dx * ovx + r.dy * ovy + r.dz * ovz;
     const float perp = ovs - proj * proj;
-    if (s.w < perp) return false;
     const float dist = sqrtf(s.w - perp);
     t = proj - dist;
-    return !(t < r.tmin || t > r.tmax);
+    return !(s.w < perp) && !(t < r.tmin || t > r.tmax);
 }
 
 // HitTest_Plane (Utils.h:84-97)
@@ -77,143 +77,173 @@ __device__ __forceinline__ bool plane_t(const float4 p0, const float4 p1, const 
     return t >= r.tmin && t < r.tmax;
 }
 
-// HitTest_Triangle (Utils.h:109-184), Möller–Trumbore with the reference's cull rules;
-// SHADOW swaps front/back culling (:114-127).  Cross products are written in their
-// reduced form {a, -b, c}: identical to Vector3::Cross's UnitX*a - UnitY*b + UnitZ*c
-// for finite inputs up to the sign of a zero, which no comparison below can observe.
-template <bool SHADOW>
-__device__ __forceinline__ bool tri_t(const float4 A, const float4 B, const float4 C, int cull, const Ray& r,
+// HitTest_Triangle (Utils.h:109-184), Möller–Trumbore with the reference's cull rules
+// (shadow rays swap front/back culling, :114-127).
+//
+// Written branch-free: every early `return false` of the reference becomes a term whose
+// positive value means "reject", folded with v_max_f32 (which ignores NaN exactly as the
+// reference's comparisons do: a NaN never rejects).  For binary32 x, y:
+//   x < y  <=>  (y - x) > 0   (a non-zero exact difference never rounds to 0 or flips sign)
+// so  |c| < EPS <=> EPS-|c| > 0,  u < 0 || u > 1 <=> max(-u, u-1) > 0,
+//     v < 0 || (u+v) > 1 <=> max(-v, (u+v)-1) > 0,  t < tmin <=> tmin - t > 0.
+// Cross products use the reduced form {a, -b, c}: identical to Vector3::Cross's
+// UnitX*a - UnitY*b + UnitZ*c for finite inputs up to the sign of a zero, which none of
+// the tests below can observe.  Returns the reject score; accept iff !(score > 0) && t < tmax.
+// `cs` is the mesh's cull sign: -1 FrontFaceCulling (reject cullDot < 0), +1
+// BackFaceCulling (reject cullDot > 0), 0 NoCulling (the term 0*cullDot never exceeds 0);
+// shadow rays pass -cs, which is the reference's front/back swap.
+__device__ __forceinline__ bool tri_t(const float4 A, const float4 B, const float4 C, float cs, const Ray& r,
                                       float& t) {
     const float cullDot = A.w * r.dx + B.w * r.dy + C.w * r.dz;
-    if (fabsf(cullDot) < FLT_EPSILON) return false;
-    if (SHADOW) cull = (cull == RTX_CULL_FRONT) ? RTX_CULL_BACK : (cull == RTX_CULL_BACK ? RTX_CULL_FRONT : cull);
-    if (cull == RTX_CULL_FRONT && cullDot < 0) return false;
-    if (cull == RTX_CULL_BACK && cullDot > 0) return false;
+    float rej = fmaxf(FLT_EPSILON - fabsf(cullDot), cs * cullDot);
     const float hx = r.dy * C.z - r.dz * C.y;
     const float hy = -(r.dx * C.z - r.dz * C.x);
     const float hz = r.dx * C.y - r.dy * C.x;
     const float a = B.x * hx + B.y * hy + B.z * hz;
-    if (fabsf(a) < FLT_EPSILON) return false;
+    rej = fmaxf(rej, FLT_EPSILON - fabsf(a));
     const float ai = 1.f / a;
     const float sx = r.ox - A.x, sy = r.oy - A.y, sz = r.oz - A.z;
     const float u = ai * (sx * hx + sy * hy + sz * hz);
-    if (u < 0.f || u > 1.f) return false;
+    rej = fmaxf(rej, fmaxf(-u, u - 1.f));
     const float qx = sy * B.z - sz * B.y;
     const float qy = -(sx * B.z - sz * B.x);
     const float qz = sx * B.y - sy * B.x;
     const float v = ai * (r.dx * qx + r.dy * qy + r.dz * qz);
-    if (v < 0.f || (u + v) > 1.f) return false;
+    rej = fmaxf(rej, fmaxf(-v, (u + v) - 1.f));
     t = ai * (C.x * qx + C.y * qy + C.z * qz);
-    return !(t < r.tmin || t >= r.tmax);
+    rej = fmaxf(rej, r.tmin - t);
+    return !(rej > 0.f) && !(t >= r.tmax);
 }
 
-// SlabTest_BVH (Utils.h:221-243)
+// SlabTest_BVH (Utils.h:221-243).  FAST uses v_min/v_max_f32, which differ from std::min/
+// std::max only when an operand is NaN; a NaN slab value needs (box - origin) * inv with
+// an infinite inv component, so FAST is taken only when every live lane's inverse
+// direction is finite (decided once per ray batch with a ballot).
+template <bool FAST>
 __device__ __forceinline__ bool slab(const float4 mn, const float4 mx, const Ray& r) {
     const float tx1 = (mn.x - r.ox) * r.ix, tx2 = (mx.x - r.ox) * r.ix;
-    float tMin = smin(tx1, tx2), tMax = smax(tx1, tx2);
     const float ty1 = (mn.y - r.oy) * r.iy, ty2 = (mx.y - r.oy) * r.iy;
-    tMin = smax(tMin, smin(ty1, ty2));
-    tMax = smin(tMax, smax(ty1, ty2));
     const float tz1 = (mn.z - r.oz) * r.iz, tz2 = (mx.z - r.oz) * r.iz;
-    tMin = smax(tMin, smin(tz1, tz2));
-    tMax = smin(tMax, smax(tz1, tz2));
+    float tMin, tMax;
+    if (FAST) {
+        tMin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+        tMax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    } else {
+        tMin = smin(tx1, tx2);
+        tMax = smax(tx1, tx2);
+        tMin = smax(tMin, smin(ty1, ty2));
+        tMax = smin(tMax, smax(ty1, ty2));
+        tMin = smax(tMin, smin(tz1, tz2));
+        tMax = smin(tMax, smax(tz1, tz2));
+    }
     return tMax > 0 && tMax >= tMin;
+}
+
+__device__ __forceinline__ bool finite_inv(const Ray& r) {
+    return fabsf(r.ix) <= FLT_MAX && fabsf(r.iy) <= FLT_MAX && fabsf(r.iz) <= FLT_MAX;
+}
+
+__device__ __forceinline__ float cull_sign(int cull, bool shadow) {
+    const float cs = cull == RTX_CULL_FRONT ? -1.f : (cull == RTX_CULL_BACK ? 1.f : 0.f);
+    return shadow ? -cs : cs;
 }
 
 struct Counts {
     uint32_t c[kNumCounters];
 };
 
-// Closest-hit packet traversal of one mesh.  `sc_t` is the reference's shared scratch
-// HitRecord t (Scene.cpp:31, Utils.h:270-273): a triangle replaces it iff t < sc_t.
-template <bool COUNT>
-__device__ void mesh_closest(const DevScene& S, const int4 M, const Ray& r, unsigned long long mask, uint32_t lane,
-                             uint32_t* sN, unsigned long long* sM, float& sc_t, uint32_t& sc_tri, Counts& cnt) {
-    if (M.y == 0 || mask == 0) return;
-    int sp = 0;
+// Packet traversal of one mesh's BVH by the whole wave.
+//
+// A node is entered with the mask of lanes whose slab test on it passed; an inner node
+// then tests BOTH children (adjacent, one 64-byte scalar load) for those lanes, descends
+// into the left child and pushes the right one with its own pass mask.  Each lane thus
+// evaluates exactly the slab tests and triangle tests of the reference's recursive DFS
+// (Utils.h:246-288), triangles in the same left-to-right order.
+//   closest (ANY = false): `sc_t` is the shared scratch HitRecord t of Scene.cpp:31 that
+//       IntersectionTest_BVH compares against (Utils.h:270-273); t < sc_t replaces it.
+//   any-hit (ANY = true, shadow rays, Scene::DoesHit): a lane leaves at its first
+//       occluder; the wave leaves as soon as every lane in `mask` is occluded.
+// COUNT: per-lane SURVEY §8(d) work counters, any-hit counted up to the first occluder.
+template <bool ANY, bool FAST, bool COUNT>
+__device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, unsigned long long mask, uint32_t lane,
+                              uint32_t* sN, unsigned long long* sM, unsigned long long* sT, float& sc_t,
+                              uint32_t& sc_tri, bool& occ, Counts& cnt) {
+    if (M.y == 0) return;
+    const float cs = cull_sign(M.z, ANY);
     uint32_t node = static_cast<uint32_t>(M.x);
-    unsigned long long m = mask;
+    unsigned long long m;
+    {
+        const float4 b0 = S.nodes[2 * node], b1 = S.nodes[2 * node + 1];
+        const bool in = (mask >> lane) & 1ull;
+        if (COUNT && in) cnt.c[kSlab]++;
+        m = ballot(in && slab<FAST>(b0, b1, r));
+        if (m == 0) return;
+    }
+    int sp = 0;
     for (;;) {
         const float4 b0 = S.nodes[2 * node], b1 = S.nodes[2 * node + 1];
+        const uint32_t link = __float_as_uint(b0.w);
+        const uint32_t ntri = __float_as_uint(b1.w);
         const bool in = (m >> lane) & 1ull;
-        if (COUNT && in) cnt.c[kSlab]++;
-        const bool pass = in && slab(b0, b1, r);
-        const unsigned long long pm = ballot(pass);
-        if (pm) {
-            const uint32_t link = __float_as_uint(b0.w);
-            const uint32_t ntri = __float_as_uint(b1.w);
-            if (ntri) {
-                for (uint32_t k = 0; k < ntri; ++k) {
-                    const uint32_t ti = link + k;
-                    const float4 A = S.tris[3 * ti], B = S.tris[3 * ti + 1], C = S.tris[3 * ti + 2];
-                    if (pass) {
-                        if (COUNT) cnt.c[kTri]++;
-                        float t;
-                        if (tri_t<false>(A, B, C, M.z, r, t) && t < sc_t) { sc_t = t; sc_tri = ti; }
-                    }
+        if (ntri) {
+            for (uint32_t k = 0; k < ntri; ++k) {
+                const uint32_t ti = link + k;
+                const Tri T = S.tris[ti];
+                float t;
+                const bool h = tri_t(T.a, T.b, T.c, cs, r, t);
+                if (ANY) {
+                    const bool live = in & !occ;
+                    if (COUNT && live) cnt.c[kTri]++;
+                    occ = occ | (live & h);
+                } else {
+                    if (COUNT && in) cnt.c[kTri]++;
+                    const bool u = in & h & (t < sc_t);
+                    sc_t = u ? t : sc_t;
+                    sc_tri = u ? ti : sc_tri;
                 }
-            } else {
-                sN[sp] = link + 1;   // right child after the whole left subtree
-                sM[sp] = pm;
-                ++sp;
+            }
+            if (ANY && (ballot(!occ) & mask) == 0) return;
+        } else {
+            const float4 c0 = S.nodes[2 * link], c1 = S.nodes[2 * link + 1];
+            const float4 c2 = S.nodes[2 * link + 2], c3 = S.nodes[2 * link + 3];
+            const unsigned long long ml = ballot(in && slab<FAST>(c0, c1, r));
+            const unsigned long long mr = ballot(in && slab<FAST>(c2, c3, r));
+            if (COUNT && in) cnt.c[kSlab]++;               // left child's test
+            if (COUNT && !ANY && in) cnt.c[kSlab]++;       // right child's (closest: always reached)
+            if (ml) {
+                if (mr || (COUNT && ANY)) {                // any-hit COUNT: right is counted at pop
+                    sN[sp] = link + 1;
+                    sM[sp] = mr;
+                    if (COUNT && ANY) sT[sp] = m;
+                    ++sp;
+                }
                 node = link;
-                m = pm;
+                m = ml;
+                continue;
+            }
+            if (COUNT && ANY && in) cnt.c[kSlab]++;        // right child's test, reached now
+            if (mr) {
+                node = link + 1;
+                m = mr;
                 continue;
             }
         }
-        if (sp == 0) break;
-        --sp;
-        node = uni(sN[sp]);
-        m = uni64(sM[sp]);
-    }
-}
-
-// Any-hit packet traversal (shadow rays, Scene::DoesHit → HitTest_TriangleMesh with
-// ignoreHitRecord).  Lanes leave at their first occluder; the wave leaves when all did.
-template <bool COUNT>
-__device__ void mesh_any(const DevScene& S, const int4 M, const Ray& r, unsigned long long mask, uint32_t lane,
-                         uint32_t* sN, unsigned long long* sM, bool& occ, Counts& cnt) {
-    if (M.y == 0) return;
-    unsigned long long m = mask & ballot(!occ);
-    if (m == 0) return;
-    int sp = 0;
-    uint32_t node = static_cast<uint32_t>(M.x);
-    for (;;) {
-        m &= ballot(!occ);
-        if (m) {
-            const float4 b0 = S.nodes[2 * node], b1 = S.nodes[2 * node + 1];
-            const bool in = (m >> lane) & 1ull;
-            if (COUNT && in) cnt.c[kSlab]++;
-            const bool pass = in && slab(b0, b1, r);
-            const unsigned long long pm = ballot(pass);
-            if (pm) {
-                const uint32_t link = __float_as_uint(b0.w);
-                const uint32_t ntri = __float_as_uint(b1.w);
-                if (ntri) {
-                    for (uint32_t k = 0; k < ntri; ++k) {
-                        const uint32_t ti = link + k;
-                        const float4 A = S.tris[3 * ti], B = S.tris[3 * ti + 1], C = S.tris[3 * ti + 2];
-                        if (pass && !occ) {
-                            if (COUNT) cnt.c[kTri]++;
-                            float t;
-                            if (tri_t<true>(A, B, C, M.z, r, t)) occ = true;
-                        }
-                    }
-                    if ((ballot(!occ) & mask) == 0) break;
-                } else {
-                    sN[sp] = link + 1;
-                    sM[sp] = pm;
-                    ++sp;
-                    node = link;
-                    m = pm;
-                    continue;
+        // pop the next pending right child
+        for (;;) {
+            if (sp == 0) return;
+            --sp;
+            node = uni(sN[sp]);
+            m = uni64(sM[sp]);
+            if (ANY) {
+                const unsigned long long live = ballot(!occ);
+                if (COUNT) {
+                    const unsigned long long tested = uni64(sT[sp]);
+                    if (((tested & live) >> lane) & 1ull) cnt.c[kSlab]++;
                 }
+                m &= live;
             }
+            if (m) break;
         }
-        if (sp == 0) break;
-        --sp;
-        node = uni(sN[sp]);
-        m = uni64(sM[sp]);
     }
 }
 
@@ -281,12 +311,17 @@ __device__ __forceinline__ uint32_t q8(float c) {
 
 // Renderer::RenderPixel (source/Renderer.cpp:100-182) for a 16x16 tile per workgroup.
 template <bool COUNT>
-__global__ void __launch_bounds__(kBlockThreads) rtx_render_kernel(const DevScene S, const FrameArgs F) {
+#ifndef RTX_MIN_WAVES_PER_EU
+#define RTX_MIN_WAVES_PER_EU 1
+#endif
+__global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_render_kernel(const DevScene S, const FrameArgs F) {
     __shared__ uint32_t stkN[kBlockThreads / 64][kStackDepth];
     __shared__ unsigned long long stkM[kBlockThreads / 64][kStackDepth];
+    __shared__ unsigned long long stkT[COUNT ? kBlockThreads / 64 : 1][kStackDepth];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t* sN = stkN[wave];
     unsigned long long* sM = stkM[wave];
+    unsigned long long* sT = stkT[COUNT ? wave : 0];
 
     const uint32_t view = blockIdx.z;
     const ViewCam& V = F.cam[view];
@@ -315,36 +350,41 @@ __global__ void __launch_bounds__(kBlockThreads) rtx_render_kernel(const DevScen
     dx /= dm; dy /= dm; dz /= dm;
     const Ray vr = make_ray(V.origin[0], V.origin[1], V.origin[2], dx, dy, dz, 0.0001f, FLT_MAX);
     const unsigned long long active = ballot(valid);
+    const bool fast = (ballot(valid && !finite_inv(vr)) == 0);
 
     // ---- Scene::GetClosestHit (Scene.cpp:29-66)
     float best_t = FLT_MAX, sc_t = FLT_MAX;
     uint32_t best_kind = 0, best_idx = 0;   // kind: 0 none, 1 sphere, 2 plane, 3 triangle
     for (uint32_t i = 0; i < S.n_spheres; ++i) {
         const float4 s = S.spheres[i];
-        if (valid) {
-            if (COUNT) cnt.c[kSphere]++;
-            float t;
-            if (sphere_t(s, vr, t)) {
-                sc_t = t;
-                if (t < best_t) { best_t = t; best_kind = 1; best_idx = i; }
-            }
-        }
+        if (COUNT && valid) cnt.c[kSphere]++;
+        float t;
+        const bool h = valid && sphere_t(s, vr, t);
+        sc_t = h ? t : sc_t;
+        const bool b = h && t < best_t;
+        best_t = b ? t : best_t;
+        best_kind = b ? 1u : best_kind;
+        best_idx = b ? i : best_idx;
     }
     for (uint32_t i = 0; i < S.n_planes; ++i) {
         const float4 p0 = S.planes[2 * i], p1 = S.planes[2 * i + 1];
-        if (valid) {
-            if (COUNT) cnt.c[kPlane]++;
-            float t;
-            if (plane_t(p0, p1, vr, t)) {
-                sc_t = t;
-                if (t < best_t) { best_t = t; best_kind = 2; best_idx = i; }
-            }
-        }
+        if (COUNT && valid) cnt.c[kPlane]++;
+        float t;
+        const bool h = valid && plane_t(p0, p1, vr, t);
+        sc_t = h ? t : sc_t;
+        const bool b = h && t < best_t;
+        best_t = b ? t : best_t;
+        best_kind = b ? 2u : best_kind;
+        best_idx = b ? i : best_idx;
     }
     for (uint32_t mi = 0; mi < S.n_meshes; ++mi) {
         const int4 M = S.meshes[mi];
         uint32_t sc_tri = 0;
-        mesh_closest<COUNT>(S, M, vr, active, lane, sN, sM, sc_t, sc_tri, cnt);
+        bool unused = false;
+        if (fast)
+            mesh_traverse<false, true, COUNT>(S, M, vr, active, lane, sN, sM, sT, sc_t, sc_tri, unused, cnt);
+        else
+            mesh_traverse<false, false, COUNT>(S, M, vr, active, lane, sN, sM, sT, sc_t, sc_tri, unused, cnt);
         if (sc_t < best_t) { best_t = sc_t; best_kind = 3; best_idx = sc_tri; }
     }
 
@@ -365,9 +405,9 @@ __global__ void __launch_bounds__(kBlockThreads) rtx_render_kernel(const DevScen
             nx = p1.x; ny = p1.y; nz = p1.z;
             mat = __float_as_uint(p0.w);
         } else {
-            const float4 A = S.tris[3 * best_idx], B = S.tris[3 * best_idx + 1], C = S.tris[3 * best_idx + 2];
-            nx = A.w; ny = B.w; nz = C.w;
-            mat = S.tri_mat[best_idx];
+            const Tri T = S.tris[best_idx];
+            nx = T.a.w; ny = T.b.w; nz = T.c.w;
+            mat = __float_as_uint(T.d.x);
         }
     }
     if (COUNT && did) cnt.c[kHit]++;
@@ -390,29 +430,34 @@ __global__ void __launch_bounds__(kBlockThreads) rtx_render_kernel(const DevScen
             if (F.shadows) {
                 // Scene::DoesHit (Scene.cpp:68-96) on Ray{originOffset, l, 1e-4, |l|}
                 const Ray sr = make_ray(oox, ooy, ooz, lx, ly, lz, 0.0001f, mag);
+                const bool sfast = (ballot(did && !finite_inv(sr)) == 0);
                 if (COUNT && did) cnt.c[kShadow]++;
                 for (uint32_t i = 0; i < S.n_spheres; ++i) {
                     if ((ballot(did && !occ)) == 0) break;
                     const float4 s = S.spheres[i];
-                    if (did && !occ) {
-                        if (COUNT) cnt.c[kSphere]++;
-                        float t;
-                        occ = sphere_t(s, sr, t);
-                    }
+                    const bool live = did && !occ;
+                    if (COUNT && live) cnt.c[kSphere]++;
+                    float t;
+                    occ = occ || (live && sphere_t(s, sr, t));
                 }
                 for (uint32_t i = 0; i < S.n_planes; ++i) {
                     if ((ballot(did && !occ)) == 0) break;
                     const float4 p0 = S.planes[2 * i], p1 = S.planes[2 * i + 1];
-                    if (did && !occ) {
-                        if (COUNT) cnt.c[kPlane]++;
-                        float t;
-                        occ = plane_t(p0, p1, sr, t);
-                    }
+                    const bool live = did && !occ;
+                    if (COUNT && live) cnt.c[kPlane]++;
+                    float t;
+                    occ = occ || (live && plane_t(p0, p1, sr, t));
                 }
                 for (uint32_t mi = 0; mi < S.n_meshes; ++mi) {
                     const unsigned long long live = ballot(did && !occ);
                     if (live == 0) break;
-                    mesh_any<COUNT>(S, S.meshes[mi], sr, live, lane, sN, sM, occ, cnt);
+                    float st = 0.f;
+                    uint32_t stri = 0;
+                    if (sfast)
+                        mesh_traverse<true, true, COUNT>(S, S.meshes[mi], sr, live, lane, sN, sM, sT, st, stri, occ, cnt);
+                    else
+                        mesh_traverse<true, false, COUNT>(S, S.meshes[mi], sr, live, lane, sN, sM, sT, st, stri, occ,
+                                                          cnt);
                 }
             }
             if (!did) continue;
@@ -588,7 +633,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     if (s->n_materials == 0 || s->n_materials > 256) return fail(c, RTX_E_INVALID, "need 1..256 materials");
     const uint32_t nm = s->n_materials;
     std::vector<float4> sph, pl, tri, nodes, lights, mats;
-    std::vector<uint32_t> sph_mat, tri_mat;
+    std::vector<uint32_t> sph_mat;
     std::vector<int4> meshes;
     for (uint32_t i = 0; i < s->n_spheres; ++i) {
         const rtx_sphere& p = s->spheres[i];
@@ -607,7 +652,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
         if (m.material >= nm) return fail(c, RTX_E_INVALID, "mesh material out of range");
         if (m.cull_mode < RTX_CULL_FRONT || m.cull_mode > RTX_CULL_NONE) return fail(c, RTX_E_INVALID, "bad cull mode");
         if (m.n_indices % 3) return fail(c, RTX_E_INVALID, "mesh index count not a multiple of 3");
-        const uint32_t tri0 = static_cast<uint32_t>(tri.size() / 3), node0 = static_cast<uint32_t>(nodes.size() / 2);
+        const uint32_t tri0 = static_cast<uint32_t>(tri.size() / 4), node0 = static_cast<uint32_t>(nodes.size() / 2);
         const uint32_t ntri = m.n_indices / 3;
         if (ntri && (!m.positions || !m.indices || !m.normals)) return fail(c, RTX_E_INVALID, "mesh arrays missing");
         for (uint32_t k = 0; k < ntri; ++k) {
@@ -623,7 +668,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
             tri.push_back(f4(v0[0], v0[1], v0[2], n[0]));
             tri.push_back(f4(v1[0] - v0[0], v1[1] - v0[1], v1[2] - v0[2], n[1]));
             tri.push_back(f4(v2[0] - v0[0], v2[1] - v0[1], v2[2] - v0[2], n[2]));
-            tri_mat.push_back(m.material);
+            tri.push_back(f4(bits(m.material), 0.f, 0.f, 0.f));
         }
         if (m.n_nodes) {
             if (!m.nodes) return fail(c, RTX_E_INVALID, "mesh nodes missing");
@@ -664,7 +709,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     struct Sec { const void* p; size_t n; size_t off; };
     Sec secs[] = {{sph.data(), sph.size() * 16, 0},       {sph_mat.data(), sph_mat.size() * 4, 0},
                   {pl.data(), pl.size() * 16, 0},         {tri.data(), tri.size() * 16, 0},
-                  {tri_mat.data(), tri_mat.size() * 4, 0}, {nodes.data(), nodes.size() * 16, 0},
+                  {nodes.data(), nodes.size() * 16, 0},
                   {meshes.data(), meshes.size() * 16, 0}, {lights.data(), lights.size() * 16, 0},
                   {mats.data(), mats.size() * 16, 0}};
     size_t total = 0;
@@ -685,15 +730,14 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     d.spheres = reinterpret_cast<const float4*>(c->d_scene + secs[0].off);
     d.sphere_mat = reinterpret_cast<const uint32_t*>(c->d_scene + secs[1].off);
     d.planes = reinterpret_cast<const float4*>(c->d_scene + secs[2].off);
-    d.tris = reinterpret_cast<const float4*>(c->d_scene + secs[3].off);
-    d.tri_mat = reinterpret_cast<const uint32_t*>(c->d_scene + secs[4].off);
-    d.nodes = reinterpret_cast<const float4*>(c->d_scene + secs[5].off);
-    d.meshes = reinterpret_cast<const int4*>(c->d_scene + secs[6].off);
-    d.lights = reinterpret_cast<const float4*>(c->d_scene + secs[7].off);
-    d.materials = reinterpret_cast<const float4*>(c->d_scene + secs[8].off);
+    d.tris = reinterpret_cast<const Tri*>(c->d_scene + secs[3].off);
+    d.nodes = reinterpret_cast<const float4*>(c->d_scene + secs[4].off);
+    d.meshes = reinterpret_cast<const int4*>(c->d_scene + secs[5].off);
+    d.lights = reinterpret_cast<const float4*>(c->d_scene + secs[6].off);
+    d.materials = reinterpret_cast<const float4*>(c->d_scene + secs[7].off);
     d.n_spheres = s->n_spheres; d.n_planes = s->n_planes; d.n_meshes = s->n_meshes;
     d.n_lights = s->n_lights; d.n_materials = nm;
-    d.n_tris = static_cast<uint32_t>(tri.size() / 3); d.n_nodes = static_cast<uint32_t>(nodes.size() / 2);
+    d.n_tris = static_cast<uint32_t>(tri.size() / 4); d.n_nodes = static_cast<uint32_t>(nodes.size() / 2);
     c->dev = d;
     c->has_scene = true;
     return RTX_OK;

@@ -21,17 +21,20 @@ enum Counter {
 // becomes one s_load_dwordx4/x8 (scalar cache) instead of 64 vector loads:
 //   sphere   1 x float4 {cx, cy, cz, r*r}          + mat u32
 //   plane    2 x float4 {ox, oy, oz, mat}, {nx, ny, nz, 0}
-//   triangle 3 x float4 {v0, n.x}, {v1-v0, n.y}, {v2-v0, n.z}  (BVH leaf order, all meshes)
+//   triangle 4 x float4 {v0, n.x}, {v1-v0, n.y}, {v2-v0, n.z}, {mat}  (BVH leaf order, all meshes)
 //   node     2 x float4 {min, link}, {max, tri_count}  link = first tri (leaf) | left node
 //   mesh     int4 {first node, n nodes, cull, mat}
 //   light    2 x float4 {origin, type}, {color, intensity}
 //   material 3 x float4 {kind, rgb}, {kd, ks, exp, metal}, {rough, (rgb*kd)/PI}
+struct alignas(64) Tri {
+    float4 a, b, c, d;   // {v0, n.x}, {v1-v0, n.y}, {v2-v0, n.z}, {mat, 0, 0, 0}
+};
+
 struct DevScene {
     const float4* __restrict__ spheres;
     const uint32_t* __restrict__ sphere_mat;
     const float4* __restrict__ planes;
-    const float4* __restrict__ tris;
-    const uint32_t* __restrict__ tri_mat;     // material of the owning mesh, per triangle
+    const Tri* __restrict__ tris;
     const float4* __restrict__ nodes;
     const int4* __restrict__ meshes;
     const float4* __restrict__ lights;

@@ -1,0 +1,30 @@
+"""Summarise a tools/profile.sh output dir: mean counter value per dispatch of the render kernel."""
+import collections
+import csv
+import glob
+import json
+import sys
+
+d = sys.argv[1]
+out = {}
+meta = {}
+for f in sorted(glob.glob(f"{d}/pmc*/run_counter_collection.csv")):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        if "rtx_render_kernel<false>" in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count",
+                                      "SGPR_Count")}
+    for k, v in agg.items():
+        out[k] = round(sum(v) / len(v), 1)
+w = out.get("SQ_WAVES", 1)
+derived = {}
+for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH", "SQ_INSTS_VMEM_RD"):
+    if k in out:
+        derived[k + "_per_wave"] = round(out[k] / w, 1)
+if "SQ_THREAD_CYCLES_VALU" in out and "SQ_ACTIVE_INST_VALU" in out:
+    derived["valu_lane_utilisation"] = round(out["SQ_THREAD_CYCLES_VALU"] / (64 * out["SQ_ACTIVE_INST_VALU"]), 3)
+if "SQ_WAIT_ANY" in out and "SQ_WAVE_CYCLES" in out:
+    for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+        derived[k + "_frac_of_wave_cycles"] = round(out[k] / out["SQ_WAVE_CYCLES"], 3)
+print(json.dumps({"counters": out, "derived": derived, "dispatch": meta}, indent=1))
