@@ -134,7 +134,7 @@ def load_host() -> C.CDLL:
 HIP_SYMBOLS = ["rtx_abi_version", "rtx_create", "rtx_destroy", "rtx_last_error", "rtx_upload_scene",
                "rtx_render", "rtx_render_async", "rtx_synchronize", "rtx_download", "rtx_device_buffers",
                "rtx_time_frames", "rtx_scene_bytes", "rtx_count_work",
-               "rtx_render_views_async", "rtx_time_views"]
+               "rtx_render_views_async", "rtx_time_views", "rtx_count_work_ex"]
 
 
 def load_hip() -> C.CDLL:
@@ -181,6 +181,9 @@ def load_hip() -> C.CDLL:
         lib.rtx_scene_bytes.restype = C.c_int
         lib.rtx_count_work.argtypes = [VP, C.POINTER(Camera), C.POINTER(RenderParams), C.POINTER(C.c_uint64)]
         lib.rtx_count_work.restype = C.c_int
+        lib.rtx_count_work_ex.argtypes = [VP, C.POINTER(Camera), C.POINTER(RenderParams), C.POINTER(C.c_uint64),
+                                          C.c_int]
+        lib.rtx_count_work_ex.restype = C.c_int
         _hip = lib
     return _hip
 

@@ -49,7 +49,7 @@ def build_host(force: bool = False) -> Path:
     deps = srcs + list((CSRC / "host").glob("*.h")) + [INC / "rtx.h", INC / "rtx_host.h"]
     if force or _stale(out, deps):
         _run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
-              "-Wall", "-Wextra", f"-I{INC}", *srcs, "-o", out])
+              "-Wall", "-Wextra", f"-I{INC}", *srcs, "-o", out, "-ldl"])
     return out
 
 
@@ -65,6 +65,18 @@ def build_hip(force: bool = False) -> Path:
               "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize",
               "-DRTX_MIN_WAVES_PER_EU=6", "-fPIC", "-shared",
               "-Wall", f"-I{INC}", f"-I{CSRC}", *srcs, "-o", out])
+    return out
+
+
+def build_cli(force: bool = False) -> Path:
+    """Headless C++ host program over both libraries (lib/rtx_render)."""
+    out = LIB / "rtx_render"
+    src = CSRC / "cli" / "rtx_render.cpp"
+    deps = [src, INC / "rtx_renderer.hpp", INC / "rtx.h", INC / "rtx_host.h", LIB / "librtx_hip.so",
+            LIB / "librtx_host.so"]
+    if force or _stale(out, deps):
+        _run(["g++", "-std=c++17", "-O2", "-Wall", f"-I{INC}", src, "-o", out, f"-L{LIB}", "-lrtx_hip", "-lrtx_host",
+              "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"])
     return out
 
 
@@ -97,6 +109,7 @@ def build_all(force: bool = False) -> None:
     build_oracle(force)
     build_reference(force)
     build_hip(force)
+    build_cli(force)
 
 
 if __name__ == "__main__":

@@ -1,10 +1,23 @@
 // host_api.cpp — extern "C" wrappers of the host scene model (include/rtx_host.h).
+#include <dlfcn.h>
+
 #include <cstring>
 #include <new>
 #include <string>
 
 #include "rtx_host.h"
 #include "scene.h"
+
+// Default asset directory: <dir of librtx_host.so>/../assets (the in-tree package layout).
+static std::string default_asset_dir() {
+    Dl_info info;
+    if (dladdr(reinterpret_cast<void*>(&default_asset_dir), &info) && info.dli_fname) {
+        std::string p = info.dli_fname;
+        const size_t slash = p.rfind('/');
+        if (slash != std::string::npos) return p.substr(0, slash) + "/../assets";
+    }
+    return "assets";
+}
 
 struct rtx_host_scene {
     std::unique_ptr<rtx::Scene> scene;
@@ -22,7 +35,7 @@ extern "C" int rtx_host_scene_create(const char* name, const char* asset_dir, rt
     if (!name || !out) return RTX_E_INVALID;
     *out = nullptr;
     try {
-        auto s = rtx::MakeScene(name, asset_dir ? asset_dir : "");
+        auto s = rtx::MakeScene(name, (asset_dir && *asset_dir) ? asset_dir : default_asset_dir());
         if (!s) { set_err(err, err_len, std::string("unknown scene: ") + name); return RTX_E_INVALID; }
         if (!s->Initialize()) { set_err(err, err_len, s->Error()); return RTX_E_UNSUPPORTED; }
         auto* h = new rtx_host_scene;

@@ -42,7 +42,8 @@ __device__ __forceinline__ unsigned long long uni64(unsigned long long x) {
     const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32));
     return (static_cast<unsigned long long>(hi) << 32) | lo;
 }
-__device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ unsigned long long wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 struct Ray {
     float ox, oy, oz, dx, dy, dz, ix, iy, iz, tmin, tmax;
@@ -148,6 +149,10 @@ __device__ __forceinline__ float cull_sign(int cull, bool shadow) {
     return shadow ? -cs : cs;
 }
 
+struct alignas(64) NodePair {
+    float4 l0, l1, r0, r1;   // left child {min, link}, {max, ntri}; right child likewise
+};
+
 struct Counts {
     uint32_t c[kNumCounters];
 };
@@ -166,35 +171,36 @@ struct Counts {
 // COUNT: per-lane SURVEY §8(d) work counters, any-hit counted up to the first occluder.
 template <bool ANY, bool FAST, bool COUNT>
 __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, unsigned long long mask, uint32_t lane,
-                              uint32_t* sN, unsigned long long* sM, unsigned long long* sT, float& sc_t,
-                              uint32_t& sc_tri, bool& occ, Counts& cnt) {
+                              uint4* stk, unsigned long long* sT, float& sc_t, uint32_t& sc_tri,
+                              unsigned long long& live, Counts& cnt) {
     if (M.y == 0) return;
     const float cs = cull_sign(M.z, ANY);
-    uint32_t node = static_cast<uint32_t>(M.x);
+    const NodePair* __restrict__ pairs = reinterpret_cast<const NodePair*>(S.nodes);
     unsigned long long m;
+    uint32_t link, ntri;
     {
-        const float4 b0 = S.nodes[2 * node], b1 = S.nodes[2 * node + 1];
-        const bool in = (mask >> lane) & 1ull;
-        if (COUNT && in) cnt.c[kSlab]++;
-        m = ballot(in && slab<FAST>(b0, b1, r));
+        // root (odd global index; every child pair starts at an even one, 64-B aligned)
+        const float4 b0 = S.nodes[2 * M.x], b1 = S.nodes[2 * M.x + 1];
+        if (COUNT && ((mask >> lane) & 1ull)) cnt.c[kSlab]++;
+        m = wballot(slab<FAST>(b0, b1, r)) & mask;
         if (m == 0) return;
+        link = __float_as_uint(b0.w);
+        ntri = __float_as_uint(b1.w);
     }
     int sp = 0;
     for (;;) {
-        const float4 b0 = S.nodes[2 * node], b1 = S.nodes[2 * node + 1];
-        const uint32_t link = __float_as_uint(b0.w);
-        const uint32_t ntri = __float_as_uint(b1.w);
-        const bool in = (m >> lane) & 1ull;
+        // invariant: the node (link, ntri) passed its slab test exactly for the lanes in m
         if (ntri) {
+            if (COUNT && lane == 0) cnt.c[kWaveTriTests] += ntri;
+            const bool in = (m >> lane) & 1ull;
             for (uint32_t k = 0; k < ntri; ++k) {
                 const uint32_t ti = link + k;
                 const Tri T = S.tris[ti];
                 float t;
                 const bool h = tri_t(T.a, T.b, T.c, cs, r, t);
                 if (ANY) {
-                    const bool live = in & !occ;
-                    if (COUNT && live) cnt.c[kTri]++;
-                    occ = occ | (live & h);
+                    if (COUNT && ((m & live) >> lane) & 1ull) cnt.c[kTri]++;
+                    live &= ~(wballot(h) & m);
                 } else {
                     if (COUNT && in) cnt.c[kTri]++;
                     const bool u = in & h & (t < sc_t);
@@ -202,28 +208,31 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, uns
                     sc_tri = u ? ti : sc_tri;
                 }
             }
-            if (ANY && (ballot(!occ) & mask) == 0) return;
+            if (ANY && (live & mask) == 0) return;
         } else {
-            const float4 c0 = S.nodes[2 * link], c1 = S.nodes[2 * link + 1];
-            const float4 c2 = S.nodes[2 * link + 2], c3 = S.nodes[2 * link + 3];
-            const unsigned long long ml = ballot(in && slab<FAST>(c0, c1, r));
-            const unsigned long long mr = ballot(in && slab<FAST>(c2, c3, r));
+            if (COUNT && lane == 0) cnt.c[kWaveNodeTests]++;
+            const NodePair P = pairs[link >> 1];
+            const unsigned long long ml = wballot(slab<FAST>(P.l0, P.l1, r)) & m;
+            const unsigned long long mr = wballot(slab<FAST>(P.r0, P.r1, r)) & m;
+            const bool in = COUNT && ((m >> lane) & 1ull);
             if (COUNT && in) cnt.c[kSlab]++;               // left child's test
             if (COUNT && !ANY && in) cnt.c[kSlab]++;       // right child's (closest: always reached)
             if (ml) {
                 if (mr || (COUNT && ANY)) {                // any-hit COUNT: right is counted at pop
-                    sN[sp] = link + 1;
-                    sM[sp] = mr;
+                    stk[sp] = make_uint4(__float_as_uint(P.r0.w), __float_as_uint(P.r1.w),
+                                         static_cast<uint32_t>(mr), static_cast<uint32_t>(mr >> 32));
                     if (COUNT && ANY) sT[sp] = m;
                     ++sp;
                 }
-                node = link;
+                link = __float_as_uint(P.l0.w);
+                ntri = __float_as_uint(P.l1.w);
                 m = ml;
                 continue;
             }
             if (COUNT && ANY && in) cnt.c[kSlab]++;        // right child's test, reached now
             if (mr) {
-                node = link + 1;
+                link = __float_as_uint(P.r0.w);
+                ntri = __float_as_uint(P.r1.w);
                 m = mr;
                 continue;
             }
@@ -232,10 +241,11 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, uns
         for (;;) {
             if (sp == 0) return;
             --sp;
-            node = uni(sN[sp]);
-            m = uni64(sM[sp]);
+            const uint4 e = stk[sp];
+            link = uni(e.x);
+            ntri = uni(e.y);
+            m = (static_cast<unsigned long long>(uni(e.w)) << 32) | uni(e.z);
             if (ANY) {
-                const unsigned long long live = ballot(!occ);
                 if (COUNT) {
                     const unsigned long long tested = uni64(sT[sp]);
                     if (((tested & live) >> lane) & 1ull) cnt.c[kSlab]++;
@@ -311,16 +321,27 @@ __device__ __forceinline__ uint32_t q8(float c) {
 
 // Renderer::RenderPixel (source/Renderer.cpp:100-182) for a 16x16 tile per workgroup.
 template <bool COUNT>
+// Timing-only ablation switches (results are wrong when set; never in a product build).
+#ifndef RTX_ABL_PPLANE
+#define RTX_ABL_PPLANE 0
+#endif
+#ifndef RTX_ABL_PMESH
+#define RTX_ABL_PMESH 0
+#endif
+#ifndef RTX_ABL_SPLANE
+#define RTX_ABL_SPLANE 0
+#endif
+#ifndef RTX_ABL_SMESH
+#define RTX_ABL_SMESH 0
+#endif
 #ifndef RTX_MIN_WAVES_PER_EU
 #define RTX_MIN_WAVES_PER_EU 1
 #endif
 __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_render_kernel(const DevScene S, const FrameArgs F) {
-    __shared__ uint32_t stkN[kBlockThreads / 64][kStackDepth];
-    __shared__ unsigned long long stkM[kBlockThreads / 64][kStackDepth];
+    __shared__ uint4 stkE[kBlockThreads / 64][kStackDepth];
     __shared__ unsigned long long stkT[COUNT ? kBlockThreads / 64 : 1][kStackDepth];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint32_t* sN = stkN[wave];
-    unsigned long long* sM = stkM[wave];
+    uint4* stk = stkE[wave];
     unsigned long long* sT = stkT[COUNT ? wave : 0];
 
     const uint32_t view = blockIdx.z;
@@ -366,7 +387,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         best_kind = b ? 1u : best_kind;
         best_idx = b ? i : best_idx;
     }
-    for (uint32_t i = 0; i < S.n_planes; ++i) {
+    for (uint32_t i = 0; i < ((RTX_ABL_PPLANE) ? 0u : S.n_planes); ++i) {
         const float4 p0 = S.planes[2 * i], p1 = S.planes[2 * i + 1];
         if (COUNT && valid) cnt.c[kPlane]++;
         float t;
@@ -377,14 +398,14 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         best_kind = b ? 2u : best_kind;
         best_idx = b ? i : best_idx;
     }
-    for (uint32_t mi = 0; mi < S.n_meshes; ++mi) {
+    for (uint32_t mi = 0; mi < ((RTX_ABL_PMESH) ? 0u : S.n_meshes); ++mi) {
         const int4 M = S.meshes[mi];
         uint32_t sc_tri = 0;
-        bool unused = false;
+        unsigned long long unused = 0;
         if (fast)
-            mesh_traverse<false, true, COUNT>(S, M, vr, active, lane, sN, sM, sT, sc_t, sc_tri, unused, cnt);
+            mesh_traverse<false, true, COUNT>(S, M, vr, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
         else
-            mesh_traverse<false, false, COUNT>(S, M, vr, active, lane, sN, sM, sT, sc_t, sc_tri, unused, cnt);
+            mesh_traverse<false, false, COUNT>(S, M, vr, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
         if (sc_t < best_t) { best_t = sc_t; best_kind = 3; best_idx = sc_tri; }
     }
 
@@ -428,37 +449,34 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
             lx /= mag; ly /= mag; lz /= mag;
             bool occ = false;
             if (F.shadows) {
-                // Scene::DoesHit (Scene.cpp:68-96) on Ray{originOffset, l, 1e-4, |l|}
+                // Scene::DoesHit (Scene.cpp:68-96) on Ray{originOffset, l, 1e-4, |l|}; `live` =
+                // lanes still without an occluder (first hit wins, order irrelevant for a bool)
                 const Ray sr = make_ray(oox, ooy, ooz, lx, ly, lz, 0.0001f, mag);
-                const bool sfast = (ballot(did && !finite_inv(sr)) == 0);
+                unsigned long long live = hitmask;
+                const bool sfast = (wballot(did && !finite_inv(sr)) == 0);
                 if (COUNT && did) cnt.c[kShadow]++;
-                for (uint32_t i = 0; i < S.n_spheres; ++i) {
-                    if ((ballot(did && !occ)) == 0) break;
+                for (uint32_t i = 0; i < S.n_spheres && live; ++i) {
                     const float4 s = S.spheres[i];
-                    const bool live = did && !occ;
-                    if (COUNT && live) cnt.c[kSphere]++;
+                    if (COUNT && ((live >> lane) & 1ull)) cnt.c[kSphere]++;
                     float t;
-                    occ = occ || (live && sphere_t(s, sr, t));
+                    live &= ~wballot(sphere_t(s, sr, t));
                 }
-                for (uint32_t i = 0; i < S.n_planes; ++i) {
-                    if ((ballot(did && !occ)) == 0) break;
+                for (uint32_t i = 0; i < ((RTX_ABL_SPLANE) ? 0u : S.n_planes) && live; ++i) {
                     const float4 p0 = S.planes[2 * i], p1 = S.planes[2 * i + 1];
-                    const bool live = did && !occ;
-                    if (COUNT && live) cnt.c[kPlane]++;
+                    if (COUNT && ((live >> lane) & 1ull)) cnt.c[kPlane]++;
                     float t;
-                    occ = occ || (live && plane_t(p0, p1, sr, t));
+                    live &= ~wballot(plane_t(p0, p1, sr, t));
                 }
-                for (uint32_t mi = 0; mi < S.n_meshes; ++mi) {
-                    const unsigned long long live = ballot(did && !occ);
-                    if (live == 0) break;
+                for (uint32_t mi = 0; mi < ((RTX_ABL_SMESH) ? 0u : S.n_meshes) && live; ++mi) {
                     float st = 0.f;
                     uint32_t stri = 0;
                     if (sfast)
-                        mesh_traverse<true, true, COUNT>(S, S.meshes[mi], sr, live, lane, sN, sM, sT, st, stri, occ, cnt);
+                        mesh_traverse<true, true, COUNT>(S, S.meshes[mi], sr, live, lane, stk, sT, st, stri, live, cnt);
                     else
-                        mesh_traverse<true, false, COUNT>(S, S.meshes[mi], sr, live, lane, sN, sM, sT, st, stri, occ,
+                        mesh_traverse<true, false, COUNT>(S, S.meshes[mi], sr, live, lane, stk, sT, st, stri, live,
                                                           cnt);
                 }
+                occ = did && !((live >> lane) & 1ull);
             }
             if (!did) continue;
             if (occ) {
@@ -670,12 +688,22 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
             tri.push_back(f4(v2[0] - v0[0], v2[1] - v0[1], v2[2] - v0[2], n[2]));
             tri.push_back(f4(bits(m.material), 0.f, 0.f, 0.f));
         }
+        uint32_t root = 0;
         if (m.n_nodes) {
             if (!m.nodes) return fail(c, RTX_E_INVALID, "mesh nodes missing");
             std::string why;
             if (!bvh_depth_ok(m, why)) return fail(c, RTX_E_INVALID, why);
-            for (uint32_t k = 0; k < m.n_nodes; ++k) {
-                const rtx_bvh_node& nd = m.nodes[k];
+            // Re-lay the tree out for the device: the root at an odd slot, every child pair
+            // (left, left + 1) at an even slot so one 64-B scalar load fetches both boxes.
+            // Only the numbering changes; the tree and the left-then-right order do not.
+            if ((nodes.size() / 2) % 2 == 0) { nodes.push_back(f4(0, 0, 0, 0)); nodes.push_back(f4(0, 0, 0, 0)); }
+            root = static_cast<uint32_t>(nodes.size() / 2);
+            std::vector<std::pair<uint32_t, uint32_t>> work{{0u, root}};   // (mesh-local node, device slot)
+            nodes.resize(nodes.size() + 2);
+            while (!work.empty()) {
+                const auto [src, dst] = work.back();
+                work.pop_back();
+                const rtx_bvh_node& nd = m.nodes[src];
                 uint32_t link, cnt;
                 if (nd.idx_count > 0) {
                     if (nd.first_idx % 3 || nd.idx_count % 3 || nd.first_idx + nd.idx_count > m.n_indices)
@@ -683,14 +711,18 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
                     link = tri0 + nd.first_idx / 3;
                     cnt = nd.idx_count / 3;
                 } else {
-                    link = node0 + nd.left_node;
+                    link = static_cast<uint32_t>(nodes.size() / 2);   // even: sizes stay even after the root
                     cnt = 0;
+                    nodes.resize(nodes.size() + 4);
+                    work.push_back({nd.left_node + 1, link + 1});
+                    work.push_back({nd.left_node, link});
                 }
-                nodes.push_back(f4(nd.min[0], nd.min[1], nd.min[2], bits(link)));
-                nodes.push_back(f4(nd.max[0], nd.max[1], nd.max[2], bits(cnt)));
+                nodes[2 * dst] = f4(nd.min[0], nd.min[1], nd.min[2], bits(link));
+                nodes[2 * dst + 1] = f4(nd.max[0], nd.max[1], nd.max[2], bits(cnt));
             }
         }
-        meshes.push_back(make_int4(static_cast<int>(node0), static_cast<int>(m.n_nodes), m.cull_mode, m.material));
+        meshes.push_back(make_int4(static_cast<int>(root), static_cast<int>(m.n_nodes), m.cull_mode, m.material));
+        (void)node0;
     }
     for (uint32_t i = 0; i < s->n_lights; ++i) {
         const rtx_light& l = s->lights[i];
@@ -917,8 +949,18 @@ extern "C" int rtx_time_frames(rtx_ctx* c, const rtx_camera* cam, const rtx_rend
 }
 
 // Instrumented variant: the same traversal with per-lane work counters.
+extern "C" int rtx_count_work_ex(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* counts,
+                                 int n_counts);
+
 extern "C" int rtx_count_work(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* counts) {
-    if (!counts) return RTX_E_INVALID;
+    return rtx_count_work_ex(c, cam, p, counts, kModelCounters);
+}
+
+// Same with the per-wave diagnostic counters appended (up to kNumCounters values).
+extern "C" int rtx_count_work_ex(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* counts,
+                                 int n_counts) {
+    if (!counts || n_counts <= 0) return RTX_E_INVALID;
+    if (n_counts > kNumCounters) n_counts = kNumCounters;
     FrameArgs F;
     dim3 grid;
     int rc = prepare(c, cam, 1, p, false, F, grid);
@@ -926,9 +968,11 @@ extern "C" int rtx_count_work(rtx_ctx* c, const rtx_camera* cam, const rtx_rende
     HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long) * kNumCounters, c->stream));
     rc = launch(c, F, grid, true);
     if (rc != RTX_OK) return rc;
-    HIP_TRY(c, hipMemcpyAsync(counts, c->d_counters, sizeof(unsigned long long) * kNumCounters,
-                              hipMemcpyDeviceToHost, c->stream));
+    unsigned long long tmp[kNumCounters];
+    HIP_TRY(c, hipMemcpyAsync(tmp, c->d_counters, sizeof(unsigned long long) * kNumCounters, hipMemcpyDeviceToHost,
+                              c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < n_counts; ++k) counts[k] = tmp[k];
     remember(c, p, 1, false);
     return RTX_OK;
 }

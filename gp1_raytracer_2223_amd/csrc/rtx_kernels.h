@@ -14,8 +14,12 @@ constexpr int kTile = 16;
 // Work counters (SURVEY §8(d) cost model; same order as the oracle's).
 enum Counter {
     kPixels = 0, kSphere, kPlane, kSlab, kTri, kHit, kShadow, kOccluded,
-    kShadeBase, kShadeLambert, kShadePhong, kShadeCT, kNumCounters
+    kShadeBase, kShadeLambert, kShadePhong, kShadeCT,
+    // diagnostics (not part of the FLOP model): per-WAVE packet work, counted once per
+    // wave by lane 0 — node-pair tests and triangle tests the wave executed
+    kWaveNodeTests, kWaveTriTests, kNumCounters
 };
+constexpr int kModelCounters = 12;
 
 // HBM scene image, every record 16-byte aligned so a wave-uniform index
 // becomes one s_load_dwordx4/x8 (scalar cache) instead of 64 vector loads:

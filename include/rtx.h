@@ -214,6 +214,10 @@ int rtx_scene_bytes(const rtx_ctx* ctx, uint64_t* bytes);
  * shade_lambert, shade_phong, shade_ct — the SURVEY §8(d) FLOP model).  Not timed. */
 int rtx_count_work(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
                    uint64_t* counts12);
+/* Same, plus diagnostics appended after the 12 model counters: [12] node-pair tests and
+ * [13] triangle tests executed per WAVE (packet work, one count per wave per step). */
+int rtx_count_work_ex(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
+                      uint64_t* counts, int n_counts);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,114 @@
+// validate_fastdiv.hip — exhaustive / randomized proof-by-test of the cheap
+// correctly-rounded reciprocal and quotient used by the render kernel (csrc/rtx_fastdiv.h)
+// against the compiler's IEEE-correct 1.f/x and a/b on THIS hardware (gfx950).
+//
+//   rcp:  all 2^32 bit patterns; inside the fast domain the result must equal 1.f/x
+//   div:  2^32 random (a, b) pairs over the fast domain + 2^30 near-halfway pairs
+//         (a = b*q with q's low bits forced to produce ties after rounding)
+// Build+run on the GPU box:  hipcc --offload-arch=gfx950 -O3 -ffp-contract=off ... && ./a.out
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include "rtx_fastdiv.h"
+
+__global__ void k_rcp(unsigned long long* bad, unsigned long long* tested, unsigned* first) {
+    const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long nb = 0, nt = 0;
+    for (uint64_t u = tid; u < (1ull << 32); u += nthreads) {
+        const float x = __uint_as_float(static_cast<uint32_t>(u));
+        if (!rtxd::fast_rcp_ok(x)) continue;
+        ++nt;
+        const float ref = 1.f / x;
+        const float got = rtxd::rcp_rn(x);
+        if (__float_as_uint(ref) != __float_as_uint(got)) {
+            ++nb;
+            atomicMin(first, static_cast<uint32_t>(u));
+        }
+    }
+    atomicAdd(bad, nb);
+    atomicAdd(tested, nt);
+}
+
+__device__ __forceinline__ uint32_t hash32(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+    return static_cast<uint32_t>(x);
+}
+
+__global__ void k_div(uint64_t n, uint64_t seed, int mode, unsigned long long* bad, unsigned long long* tested,
+                      uint32_t* ex) {
+    const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long nb = 0, nt = 0;
+    for (uint64_t i = tid; i < n; i += nthreads) {
+        const uint32_t h1 = hash32(seed * 0x9E3779B97F4A7C15ull + 2 * i);
+        const uint32_t h2 = hash32(seed * 0x9E3779B97F4A7C15ull + 2 * i + 1);
+        float a, b;
+        if (mode == 0) {
+            // random significands, exponents spread over the fast domain
+            a = __uint_as_float((h1 & 0x807fffffu) | ((64u + (h1 >> 8) % 128u) << 23));
+            b = __uint_as_float((h2 & 0x807fffffu) | ((64u + (h2 >> 9) % 128u) << 23));
+        } else {
+            // near-halfway quotients: q with random significand, a = RN(b*q) nudged by
+            // +-1 ulp, which puts a/b within a few ulp/2^24 of a rounding boundary
+            b = __uint_as_float((h2 & 0x807fffffu) | (127u << 23));
+            const float q = __uint_as_float((h1 & 0x007fffffu) | ((120u + (h1 >> 29)) << 23));
+            const uint32_t ab = __float_as_uint(b * q) + ((h1 >> 23) & 1 ? 1u : 0xffffffffu);
+            a = __uint_as_float(ab);
+        }
+        const float y = rtxd::rcp_rn(b);
+        if (!rtxd::fast_rcp_ok(b) || !rtxd::fast_div_ok(a, b)) continue;
+        ++nt;
+        const float ref = a / b;
+        const float got = rtxd::div_rn(a, b, y);
+        if (__float_as_uint(ref) != __float_as_uint(got)) {
+            ++nb;
+            ex[0] = __float_as_uint(a);
+            ex[1] = __float_as_uint(b);
+        }
+    }
+    atomicAdd(bad, nb);
+    atomicAdd(tested, nt);
+}
+
+int main() {
+    unsigned long long *bad, *tested;
+    unsigned* first;
+    uint32_t* ex;
+    if (hipMalloc(&bad, 8) || hipMalloc(&tested, 8) || hipMalloc(&first, 4) || hipMalloc(&ex, 8)) return 2;
+    unsigned long long hb = 0, ht = 0;
+    unsigned hf = 0xffffffffu;
+    (void)hipMemcpy(bad, &hb, 8, hipMemcpyHostToDevice);
+    (void)hipMemcpy(tested, &ht, 8, hipMemcpyHostToDevice);
+    (void)hipMemcpy(first, &hf, 4, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_rcp, dim3(8192), dim3(256), 0, 0, bad, tested, first);
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&ht, tested, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&hf, first, 4, hipMemcpyDeviceToHost);
+    std::printf("{\"check\": \"rcp exhaustive\", \"tested\": %llu, \"mismatches\": %llu, \"first_bad_bits\": \"0x%08x\"}\n",
+                ht, hb, hf);
+    int rc = hb ? 1 : 0;
+    for (int mode = 0; mode < 2; ++mode) {
+        for (uint64_t seed = 1; seed <= 4; ++seed) {
+            hb = ht = 0;
+            uint32_t hex[2] = {0, 0};
+            (void)hipMemcpy(bad, &hb, 8, hipMemcpyHostToDevice);
+            (void)hipMemcpy(tested, &ht, 8, hipMemcpyHostToDevice);
+            (void)hipMemcpy(ex, hex, 8, hipMemcpyHostToDevice);
+            hipLaunchKernelGGL(k_div, dim3(8192), dim3(256), 0, 0, 1ull << 30, seed, mode, bad, tested, ex);
+            (void)hipDeviceSynchronize();
+            (void)hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(&ht, tested, 8, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(hex, ex, 8, hipMemcpyDeviceToHost);
+            std::printf("{\"check\": \"div %s seed %llu\", \"tested\": %llu, \"mismatches\": %llu, "
+                        "\"example\": [\"0x%08x\", \"0x%08x\"]}\n",
+                        mode ? "near-halfway" : "random", (unsigned long long)seed, ht, hb, hex[0], hex[1]);
+            rc |= hb ? 1 : 0;
+        }
+    }
+    return rc;
+}
