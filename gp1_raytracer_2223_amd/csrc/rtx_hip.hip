@@ -18,6 +18,7 @@
 
 #include <cfloat>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -321,6 +322,9 @@ __device__ __forceinline__ uint32_t q8(float c) {
 
 // Renderer::RenderPixel (source/Renderer.cpp:100-182) for a 16x16 tile per workgroup.
 template <bool COUNT>
+#ifndef RTX_STAMPS
+#define RTX_STAMPS 0
+#endif
 // Timing-only ablation switches (results are wrong when set; never in a product build).
 #ifndef RTX_ABL_PPLANE
 #define RTX_ABL_PPLANE 0
@@ -341,19 +345,34 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     __shared__ uint4 stkE[kBlockThreads / 64][kStackDepth];
     __shared__ unsigned long long stkT[COUNT ? kBlockThreads / 64 : 1][kStackDepth];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+#if RTX_STAMPS
+    // diagnostic build only: per-wave {start, end, hw_id} in the counters buffer
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     uint4* stk = stkE[wave];
     unsigned long long* sT = stkT[COUNT ? wave : 0];
 
-    const uint32_t view = blockIdx.z;
+    // Work unit = one 16x16 tile of one view.  The dispatch order is a permutation
+    // (F.order, null = identity) that rtx_reorder_kernel derives from the previous frame's
+    // measured per-tile cost, so the heavy tiles start first and do not form a tail;
+    // which tile a block renders never changes a pixel's value.
+    const uint32_t b = blockIdx.x;
+    const uint32_t tile = F.order ? F.order[b] : b;
+    const uint32_t per_view = F.tiles_x * F.tiles_y;
+    const uint32_t view = tile / per_view;
+    const uint32_t rem = tile - view * per_view;
+    const uint32_t bx = rem % F.tiles_x;
     const ViewCam& V = F.cam[view];
-    uint32_t gy = blockIdx.y;
+    uint32_t gy = rem / F.tiles_x;
+    unsigned long long t_block0 = 0;
+    if (F.cost) t_block0 = __builtin_amdgcn_s_memtime();
     if (F.groups_per_stripe) {
         // view v owns the stripes s with s % step == (first - v) mod step (rtx.h)
         const uint32_t first = (F.stripe_first + F.stripe_step - view % F.stripe_step) % F.stripe_step;
         const uint32_t k = gy / F.groups_per_stripe, sub = gy % F.groups_per_stripe;
         gy = (first + k * F.stripe_step) * F.groups_per_stripe + sub;
     }
-    const int px = static_cast<int>(blockIdx.x * kTile + (wave & 1u) * 8u + (lane & 7u));
+    const int px = static_cast<int>(bx * kTile + (wave & 1u) * 8u + (lane & 7u));
     const int py = static_cast<int>(gy * kTile + (wave >> 1) * 8u + (lane >> 3));
     const bool valid = px < static_cast<int>(F.width) && py < static_cast<int>(F.height);
     Counts cnt;
@@ -526,6 +545,23 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
             F.out_rgb[3 * o] = fr; F.out_rgb[3 * o + 1] = fg; F.out_rgb[3 * o + 2] = fb;
         }
     }
+    if (F.cost && lane == 0) {
+        const unsigned long long dt = (__builtin_amdgcn_s_memtime() - t_block0) >> 4;
+        atomicMax(&F.cost[tile], static_cast<uint32_t>(dt < 0xffffffffull ? dt : 0xffffffffull));
+    }
+#if RTX_STAMPS
+    if (lane == 0 && F.stamps) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        const size_t w = static_cast<size_t>(tile) * 4 + wave;
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        F.stamps[3 * w] = t_start;
+        F.stamps[3 * w + 1] = t_end;
+        F.stamps[3 * w + 2] = (static_cast<unsigned long long>(xcc) << 32) | hw;
+    }
+#endif
     if (COUNT) {
         for (int k = 0; k < kNumCounters; ++k)
             if (cnt.c[k]) atomicAdd(&F.counters[k], static_cast<unsigned long long>(cnt.c[k]));
@@ -534,6 +570,47 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
 
 template __global__ void rtx_render_kernel<false>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<true>(const DevScene, const FrameArgs);
+
+// Next frames' dispatch order from this frame's per-tile cost: heaviest first, STABLE
+// within a cost class so that tiles rendered together stay spatial neighbours (they walk
+// the same BVH nodes: scalar-cache locality).  One workgroup: each thread owns a
+// contiguous run of tiles; counts[class][thread] + an exclusive scan in (class, thread)
+// order give every tile its slot.  Clears the costs it read.
+__global__ void __launch_bounds__(kReorderThreads) rtx_reorder_kernel(uint32_t* __restrict__ cost,
+                                                                      uint32_t* __restrict__ order, uint32_t n) {
+    __shared__ uint32_t cnt[kCostBuckets][kReorderThreads];
+    __shared__ uint32_t tot[kCostBuckets];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t per = (n + kReorderThreads - 1) / kReorderThreads;
+    const uint32_t lo = tid * per, hi = (lo + per < n) ? lo + per : n;
+    auto bucket = [](uint32_t cst) -> uint32_t {   // heavier -> smaller class
+        const uint32_t lg = cst ? 32u - static_cast<uint32_t>(__builtin_clz(cst)) : 0u;   // 0..32
+        const uint32_t half = (cst && lg >= 2) ? ((cst >> (lg - 2)) & 1u) : 0u;
+        uint32_t k = 2u * lg + half;                                                     // 0..65
+        k = k > 2u * 6u ? k - 2u * 6u : 0u;        // costs below 2^6 (x16 cycles) share a class
+        return (kCostBuckets - 1) - (k < kCostBuckets ? k : kCostBuckets - 1);
+    };
+    for (int k = 0; k < kCostBuckets; ++k) cnt[k][tid] = 0;
+    for (uint32_t t = lo; t < hi; ++t) cnt[bucket(cost[t])][tid]++;
+    __syncthreads();
+    if (tid < kCostBuckets) {   // exclusive scan of one class row
+        uint32_t acc = 0;
+        for (int j = 0; j < kReorderThreads; ++j) { const uint32_t v = cnt[tid][j]; cnt[tid][j] = acc; acc += v; }
+        tot[tid] = acc;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (int k = 0; k < kCostBuckets; ++k) { const uint32_t v = tot[k]; tot[k] = acc; acc += v; }
+    }
+    __syncthreads();
+    for (uint32_t t = lo; t < hi; ++t) {
+        const uint32_t k = bucket(cost[t]);
+        order[tot[k] + cnt[k][tid]++] = t;
+    }
+    __syncthreads();
+    for (uint32_t t = lo; t < hi; ++t) cost[t] = 0;
+}
 
 // ====================================================================== host side
 struct rtx_ctx {
@@ -552,6 +629,15 @@ struct rtx_ctx {
     size_t px_cap = 0, rgb_cap = 0;
     unsigned long long* d_counters = nullptr;
     // last render
+    // cost-ordered tile dispatch
+    uint32_t* d_order = nullptr;
+    uint32_t* d_cost = nullptr;
+    uint32_t sched_cap = 0;
+    std::string sched_key;
+    bool sched_ready = false;
+    bool sched_enabled = true;
+    uint64_t sched_frame = 0;
+    uint64_t scene_gen = 0;
     rtx_render_params last{};
     int last_views = 1;
     bool last_valid = false, last_rgb = false;
@@ -610,6 +696,8 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) { delete c; return RTX_E_DEVICE; }
     if (device_id < 0 || device_id >= n) { delete c; return RTX_E_INVALID; }
     c->device = device_id;
+    // RTX_TILE_ORDER=0 disables cost-ordered tile dispatch (identity order every frame)
+    if (const char* e = std::getenv("RTX_TILE_ORDER")) c->sched_enabled = std::strcmp(e, "0") != 0;
     if (hipSetDevice(device_id) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
@@ -629,6 +717,8 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     (void)hipFree(c->d_px);
     (void)hipFree(c->d_rgb);
     (void)hipFree(c->d_counters);
+    (void)hipFree(c->d_order);
+    (void)hipFree(c->d_cost);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -772,6 +862,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     d.n_tris = static_cast<uint32_t>(tri.size() / 4); d.n_nodes = static_cast<uint32_t>(nodes.size() / 2);
     c->dev = d;
     c->has_scene = true;
+    ++c->scene_gen;
     return RTX_OK;
 }
 
@@ -832,20 +923,62 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         gy = owned * gps;
     }
     F.tiles_x = (p->width + kTile - 1) / kTile;
+    F.tiles_y = gy;
     F.out_px = c->d_px;
     F.out_rgb = want_rgb ? c->d_rgb : nullptr;
     F.counters = c->d_counters;
-    grid = dim3(F.tiles_x, gy, static_cast<uint32_t>(n_views));
+    const uint32_t ntiles = F.tiles_x * gy * static_cast<uint32_t>(n_views);
+    grid = dim3(ntiles, 1, 1);
+    // Cost-ordered dispatch (see the kernel): keep one order/cost pair per launch shape.
+    if (ntiles > c->sched_cap) {
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_order);
+        (void)hipFree(c->d_cost);
+        c->d_order = nullptr;
+        c->d_cost = nullptr;
+        c->sched_cap = 0;
+        HIP_TRY(c, hipMalloc(&c->d_order, ntiles * 4));
+        HIP_TRY(c, hipMalloc(&c->d_cost, ntiles * 4));
+        c->sched_cap = ntiles;
+        c->sched_key.clear();
+    }
+    std::string key = std::to_string(p->width) + "x" + std::to_string(p->height) + "v" + std::to_string(n_views) +
+                      "s" + std::to_string(p->stripe_rows) + "/" + std::to_string(p->stripe_first) + "/" +
+                      std::to_string(p->stripe_step) + "g" + std::to_string(c->scene_gen) + "m" +
+                      std::to_string(p->lighting_mode) + std::to_string(p->shadows_enabled);
+    if (key != c->sched_key) {   // new shape or scene: identity order, fresh costs
+        c->sched_key = key;
+        c->sched_ready = false;
+        c->sched_frame = 0;
+        HIP_TRY(c, hipMemsetAsync(c->d_cost, 0, ntiles * 4, c->stream));
+    }
+    // Measure tile costs on the first frame of a shape and then every kSchedPeriod frames;
+    // the frames in between reuse the last order and pay nothing for scheduling.
+    const bool measure = c->sched_enabled && (!c->sched_ready || c->sched_frame % kSchedPeriod == 0);
+    ++c->sched_frame;
+    F.order = (c->sched_enabled && c->sched_ready) ? c->d_order : nullptr;
+    F.cost = measure ? c->d_cost : nullptr;
     return RTX_OK;
 }
 
 int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
     if (grid.x == 0 || grid.y == 0) return RTX_OK;
-    if (count)
-        hipLaunchKernelGGL(rtx_render_kernel<true>, grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
-    else
-        hipLaunchKernelGGL(rtx_render_kernel<false>, grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
+    if (count) {
+        FrameArgs G = F;   // the instrumented variant neither reads nor feeds the schedule
+        G.order = nullptr;
+        G.cost = nullptr;
+        hipLaunchKernelGGL(rtx_render_kernel<true>, grid, dim3(kBlockThreads), 0, c->stream, c->dev, G);
+        HIP_TRY(c, hipGetLastError());
+        return RTX_OK;
+    }
+    hipLaunchKernelGGL(rtx_render_kernel<false>, grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
     HIP_TRY(c, hipGetLastError());
+    if (F.cost) {
+        hipLaunchKernelGGL(rtx_reorder_kernel, dim3(1), dim3(kReorderThreads), 0, c->stream, F.cost, c->d_order,
+                           grid.x);
+        HIP_TRY(c, hipGetLastError());
+        c->sched_ready = true;
+    }
     return RTX_OK;
 }
 
@@ -976,3 +1109,26 @@ extern "C" int rtx_count_work_ex(rtx_ctx* c, const rtx_camera* cam, const rtx_re
     remember(c, p, 1, false);
     return RTX_OK;
 }
+
+#if RTX_STAMPS
+// Diagnostic build only: render once with per-wave {start, end, hw ids} stamps.
+extern "C" int rtx_debug_stamps(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* out,
+                                uint64_t capacity, uint64_t* n_waves) {
+    FrameArgs F;
+    dim3 grid;
+    int rc = prepare(c, cam, 1, p, false, F, grid);
+    if (rc != RTX_OK) return rc;
+    const uint64_t nw = static_cast<uint64_t>(grid.x) * grid.y * grid.z * 4;
+    *n_waves = nw;
+    if (3 * nw > capacity) return RTX_E_INVALID;
+    unsigned long long* d = nullptr;
+    HIP_TRY(c, hipMalloc(&d, 3 * nw * 8));
+    F.stamps = d;
+    rc = launch(c, F, grid, false);
+    if (rc != RTX_OK) return rc;
+    HIP_TRY(c, hipMemcpyAsync(out, d, 3 * nw * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    (void)hipFree(d);
+    return RTX_OK;
+}
+#endif

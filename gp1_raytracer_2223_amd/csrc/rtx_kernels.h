@@ -10,6 +10,9 @@ namespace rtxd {
 constexpr int kStackDepth = 64;
 constexpr int kBlockThreads = 256;     // 4 waves = a 16 x 16 pixel tile (8 x 8 per wave)
 constexpr int kTile = 16;
+constexpr int kReorderThreads = 256;
+constexpr int kCostBuckets = 32;
+constexpr int kSchedPeriod = 64;      // frames between tile-cost measurements
 
 // Work counters (SURVEY §8(d) cost model; same order as the oracle's).
 enum Counter {
@@ -65,10 +68,13 @@ struct FrameArgs {
     uint32_t rshift, gshift, bshift, amask;
     uint32_t groups_per_stripe;   // stripe_rows / 16 (0 => whole image)
     uint32_t stripe_first, stripe_step;
-    uint32_t tiles_x;
+    uint32_t tiles_x, tiles_y;    // 16x16 tiles per view row / per view column (owned)
+    const uint32_t* __restrict__ order;   // dispatch permutation of the tiles (null = identity)
+    uint32_t* __restrict__ cost;          // per-tile cost of this frame (null = not measured)
     uint32_t* __restrict__ out_px;   // view v at out_px + v * width * height
     float* __restrict__ out_rgb;     // may be null
     unsigned long long* __restrict__ counters;  // COUNT variant only
+    unsigned long long* __restrict__ stamps;    // diagnostic RTX_STAMPS builds only (null otherwise)
 };
 
 }  // namespace rtxd

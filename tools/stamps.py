@@ -1,0 +1,51 @@
+"""Per-wave start/end stamps (diagnostic build, RTX_STAMPS=1): occupancy over time, tail,
+per-XCD balance.  Usage: RTX_HIP_LIB=.../librtx_hip_stamps.so python tools/stamps.py [scene W H]"""
+import ctypes as C
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+from gp1_raytracer_2223_amd import abi  # noqa: E402
+
+lib = abi.load_hip()
+from gp1_raytracer_2223_amd.renderer import DeviceContext  # noqa: E402
+from gp1_raytracer_2223_amd.scene import HostScene  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else "W4_Bunny"
+W = int(sys.argv[2]) if len(sys.argv) > 2 else 1920
+H = int(sys.argv[3]) if len(sys.argv) > 3 else 1080
+lib.rtx_debug_stamps.argtypes = [C.c_void_p, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams),
+                                 C.POINTER(C.c_uint64), C.c_uint64, C.POINTER(C.c_uint64)]
+ctx = DeviceContext(0)
+hs = HostScene(name)
+s, cam = hs.view()
+ctx.upload(s)
+p = abi.make_params(W, H)
+for _ in range(5):
+    ctx.time_frames(cam, p, 20)
+cap = 3 * ((W + 15) // 16) * ((H + 15) // 16) * 4
+buf = np.zeros(cap, np.uint64)
+nw = C.c_uint64()
+abi.check(lib.rtx_debug_stamps(ctx.h, C.byref(cam), C.byref(p), buf.ctypes.data_as(C.POINTER(C.c_uint64)),
+                               cap, C.byref(nw)), "stamps", ctx.h)
+st = buf.reshape(-1, 3)[: nw.value]
+t0 = st[:, 0].min()
+start = (st[:, 0] - t0) / 100.0   # s_memrealtime = 100 MHz -> us
+end = (st[:, 1] - t0) / 100.0
+dur = end - start
+xcc = (st[:, 2] >> 32).astype(int)
+print(f"{name} {W}x{H}: waves {len(st)}  kernel span {end.max():.1f} us  wave dur mean {dur.mean():.2f} "
+      f"p50 {np.median(dur):.2f} p90 {np.percentile(dur, 90):.2f} max {dur.max():.2f} us")
+print(f"  sum of wave-us / span = {dur.sum() / end.max():.0f} concurrent waves on average")
+for q in (10, 25, 50, 75, 90, 99, 100):
+    print(f"  {q:3d}% of waves started by {np.percentile(start, q):7.1f} us, ended by {np.percentile(end, q):7.1f} us")
+tt = np.linspace(0, end.max(), 21)
+conc = [int(((start <= x) & (end > x)).sum()) for x in tt]
+print("  concurrency over time:", conc)
+for x in range(8):
+    sel = xcc == x
+    if sel.any():
+        print(f"  xcc {x}: waves {sel.sum()} busy-us {dur[sel].sum():.0f} last end {end[sel].max():.1f}")
