@@ -1,5 +1,5 @@
 // validate_fastdiv.hip — exhaustive / randomized proof-by-test of the cheap
-// correctly-rounded reciprocal and quotient used by the render kernel (csrc/rtx_fastdiv.h)
+// correctly-rounded reciprocal and quotient used by the render kernel (tools/rtx_fastdiv.h; evaluated, not adopted — see profiles/r01/ablate_history.md)
 // against the compiler's IEEE-correct 1.f/x and a/b on THIS hardware (gfx950).
 //
 //   rcp:  all 2^32 bit patterns; inside the fast domain the result must equal 1.f/x
@@ -49,8 +49,8 @@ __global__ void k_div(uint64_t n, uint64_t seed, int mode, unsigned long long* b
         float a, b;
         if (mode == 0) {
             // random significands, exponents spread over the fast domain
-            a = __uint_as_float((h1 & 0x807fffffu) | ((64u + (h1 >> 8) % 128u) << 23));
-            b = __uint_as_float((h2 & 0x807fffffu) | ((64u + (h2 >> 9) % 128u) << 23));
+            a = __uint_as_float((h1 & 0x807fffffu) | ((67u + (h1 >> 8) % 121u) << 23));
+            b = __uint_as_float((h2 & 0x807fffffu) | ((67u + (h2 >> 9) % 121u) << 23));
         } else {
             // near-halfway quotients: q with random significand, a = RN(b*q) nudged by
             // +-1 ulp, which puts a/b within a few ulp/2^24 of a rounding boundary
