@@ -46,6 +46,35 @@ __device__ __forceinline__ unsigned long long uni64(unsigned long long x) {
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ unsigned long long wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
+// Scene records are immutable for a whole launch: they are read through the constant
+// address space, so every wave-uniform read is an s_load through the scalar cache.  With
+// generic pointers the backend needs a "no clobber" proof for s_load, which any
+// side-effecting instruction on the path (s_memtime for the tile costs) defeats, and the
+// reads silently become per-lane vector loads.
+#define RTX_CONST __attribute__((address_space(4)))
+typedef float cf4 __attribute__((ext_vector_type(4)));
+typedef int ci4 __attribute__((ext_vector_type(4)));
+typedef float cf16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ float4 ldc(const float4* base, uint32_t i) {
+    const cf4 v = ((const RTX_CONST cf4*)base)[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ int4 ldc(const int4* base, uint32_t i) {
+    const ci4 v = ((const RTX_CONST ci4*)base)[i];
+    return make_int4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t ldc(const uint32_t* base, uint32_t i) {
+    return ((const RTX_CONST uint32_t*)base)[i];
+}
+// one 64-byte record (Tri, NodePair): a single s_load_dwordx16 when the index is uniform
+__device__ __forceinline__ void ldc64(const void* base, uint32_t i, float4& a, float4& b, float4& c, float4& d) {
+    const cf16 v = ((const RTX_CONST cf16*)base)[i];
+    a = make_float4(v[0], v[1], v[2], v[3]);
+    b = make_float4(v[4], v[5], v[6], v[7]);
+    c = make_float4(v[8], v[9], v[10], v[11]);
+    d = make_float4(v[12], v[13], v[14], v[15]);
+}
+
 struct Ray {
     float ox, oy, oz, dx, dy, dz, ix, iy, iz, tmin, tmax;
 };
@@ -176,12 +205,11 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, uns
                               unsigned long long& live, Counts& cnt) {
     if (M.y == 0) return;
     const float cs = cull_sign(M.z, ANY);
-    const NodePair* __restrict__ pairs = reinterpret_cast<const NodePair*>(S.nodes);
     unsigned long long m;
     uint32_t link, ntri;
     {
         // root (odd global index; every child pair starts at an even one, 64-B aligned)
-        const float4 b0 = S.nodes[2 * M.x], b1 = S.nodes[2 * M.x + 1];
+        const float4 b0 = ldc(S.nodes, 2 * M.x), b1 = ldc(S.nodes, 2 * M.x + 1);
         if (COUNT && ((mask >> lane) & 1ull)) cnt.c[kSlab]++;
         m = wballot(slab<FAST>(b0, b1, r)) & mask;
         if (m == 0) return;
@@ -196,7 +224,8 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, uns
             const bool in = (m >> lane) & 1ull;
             for (uint32_t k = 0; k < ntri; ++k) {
                 const uint32_t ti = link + k;
-                const Tri T = S.tris[ti];
+                Tri T;
+                ldc64(S.tris, ti, T.a, T.b, T.c, T.d);
                 float t;
                 const bool h = tri_t(T.a, T.b, T.c, cs, r, t);
                 if (ANY) {
@@ -212,7 +241,8 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, uns
             if (ANY && (live & mask) == 0) return;
         } else {
             if (COUNT && lane == 0) cnt.c[kWaveNodeTests]++;
-            const NodePair P = pairs[link >> 1];
+            NodePair P;
+            ldc64(S.nodes, link >> 1, P.l0, P.l1, P.r0, P.r1);
             const unsigned long long ml = wballot(slab<FAST>(P.l0, P.l1, r)) & m;
             const unsigned long long mr = wballot(slab<FAST>(P.r0, P.r1, r)) & m;
             const bool in = COUNT && ((m >> lane) & 1ull);
@@ -266,7 +296,7 @@ struct RGB {
 // the host with the same binary32 operations (BRDF::Lambert, BRDFs.h:14-17).
 __device__ __forceinline__ RGB shade(const DevScene& S, uint32_t mi, float nx, float ny, float nz, float lx, float ly,
                                      float lz, float vx, float vy, float vz, Counts& cnt, bool count) {
-    const float4 m0 = S.materials[3 * mi], m1 = S.materials[3 * mi + 1], m2 = S.materials[3 * mi + 2];
+    const float4 m0 = ldc(S.materials, 3 * mi), m1 = ldc(S.materials, 3 * mi + 1), m2 = ldc(S.materials, 3 * mi + 2);
     const int kind = __float_as_int(m0.x);
     RGB c{0.f, 0.f, 0.f};
     if (kind == RTX_MAT_SOLID_COLOR) {
@@ -357,7 +387,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     // measured per-tile cost, so the heavy tiles start first and do not form a tail;
     // which tile a block renders never changes a pixel's value.
     const uint32_t b = blockIdx.x;
-    const uint32_t tile = F.order ? F.order[b] : b;
+    const uint32_t tile = F.order ? ldc(F.order, b) : b;
     const uint32_t per_view = F.tiles_x * F.tiles_y;
     const uint32_t view = tile / per_view;
     const uint32_t rem = tile - view * per_view;
@@ -396,7 +426,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     float best_t = FLT_MAX, sc_t = FLT_MAX;
     uint32_t best_kind = 0, best_idx = 0;   // kind: 0 none, 1 sphere, 2 plane, 3 triangle
     for (uint32_t i = 0; i < S.n_spheres; ++i) {
-        const float4 s = S.spheres[i];
+        const float4 s = ldc(S.spheres, i);
         if (COUNT && valid) cnt.c[kSphere]++;
         float t;
         const bool h = valid && sphere_t(s, vr, t);
@@ -407,7 +437,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         best_idx = b ? i : best_idx;
     }
     for (uint32_t i = 0; i < ((RTX_ABL_PPLANE) ? 0u : S.n_planes); ++i) {
-        const float4 p0 = S.planes[2 * i], p1 = S.planes[2 * i + 1];
+        const float4 p0 = ldc(S.planes, 2 * i), p1 = ldc(S.planes, 2 * i + 1);
         if (COUNT && valid) cnt.c[kPlane]++;
         float t;
         const bool h = valid && plane_t(p0, p1, vr, t);
@@ -418,7 +448,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         best_idx = b ? i : best_idx;
     }
     for (uint32_t mi = 0; mi < ((RTX_ABL_PMESH) ? 0u : S.n_meshes); ++mi) {
-        const int4 M = S.meshes[mi];
+        const int4 M = ldc(S.meshes, mi);
         uint32_t sc_tri = 0;
         unsigned long long unused = 0;
         if (fast)
@@ -435,17 +465,18 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     if (did) {
         hx = vr.ox + vr.dx * best_t; hy = vr.oy + vr.dy * best_t; hz = vr.oz + vr.dz * best_t;
         if (best_kind == 1) {
-            const float4 s = S.spheres[best_idx];
+            const float4 s = ldc(S.spheres, best_idx);
             nx = hx - s.x; ny = hy - s.y; nz = hz - s.z;
             const float m = sqrtf(nx * nx + ny * ny + nz * nz);   // closestHit.normal.Normalize()
             nx /= m; ny /= m; nz /= m;
-            mat = S.sphere_mat[best_idx];
+            mat = ldc(S.sphere_mat, best_idx);
         } else if (best_kind == 2) {
-            const float4 p0 = S.planes[2 * best_idx], p1 = S.planes[2 * best_idx + 1];
+            const float4 p0 = ldc(S.planes, 2 * best_idx), p1 = ldc(S.planes, 2 * best_idx + 1);
             nx = p1.x; ny = p1.y; nz = p1.z;
             mat = __float_as_uint(p0.w);
         } else {
-            const Tri T = S.tris[best_idx];
+            Tri T;
+            ldc64(S.tris, best_idx, T.a, T.b, T.c, T.d);
             nx = T.a.w; ny = T.b.w; nz = T.c.w;
             mat = __float_as_uint(T.d.x);
         }
@@ -460,7 +491,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         const float oox = hx + nx * 0.0001f, ooy = hy + ny * 0.0001f, ooz = hz + nz * 0.0001f;
         const float vx = -dx, vy = -dy, vz = -dz;
         for (uint32_t li = 0; li < S.n_lights; ++li) {
-            const float4 L0 = S.lights[2 * li], L1 = S.lights[2 * li + 1];
+            const float4 L0 = ldc(S.lights, 2 * li), L1 = ldc(S.lights, 2 * li + 1);
             const int ltype = __float_as_int(L0.w);
             const bool known = (ltype == RTX_LIGHT_POINT || ltype == RTX_LIGHT_DIRECTIONAL);
             float lx = known ? L0.x - oox : 0.f, ly = known ? L0.y - ooy : 0.f, lz = known ? L0.z - ooz : 0.f;
@@ -475,13 +506,13 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                 const bool sfast = (wballot(did && !finite_inv(sr)) == 0);
                 if (COUNT && did) cnt.c[kShadow]++;
                 for (uint32_t i = 0; i < S.n_spheres && live; ++i) {
-                    const float4 s = S.spheres[i];
+                    const float4 s = ldc(S.spheres, i);
                     if (COUNT && ((live >> lane) & 1ull)) cnt.c[kSphere]++;
                     float t;
                     live &= ~wballot(sphere_t(s, sr, t));
                 }
                 for (uint32_t i = 0; i < ((RTX_ABL_SPLANE) ? 0u : S.n_planes) && live; ++i) {
-                    const float4 p0 = S.planes[2 * i], p1 = S.planes[2 * i + 1];
+                    const float4 p0 = ldc(S.planes, 2 * i), p1 = ldc(S.planes, 2 * i + 1);
                     if (COUNT && ((live >> lane) & 1ull)) cnt.c[kPlane]++;
                     float t;
                     live &= ~wballot(plane_t(p0, p1, sr, t));
@@ -490,9 +521,9 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                     float st = 0.f;
                     uint32_t stri = 0;
                     if (sfast)
-                        mesh_traverse<true, true, COUNT>(S, S.meshes[mi], sr, live, lane, stk, sT, st, stri, live, cnt);
+                        mesh_traverse<true, true, COUNT>(S, ldc(S.meshes, mi), sr, live, lane, stk, sT, st, stri, live, cnt);
                     else
-                        mesh_traverse<true, false, COUNT>(S, S.meshes[mi], sr, live, lane, stk, sT, st, stri, live,
+                        mesh_traverse<true, false, COUNT>(S, ldc(S.meshes, mi), sr, live, lane, stk, sT, st, stri, live,
                                                           cnt);
                 }
                 occ = did && !((live >> lane) & 1ull);
