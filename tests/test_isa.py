@@ -1,0 +1,69 @@
+"""Code-generation guards for the render kernel (CPU: reads the gfx950 code object in librtx_hip.so).
+
+These pin properties the kernel's speed depends on and that a harmless-looking source change
+can silently lose (profiles/r01/ablate_history.md, v6: one side-effecting intrinsic turned every
+wave-uniform scene read into a per-lane vector load, +17 % kernel time, with correct output):
+  * wave-uniform BVH node pairs and triangles are fetched with one s_load_dwordx16 each,
+  * per-lane vector loads are confined to the few per-hit gathers (material, hit record),
+  * no scratch, and a VGPR count that keeps >= 7 waves per SIMD.
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+KERNEL = "_Z17rtx_render_kernelILb0EEvN4rtxd8DevSceneENS0_9FrameArgsE"
+
+
+def _code_object(tmp_path, lib):
+    fb = tmp_path / "fatbin.bin"
+    co = tmp_path / "gfx950.co"
+    subprocess.run([f"{LLVM}/llvm-objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib, str(fb)], check=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fb}", f"--output={co}"], check=True)
+    return co
+
+
+@pytest.fixture(scope="module")
+def isa(tmp_path_factory):
+    if not os.path.exists(f"{LLVM}/clang-offload-bundler"):
+        pytest.skip("ROCm LLVM tools not present")
+    from gp1_raytracer_2223_amd import build
+    lib = os.path.join(os.path.dirname(build.__file__), "lib", "librtx_hip.so")
+    if not os.path.exists(lib):
+        build.build_hip()
+    co = _code_object(tmp_path_factory.mktemp("isa"), lib)
+    dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", str(co)], check=True,
+                         capture_output=True, text=True).stdout
+    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", str(co)], check=True, capture_output=True,
+                           text=True).stdout
+    start = dis.index(f"<{KERNEL}>:")
+    body = dis[start:dis.index("s_endpgm", start)]
+    meta = {}
+    for block in notes.split("  - .")[1:]:
+        if re.search(rf"\.name:\s+{KERNEL}\b", block):
+            for key in ("vgpr_count", "sgpr_count", "private_segment_fixed_size"):
+                m = re.search(rf"\.{key}:\s+(\d+)", block)
+                if m:
+                    meta[key] = int(m.group(1))
+    return body, meta
+
+
+def test_uniform_records_are_scalar_loads(isa):
+    body, _ = isa
+    # node pairs + triangles, closest-hit and any-hit, fast and exact slab variants
+    assert body.count("s_load_dwordx16") >= 8, "64-byte BVH/triangle records are no longer scalar loads"
+
+
+def test_vector_loads_only_for_per_lane_gathers(isa):
+    body, _ = isa
+    n = len(re.findall(r"\bglobal_load_", body))
+    assert n <= 20, f"{n} vector loads in the render kernel: scene reads fell back to per-lane loads"
+
+
+def test_registers_and_scratch(isa):
+    _, meta = isa
+    assert meta.get("private_segment_fixed_size") == 0, meta
+    assert meta.get("vgpr_count", 999) <= 72, meta
