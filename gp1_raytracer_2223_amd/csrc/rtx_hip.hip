@@ -101,11 +101,20 @@ __device__ __forceinline__ bool sphere_t(const float4 s, const Ray& r, float& t)
     return !(s.w < perp) && !(t < r.tmin || t > r.tmax);
 }
 
-// HitTest_Plane (Utils.h:84-97)
-__device__ __forceinline__ bool plane_t(const float4 p0, const float4 p1, const Ray& r, float& t) {
-    t = ((p0.x - r.ox) * p1.x + (p0.y - r.oy) * p1.y + (p0.z - r.oz) * p1.z) /
-        (r.dx * p1.x + r.dy * p1.y + r.dz * p1.z);
-    return t >= r.tmin && t < r.tmax;
+// HitTest_Plane (Utils.h:84-97): t = num / den.  With tmin > 0 (every ray here), a hit
+// needs t > 0, i.e. num and den non-zero with the same sign: RN(num/den) carries the exact
+// sign of the quotient, 0/x, x/0 and NaN operands all fail t >= tmin.  `plane_same_sign`
+// lets a wave skip the division when no lane can hit.
+__device__ __forceinline__ float plane_num(const float4 p0, const float4 p1, const Ray& r) {
+    return (p0.x - r.ox) * p1.x + (p0.y - r.oy) * p1.y + (p0.z - r.oz) * p1.z;
+}
+__device__ __forceinline__ float plane_den(const float4 p1, const Ray& r) {
+    return r.dx * p1.x + r.dy * p1.y + r.dz * p1.z;
+}
+// Over-inclusive is harmless (it only decides whether the division runs): equal sign bits
+// admit zeros and NaNs too, which then fail the range test on t.
+__device__ __forceinline__ unsigned long long plane_same_sign(float num, float den) {
+    return ballot((__float_as_int(num) ^ __float_as_int(den)) >= 0);
 }
 
 // HitTest_Triangle (Utils.h:109-184), Möller–Trumbore with the reference's cull rules
@@ -119,12 +128,12 @@ __device__ __forceinline__ bool plane_t(const float4 p0, const float4 p1, const 
 //     v < 0 || (u+v) > 1 <=> max(-v, (u+v)-1) > 0,  t < tmin <=> tmin - t > 0.
 // Cross products use the reduced form {a, -b, c}: identical to Vector3::Cross's
 // UnitX*a - UnitY*b + UnitZ*c for finite inputs up to the sign of a zero, which none of
-// the tests below can observe.  Returns the reject score; accept iff !(score > 0) && t < tmax.
+// the tests below can observe.  Returns the reject score; accept iff !(score > 0) && !(t >= tmax).
 // `cs` is the mesh's cull sign: -1 FrontFaceCulling (reject cullDot < 0), +1
 // BackFaceCulling (reject cullDot > 0), 0 NoCulling (the term 0*cullDot never exceeds 0);
 // shadow rays pass -cs, which is the reference's front/back swap.
-__device__ __forceinline__ bool tri_t(const float4 A, const float4 B, const float4 C, float cs, const Ray& r,
-                                      float& t) {
+__device__ __forceinline__ float tri_t(const float4 A, const float4 B, const float4 C, float cs, const Ray& r,
+                                       float& t) {
     const float cullDot = A.w * r.dx + B.w * r.dy + C.w * r.dz;
     float rej = fmaxf(FLT_EPSILON - fabsf(cullDot), cs * cullDot);
     const float hx = r.dy * C.z - r.dz * C.y;
@@ -142,16 +151,17 @@ __device__ __forceinline__ bool tri_t(const float4 A, const float4 B, const floa
     const float v = ai * (r.dx * qx + r.dy * qy + r.dz * qz);
     rej = fmaxf(rej, fmaxf(-v, (u + v) - 1.f));
     t = ai * (C.x * qx + C.y * qy + C.z * qz);
-    rej = fmaxf(rej, r.tmin - t);
-    return !(rej > 0.f) && !(t >= r.tmax);
+    return fmaxf(rej, r.tmin - t);
 }
 
 // SlabTest_BVH (Utils.h:221-243).  FAST uses v_min/v_max_f32, which differ from std::min/
 // std::max only when an operand is NaN; a NaN slab value needs (box - origin) * inv with
 // an infinite inv component, so FAST is taken only when every live lane's inverse
 // direction is finite (decided once per ray batch with a ballot).
+// Returned as a wave lane mask: one v_cmp per condition straight into SGPRs (a ballot
+// of the && would materialise the bool in a VGPR and compare it again).
 template <bool FAST>
-__device__ __forceinline__ bool slab(const float4 mn, const float4 mx, const Ray& r) {
+__device__ __forceinline__ unsigned long long slab_mask(const float4 mn, const float4 mx, const Ray& r) {
     const float tx1 = (mn.x - r.ox) * r.ix, tx2 = (mx.x - r.ox) * r.ix;
     const float ty1 = (mn.y - r.oy) * r.iy, ty2 = (mx.y - r.oy) * r.iy;
     const float tz1 = (mn.z - r.oz) * r.iz, tz2 = (mx.z - r.oz) * r.iz;
@@ -167,7 +177,7 @@ __device__ __forceinline__ bool slab(const float4 mn, const float4 mx, const Ray
         tMin = smax(tMin, smin(tz1, tz2));
         tMax = smin(tMax, smax(tz1, tz2));
     }
-    return tMax > 0 && tMax >= tMin;
+    return ballot(tMax > 0) & ballot(tMax >= tMin);
 }
 
 __device__ __forceinline__ bool finite_inv(const Ray& r) {
@@ -211,7 +221,7 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, uns
         // root (odd global index; every child pair starts at an even one, 64-B aligned)
         const float4 b0 = ldc(S.nodes, 2 * M.x), b1 = ldc(S.nodes, 2 * M.x + 1);
         if (COUNT && ((mask >> lane) & 1ull)) cnt.c[kSlab]++;
-        m = wballot(slab<FAST>(b0, b1, r)) & mask;
+        m = slab_mask<FAST>(b0, b1, r) & mask;
         if (m == 0) return;
         link = __float_as_uint(b0.w);
         ntri = __float_as_uint(b1.w);
@@ -227,13 +237,13 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, uns
                 Tri T;
                 ldc64(S.tris, ti, T.a, T.b, T.c, T.d);
                 float t;
-                const bool h = tri_t(T.a, T.b, T.c, cs, r, t);
+                const float rej = tri_t(T.a, T.b, T.c, cs, r, t);
                 if (ANY) {
                     if (COUNT && ((m & live) >> lane) & 1ull) cnt.c[kTri]++;
-                    live &= ~(wballot(h) & m);
+                    live &= ~(ballot(!(rej > 0.f)) & ballot(!(t >= r.tmax)) & m);
                 } else {
                     if (COUNT && in) cnt.c[kTri]++;
-                    const bool u = in & h & (t < sc_t);
+                    const bool u = in & !(rej > 0.f) & !(t >= r.tmax) & (t < sc_t);
                     sc_t = u ? t : sc_t;
                     sc_tri = u ? ti : sc_tri;
                 }
@@ -243,8 +253,8 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, uns
             if (COUNT && lane == 0) cnt.c[kWaveNodeTests]++;
             NodePair P;
             ldc64(S.nodes, link >> 1, P.l0, P.l1, P.r0, P.r1);
-            const unsigned long long ml = wballot(slab<FAST>(P.l0, P.l1, r)) & m;
-            const unsigned long long mr = wballot(slab<FAST>(P.r0, P.r1, r)) & m;
+            const unsigned long long ml = slab_mask<FAST>(P.l0, P.l1, r) & m;
+            const unsigned long long mr = slab_mask<FAST>(P.r0, P.r1, r) & m;
             const bool in = COUNT && ((m >> lane) & 1ull);
             if (COUNT && in) cnt.c[kSlab]++;               // left child's test
             if (COUNT && !ANY && in) cnt.c[kSlab]++;       // right child's (closest: always reached)
@@ -439,8 +449,10 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     for (uint32_t i = 0; i < ((RTX_ABL_PPLANE) ? 0u : S.n_planes); ++i) {
         const float4 p0 = ldc(S.planes, 2 * i), p1 = ldc(S.planes, 2 * i + 1);
         if (COUNT && valid) cnt.c[kPlane]++;
-        float t;
-        const bool h = valid && plane_t(p0, p1, vr, t);
+        const float num = plane_num(p0, p1, vr), den = plane_den(p1, vr);
+        if (!(plane_same_sign(num, den) & active)) continue;   // no lane can have t >= tmin > 0
+        const float t = num / den;
+        const bool h = valid & (t >= vr.tmin) & (t < vr.tmax);
         sc_t = h ? t : sc_t;
         const bool b = h && t < best_t;
         best_t = b ? t : best_t;
@@ -514,8 +526,11 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                 for (uint32_t i = 0; i < ((RTX_ABL_SPLANE) ? 0u : S.n_planes) && live; ++i) {
                     const float4 p0 = ldc(S.planes, 2 * i), p1 = ldc(S.planes, 2 * i + 1);
                     if (COUNT && ((live >> lane) & 1ull)) cnt.c[kPlane]++;
-                    float t;
-                    live &= ~wballot(plane_t(p0, p1, sr, t));
+                    const float num = plane_num(p0, p1, sr), den = plane_den(p1, sr);
+                    const unsigned long long cand = plane_same_sign(num, den) & live;
+                    if (!cand) continue;
+                    const float t = num / den;
+                    live &= ~(ballot(t >= sr.tmin) & ballot(t < sr.tmax) & cand);
                 }
                 for (uint32_t mi = 0; mi < ((RTX_ABL_SMESH) ? 0u : S.n_meshes) && live; ++mi) {
                     float st = 0.f;
