@@ -95,6 +95,16 @@ def write_obj_from_asset(asset: Path, out_obj: Path) -> None:
     out_obj.write_text("\n".join(lines) + "\n")
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
+
+
 def cpu_baseline(scene: str, width: int, height: int, frames: int) -> dict | None:
     """The reference CPU Renderer timed on this host (rank 0, N = 1 only): the
     reference's own sources built in place by oracle/ref (kind "reference"), or the C
@@ -109,11 +119,17 @@ def cpu_baseline(scene: str, width: int, height: int, frames: int) -> dict | Non
                 write_obj_from_asset(abi.ASSET_DIR / f"{stem}.rtxmesh", res / f"{stem}.obj")
             out = subprocess.run([str(harness), "bench", scene, "-1", str(width), str(height), str(threads),
                                   str(frames)], cwd=td, check=True, capture_output=True, text=True, timeout=600)
-        r = json.loads(out.stdout.strip().splitlines()[-1])
+            r = json.loads(out.stdout.strip().splitlines()[-1])
+            # one frame on one core as well (BASELINE.md §3 records both)
+            one = subprocess.run([str(harness), "bench", scene, "-1", str(width), str(height), "1", "1"], cwd=td,
+                                 check=True, capture_output=True, text=True, timeout=600)
+            r1 = json.loads(one.stdout.strip().splitlines()[-1])
         return {"value": round(r["mpix_s"], 4), "unit": "Mpixels/s", "cores": threads, "kind": "reference",
                 "sample": f"{frames} frames of {scene} {width}x{height} (median of Renderer::Render, "
                           f"reference sources built with g++ -O2 -ffp-contract=off, {threads} threads, "
-                          f"1024-pixel dynamic chunks)", "median_s": r["median_s"], "fnv": r["fnv"]}
+                          f"1024-pixel dynamic chunks)", "median_s": r["median_s"], "fnv": r["fnv"],
+                "single_thread_mpix_s": round(r1["mpix_s"], 4), "cpu_model": cpu_model(),
+                "nproc": os.cpu_count()}
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_bind   # test infrastructure: the checker, timed here as the CPU baseline
     hs = HostScene(scene)
@@ -129,6 +145,22 @@ def cpu_baseline(scene: str, width: int, height: int, frames: int) -> dict | Non
     return {"value": round(width * height / med / 1e6, 4), "unit": "Mpixels/s", "cores": threads, "kind": "port",
             "sample": f"{frames} frames of {scene} {width}x{height} (median, C restatement oracle/rtx_oracle.c, "
                       f"{threads} threads)", "median_s": med}
+
+
+def pmc_traffic(scene: str, width: int, height: int, views: int) -> tuple[int | None, str | None]:
+    """HBM bytes per launch of the render kernel from the committed rocprofv3 PMC summary of
+    this same command (tools/profile.sh -> profiles/r01/pmc_summary.json: 2 x FETCH_SIZE +
+    WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), when the configuration
+    matches.  A benchmark process cannot read its own PMC counters, so this is the
+    profiled value, not a live one."""
+    f = ROOT / "profiles" / "r01" / "pmc_summary.json"
+    try:
+        d = json.loads(f.read_text())
+    except (OSError, ValueError):
+        return None, None
+    if d.get("config") != {"scene": scene, "width": width, "height": height, "views": views}:
+        return None, None
+    return int(d["hbm_bytes_per_launch"]), str(f.relative_to(ROOT))
 
 
 def main() -> int:
@@ -216,6 +248,7 @@ def main() -> int:
     total_pixels = N * args.width * args.height * args.steps
     value = total_pixels / elapsed / 1e6
     achieved = flop / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(args.scene, args.width, args.height, N)
     out = {
         "metric": "Mpixels/s (primary+shadow rays) at 1920x1080; per-channel max-abs vs CPU ref",
         "value": round(value, 3),
@@ -235,7 +268,9 @@ def main() -> int:
                    "scene": args.scene, "width": args.width, "height": args.height, "views_per_step": N,
                    "stripe_rows": 16 if N > 1 else 0, "parallelism": f"image stripes x{N} (no collective)"},
         "roofline": {"bound": "valu", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP32_PEAK_TFLOPS, 5), "traffic": None,
+                     "frac": round(achieved / FP32_PEAK_TFLOPS, 5), "traffic": traffic,
+                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
+                     "hbm_gbs": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic and kernel_ms > 0 else None,
                      "kernel": "rtx_render_kernel<false>", "kernel_ms": round(kernel_ms, 5),
                      "flop_per_launch": flop, "pixels_per_launch": pixels_per_rank,
                      "flop_per_pixel": round(flop / max(pixels_per_rank, 1), 2),
