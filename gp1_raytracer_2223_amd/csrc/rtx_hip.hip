@@ -29,6 +29,13 @@
 
 using namespace rtxd;
 
+// Diagnostic build (never a product build): per-wave {start, end, hw id, node-pair steps,
+// triangle steps, lane-work} stamps, read back by rtx_debug_stamps / tools/stamps.py.
+#ifndef RTX_STAMPS
+#define RTX_STAMPS 0
+#endif
+[[maybe_unused]] constexpr int kStampWords = 6;
+
 #define RTX_PI 3.14159265358979323846f   // MathHelpers.h:7
 
 // ====================================================================== device code
@@ -161,7 +168,7 @@ __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const flo
 // Returned as a wave lane mask: one v_cmp per condition straight into SGPRs (a ballot
 // of the && would materialise the bool in a VGPR and compare it again).
 template <bool FAST>
-__device__ __forceinline__ unsigned long long slab_mask(const float4 mn, const float4 mx, const Ray& r) {
+__device__ __forceinline__ unsigned long long slab_mask(const float4 mn, const float4 mx, const Ray& r, float& tEnter) {
     const float tx1 = (mn.x - r.ox) * r.ix, tx2 = (mx.x - r.ox) * r.ix;
     const float ty1 = (mn.y - r.oy) * r.iy, ty2 = (mx.y - r.oy) * r.iy;
     const float tz1 = (mn.z - r.oz) * r.iz, tz2 = (mx.z - r.oz) * r.iz;
@@ -177,7 +184,13 @@ __device__ __forceinline__ unsigned long long slab_mask(const float4 mn, const f
         tMin = smax(tMin, smin(tz1, tz2));
         tMax = smin(tMax, smax(tz1, tz2));
     }
+    tEnter = tMin;
     return ballot(tMax > 0) & ballot(tMax >= tMin);
+}
+template <bool FAST>
+__device__ __forceinline__ unsigned long long slab_mask(const float4 mn, const float4 mx, const Ray& r) {
+    float t;
+    return slab_mask<FAST>(mn, mx, r, t);
 }
 
 __device__ __forceinline__ bool finite_inv(const Ray& r) {
@@ -230,7 +243,8 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, uns
     for (;;) {
         // invariant: the node (link, ntri) passed its slab test exactly for the lanes in m
         if (ntri) {
-            if (COUNT && lane == 0) cnt.c[kWaveTriTests] += ntri;
+            if ((COUNT || RTX_STAMPS) && lane == 0) cnt.c[kWaveTriTests] += ntri;
+            if (RTX_STAMPS && !COUNT && lane == 0) cnt.c[kTri] += ntri * __popcll(ANY ? (m & live) : m);
             const bool in = (m >> lane) & 1ull;
             for (uint32_t k = 0; k < ntri; ++k) {
                 const uint32_t ti = link + k;
@@ -250,7 +264,8 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, uns
             }
             if (ANY && (live & mask) == 0) return;
         } else {
-            if (COUNT && lane == 0) cnt.c[kWaveNodeTests]++;
+            if ((COUNT || RTX_STAMPS) && lane == 0) cnt.c[kWaveNodeTests]++;
+            if (RTX_STAMPS && !COUNT && lane == 0) cnt.c[kSlab] += 2 * __popcll(m);
             NodePair P;
             ldc64(S.nodes, link >> 1, P.l0, P.l1, P.r0, P.r1);
             const unsigned long long ml = slab_mask<FAST>(P.l0, P.l1, r) & m;
@@ -362,9 +377,6 @@ __device__ __forceinline__ uint32_t q8(float c) {
 
 // Renderer::RenderPixel (source/Renderer.cpp:100-182) for a 16x16 tile per workgroup.
 template <bool COUNT>
-#ifndef RTX_STAMPS
-#define RTX_STAMPS 0
-#endif
 // Timing-only ablation switches (results are wrong when set; never in a product build).
 #ifndef RTX_ABL_PPLANE
 #define RTX_ABL_PPLANE 0
@@ -416,7 +428,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     const int py = static_cast<int>(gy * kTile + (wave >> 1) * 8u + (lane >> 3));
     const bool valid = px < static_cast<int>(F.width) && py < static_cast<int>(F.height);
     Counts cnt;
-    if (COUNT) for (int k = 0; k < kNumCounters; ++k) cnt.c[k] = 0;
+    if (COUNT || RTX_STAMPS) for (int k = 0; k < kNumCounters; ++k) cnt.c[k] = 0;
     if (COUNT && valid) cnt.c[kPixels] = 1;
 
     // ---- primary ray (Renderer.cpp:104-114; Matrix::TransformVector Matrix.cpp:35-42)
@@ -603,9 +615,13 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         unsigned xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        F.stamps[3 * w] = t_start;
-        F.stamps[3 * w + 1] = t_end;
-        F.stamps[3 * w + 2] = (static_cast<unsigned long long>(xcc) << 32) | hw;
+        unsigned long long* st = F.stamps + kStampWords * w;
+        st[0] = t_start;
+        st[1] = t_end;
+        st[2] = (static_cast<unsigned long long>(xcc) << 32) | hw;
+        st[3] = cnt.c[kWaveNodeTests];
+        st[4] = cnt.c[kWaveTriTests];
+        st[5] = (static_cast<unsigned long long>(cnt.c[kSlab]) << 32) | cnt.c[kTri];
     }
 #endif
     if (COUNT) {
@@ -1166,13 +1182,13 @@ extern "C" int rtx_debug_stamps(rtx_ctx* c, const rtx_camera* cam, const rtx_ren
     if (rc != RTX_OK) return rc;
     const uint64_t nw = static_cast<uint64_t>(grid.x) * grid.y * grid.z * 4;
     *n_waves = nw;
-    if (3 * nw > capacity) return RTX_E_INVALID;
+    if (kStampWords * nw > capacity) return RTX_E_INVALID;
     unsigned long long* d = nullptr;
-    HIP_TRY(c, hipMalloc(&d, 3 * nw * 8));
+    HIP_TRY(c, hipMalloc(&d, kStampWords * nw * 8));
     F.stamps = d;
     rc = launch(c, F, grid, false);
     if (rc != RTX_OK) return rc;
-    HIP_TRY(c, hipMemcpyAsync(out, d, 3 * nw * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(out, d, kStampWords * nw * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     (void)hipFree(d);
     return RTX_OK;

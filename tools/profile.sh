@@ -1,13 +1,13 @@
 #!/bin/bash
 # rocprofv3 passes for the headline bench (run on the GPU box).
 #   1) kernel trace + stats (durations)   2..n) one PMC group per pass
-# Usage: bash tools/profile.sh <tag>
+# Usage: [BENCH_ARGS="--scene X --width W --height H"] [PMC_GROUPS="A B|C D"] bash tools/profile.sh <tag>
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 cd "$PWD" && export TMPDIR=/tmp
 TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BENCH="python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline"
+BENCH="python3 bench.py --steps ${TRACE_STEPS:-100} --warmup 10 --no-cpu-baseline ${BENCH_ARGS:-}"
 set -o pipefail
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $BENCH > $OUT/trace.log 2>&1 || { echo "trace pass failed"; tail -20 $OUT/trace.log; exit 1; }
 echo "trace ok"
@@ -16,7 +16,7 @@ PMCLIST=${PMC_GROUPS:-"FETCH_SIZE|WRITE_SIZE|SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SAL
 IFS='|' read -ra GRPS <<< "$PMCLIST"
 for grp in "${GRPS[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i ($grp) failed"; tail -5 $OUT/pmc$i.log; }
+  timeout -k 10 300 rocprofv3 --pmc $grp -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py --steps ${PMC_STEPS:-20} --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i ($grp) failed"; tail -5 $OUT/pmc$i.log; }
 done
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 find $OUT -name "*.csv" | head -50

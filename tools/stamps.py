@@ -26,12 +26,12 @@ ctx.upload(s)
 p = abi.make_params(W, H)
 for _ in range(5):
     ctx.time_frames(cam, p, 20)
-cap = 3 * ((W + 15) // 16) * ((H + 15) // 16) * 4
+cap = 6 * ((W + 15) // 16) * ((H + 15) // 16) * 4
 buf = np.zeros(cap, np.uint64)
 nw = C.c_uint64()
 abi.check(lib.rtx_debug_stamps(ctx.h, C.byref(cam), C.byref(p), buf.ctypes.data_as(C.POINTER(C.c_uint64)),
                                cap, C.byref(nw)), "stamps", ctx.h)
-st = buf.reshape(-1, 3)[: nw.value]
+st = buf.reshape(-1, 6)[: nw.value]
 t0 = st[:, 0].min()
 start = (st[:, 0] - t0) / 100.0   # s_memrealtime = 100 MHz -> us
 end = (st[:, 1] - t0) / 100.0
@@ -49,3 +49,22 @@ for x in range(8):
     sel = xcc == x
     if sel.any():
         print(f"  xcc {x}: waves {sel.sum()} busy-us {dur[sel].sum():.0f} last end {end[sel].max():.1f}")
+nodes = st[:, 3].astype(np.int64)
+tris = st[:, 4].astype(np.int64)
+lane_slab = (st[:, 5] >> 32).astype(np.int64)
+lane_tri = (st[:, 5] & 0xffffffff).astype(np.int64)
+print(f"  wave node-pair steps: mean {nodes.mean():.0f} p50 {np.median(nodes):.0f} max {nodes.max()}; "
+      f"tri steps: mean {tris.mean():.0f} max {tris.max()}")
+tiles_x = (W + 15) // 16
+order = np.argsort(-dur)[:12]
+print("  slowest waves: dur_us  node_steps  tri_steps  slab_eff  tri_eff  (px0, py0)")
+for w in order:
+    tile, wv = divmod(int(w), 4)
+    ty, tx = divmod(tile, tiles_x)
+    x0 = tx * 16 + (wv & 1) * 8
+    y0 = ty * 16 + (wv >> 1) * 8
+    se = lane_slab[w] / max(1, 128 * nodes[w])
+    te = lane_tri[w] / max(1, 64 * tris[w])
+    print(f"    {dur[w]:9.1f} {nodes[w]:10d} {tris[w]:10d} {se:9.3f} {te:8.3f}  ({x0}, {y0})")
+us_per_step = dur / np.maximum(1, nodes + tris)
+print(f"  us per (node+tri) step: p50 {np.median(us_per_step):.3f}  slowest-wave {us_per_step[order[0]]:.3f}")
