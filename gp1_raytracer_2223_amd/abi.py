@@ -134,7 +134,7 @@ def load_host() -> C.CDLL:
 HIP_SYMBOLS = ["rtx_abi_version", "rtx_create", "rtx_destroy", "rtx_last_error", "rtx_upload_scene",
                "rtx_render", "rtx_render_async", "rtx_synchronize", "rtx_download", "rtx_device_buffers",
                "rtx_time_frames", "rtx_scene_bytes", "rtx_count_work",
-               "rtx_render_views_async", "rtx_time_views", "rtx_count_work_ex"]
+               "rtx_render_views_async", "rtx_time_views", "rtx_count_work_ex", "rtx_split_info"]
 
 
 def load_hip() -> C.CDLL:
@@ -184,6 +184,9 @@ def load_hip() -> C.CDLL:
         lib.rtx_count_work_ex.argtypes = [VP, C.POINTER(Camera), C.POINTER(RenderParams), C.POINTER(C.c_uint64),
                                           C.c_int]
         lib.rtx_count_work_ex.restype = C.c_int
+        if hasattr(lib, "rtx_split_info"):   # absent only in older experiment builds (RTX_HIP_LIB)
+            lib.rtx_split_info.argtypes = [VP, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+            lib.rtx_split_info.restype = C.c_int
         _hip = lib
     return _hip
 

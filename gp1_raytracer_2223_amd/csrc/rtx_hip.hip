@@ -16,6 +16,7 @@
 // Fresnel) is the device libm's and may differ from the host's by an ulp.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cstdio>
 #include <cstdlib>
@@ -35,6 +36,18 @@ using namespace rtxd;
 #define RTX_STAMPS 0
 #endif
 [[maybe_unused]] constexpr int kStampWords = 6;
+#if RTX_STAMPS
+#define RTX_SPLIT_STAMP()                                                                          \
+    if (lane == 0 && F.split_stamps) {                                                             \
+        const unsigned long long d_ = __builtin_amdgcn_s_memrealtime() - t_start;                 \
+        unsigned long long* x_ = F.split_stamps + 3 * ((PHASE - 1) * kMaxParts + part);            \
+        atomicAdd(x_, d_);                                                                         \
+        atomicMax(x_ + 1, d_);                                                                     \
+        atomicAdd(x_ + 2, static_cast<unsigned long long>(cnt.c[kWaveNodeTests] + cnt.c[kWaveTriTests])); \
+    }
+#else
+#define RTX_SPLIT_STAMP()
+#endif
 
 #define RTX_PI 3.14159265358979323846f   // MathHelpers.h:7
 
@@ -222,23 +235,12 @@ struct Counts {
 //   any-hit (ANY = true, shadow rays, Scene::DoesHit): a lane leaves at its first
 //       occluder; the wave leaves as soon as every lane in `mask` is occluded.
 // COUNT: per-lane SURVEY §8(d) work counters, any-hit counted up to the first occluder.
+// DFS below one node (link, ntri) that passed its slab test for the lanes in m.
 template <bool ANY, bool FAST, bool COUNT>
-__device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, unsigned long long mask, uint32_t lane,
-                              uint4* stk, unsigned long long* sT, float& sc_t, uint32_t& sc_tri,
-                              unsigned long long& live, Counts& cnt) {
-    if (M.y == 0) return;
-    const float cs = cull_sign(M.z, ANY);
-    unsigned long long m;
-    uint32_t link, ntri;
-    {
-        // root (odd global index; every child pair starts at an even one, 64-B aligned)
-        const float4 b0 = ldc(S.nodes, 2 * M.x), b1 = ldc(S.nodes, 2 * M.x + 1);
-        if (COUNT && ((mask >> lane) & 1ull)) cnt.c[kSlab]++;
-        m = slab_mask<FAST>(b0, b1, r) & mask;
-        if (m == 0) return;
-        link = __float_as_uint(b0.w);
-        ntri = __float_as_uint(b1.w);
-    }
+__device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t link, uint32_t ntri, unsigned long long m,
+                         unsigned long long mask, uint32_t lane, uint4* stk, unsigned long long* sT, float& sc_t,
+                         uint32_t& sc_tri, unsigned long long& live, Counts& cnt, const uint32_t* occ_word = nullptr,
+                         uint32_t occ_bit = 0) {
     int sp = 0;
     for (;;) {
         // invariant: the node (link, ntri) passed its slab test exactly for the lanes in m
@@ -261,6 +263,11 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, uns
                     sc_t = u ? t : sc_t;
                     sc_tri = u ? ti : sc_tri;
                 }
+            }
+            if (ANY && occ_word) {
+                // split any-hit: drop the lanes another part has already found occluded
+                const uint32_t o = __hip_atomic_load(occ_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                live &= ~ballot((o & occ_bit) != 0u);
             }
             if (ANY && (live & mask) == 0) return;
         } else {
@@ -311,6 +318,49 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, uns
             if (m) break;
         }
     }
+}
+
+template <bool ANY, bool FAST, bool COUNT>
+__device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, unsigned long long mask, uint32_t lane,
+                              uint4* stk, unsigned long long* sT, float& sc_t, uint32_t& sc_tri,
+                              unsigned long long& live, Counts& cnt) {
+    if (M.y == 0) return;
+    // root (odd global index; every child pair starts at an even one, 64-B aligned)
+    const float4 b0 = ldc(S.nodes, 2 * M.x), b1 = ldc(S.nodes, 2 * M.x + 1);
+    if (COUNT && ((mask >> lane) & 1ull)) cnt.c[kSlab]++;
+    const unsigned long long m = slab_mask<FAST>(b0, b1, r) & mask;
+    if (m == 0) return;
+    bvh_walk<ANY, FAST, COUNT>(S, cull_sign(M.z, ANY), r, __float_as_uint(b0.w), __float_as_uint(b1.w), m, mask, lane,
+                               stk, sT, sc_t, sc_tri, live, cnt);
+}
+
+// One part of a split traversal: the lanes that reach frontier node E (slab tests of the
+// root and of every node on E's path, exactly the tests the full DFS makes on the way
+// down), then the DFS of E's subtree.  Parts partition the triangles, so the closest-hit
+// result is the minimum of the parts' (t, triangle index) keys — left-then-right DFS
+// order is increasing triangle index (checked at upload), which makes the key minimum
+// the reference's first-found, strict-< winner — and occlusion is the OR of the parts.
+template <bool ANY, bool FAST>
+__device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, unsigned long long mask, uint32_t lane,
+                              uint4* stk, float& sc_t, uint32_t& sc_tri, unsigned long long& live, Counts& cnt,
+                              const uint32_t* occ_word = nullptr, uint32_t occ_bit = 0) {
+    const int4 M = ldc(S.meshes, static_cast<uint32_t>(E.x));
+    const float4 b0 = ldc(S.nodes, 2 * M.x), b1 = ldc(S.nodes, 2 * M.x + 1);
+    unsigned long long m = slab_mask<FAST>(b0, b1, r) & mask;
+    uint32_t link = __float_as_uint(b0.w), ntri = __float_as_uint(b1.w);
+    const uint32_t path = static_cast<uint32_t>(E.z);
+    for (int d = 0; d < E.w && m; ++d) {
+        NodePair P;
+        ldc64(S.nodes, link >> 1, P.l0, P.l1, P.r0, P.r1);
+        const bool right = (path >> d) & 1u;
+        const float4 c0 = right ? P.r0 : P.l0, c1 = right ? P.r1 : P.l1;
+        m &= slab_mask<FAST>(c0, c1, r);
+        link = __float_as_uint(c0.w);
+        ntri = __float_as_uint(c1.w);
+    }
+    if (m == 0) return;
+    bvh_walk<ANY, FAST, false>(S, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, nullptr, sc_t, sc_tri, live,
+                               cnt, occ_word, occ_bit);
 }
 
 struct RGB {
@@ -376,7 +426,18 @@ __device__ __forceinline__ uint32_t q8(float c) {
 }  // namespace
 
 // Renderer::RenderPixel (source/Renderer.cpp:100-182) for a 16x16 tile per workgroup.
-template <bool COUNT>
+//
+// PHASE 0 renders every tile except the heavy ones.  A heavy tile (measured cost far above
+// the frame's per-slot share, see rtx_reorder_kernel) is rendered by three launches over the
+// BVH frontier parts instead, so its serial traversal work is spread over many workgroups:
+//   PHASE 1  grid (heavy, parts):          closest hit of one part -> atomicMin of the
+//                                          {t bits, triangle} key per pixel
+//   PHASE 2  grid (heavy, parts, lights):  shadow ray of one light against one part ->
+//                                          atomicOr of the light's occlusion bit
+//   PHASE 3  grid (heavy):                 hit record from the key, spheres/planes
+//                                          occlusion + the bits, shading, output
+// Every phase recomputes the primary ray and the sphere/plane hits with the same code, so
+// all of them see bit-identical values.
 // Timing-only ablation switches (results are wrong when set; never in a product build).
 #ifndef RTX_ABL_PPLANE
 #define RTX_ABL_PPLANE 0
@@ -393,6 +454,7 @@ template <bool COUNT>
 #ifndef RTX_MIN_WAVES_PER_EU
 #define RTX_MIN_WAVES_PER_EU 1
 #endif
+template <bool COUNT, int PHASE>
 __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_render_kernel(const DevScene S, const FrameArgs F) {
     __shared__ uint4 stkE[kBlockThreads / 64][kStackDepth];
     __shared__ unsigned long long stkT[COUNT ? kBlockThreads / 64 : 1][kStackDepth];
@@ -409,7 +471,20 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     // measured per-tile cost, so the heavy tiles start first and do not form a tail;
     // which tile a block renders never changes a pixel's value.
     const uint32_t b = blockIdx.x;
-    const uint32_t tile = F.order ? ldc(F.order, b) : b;
+    uint32_t tile, hb = b, part = 0, light = 0;
+    if (PHASE == 0) {
+        tile = F.order ? ldc(F.order, b) : b;
+        if (F.heavy_flag && ldc(F.heavy_flag, tile)) return;   // rendered by the split launches
+    } else {
+        // grid (heavy tiles, parts, lights), tile fastest: every heavy tile's part 0 is
+        // dispatched first, the big top-of-tree parts before the small ones.  (Pinning a
+        // part to one XCD for L2 locality was measured slower: the heavy parts then load a
+        // few XCDs only.)
+        part = blockIdx.y;
+        light = blockIdx.z;
+        tile = ldc(F.heavy_list, hb);
+    }
+    const uint32_t slot = hb * kBlockThreads + threadIdx.x;    // heavy-pixel slot (PHASE > 0)
     const uint32_t per_view = F.tiles_x * F.tiles_y;
     const uint32_t view = tile / per_view;
     const uint32_t rem = tile - view * per_view;
@@ -471,15 +546,37 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         best_kind = b ? 2u : best_kind;
         best_idx = b ? i : best_idx;
     }
-    for (uint32_t mi = 0; mi < ((RTX_ABL_PMESH) ? 0u : S.n_meshes); ++mi) {
-        const int4 M = ldc(S.meshes, mi);
+    if (PHASE == 0) {
+        for (uint32_t mi = 0; mi < ((RTX_ABL_PMESH) ? 0u : S.n_meshes); ++mi) {
+            const int4 M = ldc(S.meshes, mi);
+            uint32_t sc_tri = 0;
+            unsigned long long unused = 0;
+            if (fast)
+                mesh_traverse<false, true, COUNT>(S, M, vr, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
+            else
+                mesh_traverse<false, false, COUNT>(S, M, vr, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
+            if (sc_t < best_t) { best_t = sc_t; best_kind = 3; best_idx = sc_tri; }
+        }
+    } else if (PHASE == 1) {
+        // one frontier part; sc0 = the scratch t the reference enters the meshes with
+        const int4 E = ldc(S.parts, part);
+        const float sc0 = sc_t;
         uint32_t sc_tri = 0;
         unsigned long long unused = 0;
         if (fast)
-            mesh_traverse<false, true, COUNT>(S, M, vr, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
+            part_traverse<false, true>(S, E, vr, active, lane, stk, sc_t, sc_tri, unused, cnt);
         else
-            mesh_traverse<false, false, COUNT>(S, M, vr, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
-        if (sc_t < best_t) { best_t = sc_t; best_kind = 3; best_idx = sc_tri; }
+            part_traverse<false, false>(S, E, vr, active, lane, stk, sc_t, sc_tri, unused, cnt);
+        if (valid && sc_t < sc0)   // accepted t >= tmin > 0: the float bits order like the values
+            atomicMin(&F.hit_key[slot], (static_cast<unsigned long long>(__float_as_uint(sc_t)) << 32) | sc_tri);
+        RTX_SPLIT_STAMP();
+        return;
+    } else {
+        // the minimum over the parts; strict < against the sphere/plane winner, as after
+        // every mesh in Scene::GetClosestHit (Scene.cpp:56-63)
+        const unsigned long long key = F.hit_key[slot];
+        const float T = __uint_as_float(static_cast<uint32_t>(key >> 32));
+        if (key != ~0ull && T < best_t) { best_t = T; best_kind = 3; best_idx = static_cast<uint32_t>(key); }
     }
 
     // ---- hit record (rebuilt from t: ray.origin + t * ray.direction, Utils.h:62-64)
@@ -514,7 +611,8 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         // originOffset = hit.origin + hit.normal * 0.0001f (Renderer.cpp:126)
         const float oox = hx + nx * 0.0001f, ooy = hy + ny * 0.0001f, ooz = hz + nz * 0.0001f;
         const float vx = -dx, vy = -dy, vz = -dz;
-        for (uint32_t li = 0; li < S.n_lights; ++li) {
+        const uint32_t l_first = PHASE == 2 ? light : 0u, l_end = PHASE == 2 ? light + 1 : S.n_lights;
+        for (uint32_t li = l_first; li < l_end; ++li) {
             const float4 L0 = ldc(S.lights, 2 * li), L1 = ldc(S.lights, 2 * li + 1);
             const int ltype = __float_as_int(L0.w);
             const bool known = (ltype == RTX_LIGHT_POINT || ltype == RTX_LIGHT_DIRECTIONAL);
@@ -529,13 +627,13 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                 unsigned long long live = hitmask;
                 const bool sfast = (wballot(did && !finite_inv(sr)) == 0);
                 if (COUNT && did) cnt.c[kShadow]++;
-                for (uint32_t i = 0; i < S.n_spheres && live; ++i) {
+                for (uint32_t i = 0; i < (PHASE == 2 ? 0u : S.n_spheres) && live; ++i) {
                     const float4 s = ldc(S.spheres, i);
                     if (COUNT && ((live >> lane) & 1ull)) cnt.c[kSphere]++;
                     float t;
                     live &= ~wballot(sphere_t(s, sr, t));
                 }
-                for (uint32_t i = 0; i < ((RTX_ABL_SPLANE) ? 0u : S.n_planes) && live; ++i) {
+                for (uint32_t i = 0; i < ((RTX_ABL_SPLANE || PHASE == 2) ? 0u : S.n_planes) && live; ++i) {
                     const float4 p0 = ldc(S.planes, 2 * i), p1 = ldc(S.planes, 2 * i + 1);
                     if (COUNT && ((live >> lane) & 1ull)) cnt.c[kPlane]++;
                     const float num = plane_num(p0, p1, sr), den = plane_den(p1, sr);
@@ -544,7 +642,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                     const float t = num / den;
                     live &= ~(ballot(t >= sr.tmin) & ballot(t < sr.tmax) & cand);
                 }
-                for (uint32_t mi = 0; mi < ((RTX_ABL_SMESH) ? 0u : S.n_meshes) && live; ++mi) {
+                for (uint32_t mi = 0; mi < ((RTX_ABL_SMESH || PHASE != 0) ? 0u : S.n_meshes) && live; ++mi) {
                     float st = 0.f;
                     uint32_t stri = 0;
                     if (sfast)
@@ -553,7 +651,21 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                         mesh_traverse<true, false, COUNT>(S, ldc(S.meshes, mi), sr, live, lane, stk, sT, st, stri, live,
                                                           cnt);
                 }
+                if (PHASE == 2) {
+                    const int4 E = ldc(S.parts, part);
+                    float st = 0.f;
+                    uint32_t stri = 0;
+                    if (sfast)
+                        part_traverse<true, true>(S, E, sr, live, lane, stk, st, stri, live, cnt, &F.occ_bits[slot],
+                                                  1u << li);
+                    else
+                        part_traverse<true, false>(S, E, sr, live, lane, stk, st, stri, live, cnt, &F.occ_bits[slot],
+                                                   1u << li);
+                    if (did && !((live >> lane) & 1ull)) atomicOr(&F.occ_bits[slot], 1u << li);
+                    continue;
+                }
                 occ = did && !((live >> lane) & 1ull);
+                if (PHASE == 3) occ = occ || (did && ((F.occ_bits[slot] >> li) & 1u));
             }
             if (!did) continue;
             if (occ) {
@@ -592,6 +704,14 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         }
         if (did) { fr *= shadowFactor; fg *= shadowFactor; fb *= shadowFactor; }
     }
+    if (PHASE == 2) {
+        RTX_SPLIT_STAMP();
+        return;
+    }
+    if (PHASE == 3) {   // ready for the next frame's split launches
+        F.hit_key[slot] = ~0ull;
+        F.occ_bits[slot] = 0u;
+    }
     // ColorRGB::MaxToOne (ColorRGB.h:12-17)
     const float mv = smax(fr, smax(fg, fb));
     if (mv > 1.f) { fr /= mv; fg /= mv; fb /= mv; }
@@ -603,12 +723,12 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
             F.out_rgb[3 * o] = fr; F.out_rgb[3 * o + 1] = fg; F.out_rgb[3 * o + 2] = fb;
         }
     }
-    if (F.cost && lane == 0) {
+    if (PHASE == 0 && F.cost && lane == 0) {   // split tiles keep their one-piece cost
         const unsigned long long dt = (__builtin_amdgcn_s_memtime() - t_block0) >> 4;
         atomicMax(&F.cost[tile], static_cast<uint32_t>(dt < 0xffffffffull ? dt : 0xffffffffull));
     }
 #if RTX_STAMPS
-    if (lane == 0 && F.stamps) {
+    if (PHASE == 0 && lane == 0 && F.stamps) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         const size_t w = static_cast<size_t>(tile) * 4 + wave;
         unsigned hw;
@@ -630,18 +750,34 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     }
 }
 
-template __global__ void rtx_render_kernel<false>(const DevScene, const FrameArgs);
-template __global__ void rtx_render_kernel<true>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 0>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<true, 0>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 1>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 2>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 3>(const DevScene, const FrameArgs);
 
 // Next frames' dispatch order from this frame's per-tile cost: heaviest first, STABLE
 // within a cost class so that tiles rendered together stay spatial neighbours (they walk
 // the same BVH nodes: scalar-cache locality).  One workgroup: each thread owns a
 // contiguous run of tiles; counts[class][thread] + an exclusive scan in (class, thread)
 // order give every tile its slot.  Clears the costs it read.
+//
+// It also picks the heavy tiles for split rendering: cost > split_permille/1000 x (total cost /
+// min(tiles, concurrent workgroup slots)), i.e. a tile that alone would outlast its share of
+// the frame.  `split_slots` = 0 disables splitting, UINT32_MAX forces every tile heavy
+// (tests).  Flags and list go to the staging set the host adopts at its next frame.
 __global__ void __launch_bounds__(kReorderThreads) rtx_reorder_kernel(uint32_t* __restrict__ cost,
-                                                                      uint32_t* __restrict__ order, uint32_t n) {
+                                                                      uint32_t* __restrict__ order, uint32_t n,
+                                                                      uint32_t split_slots, uint32_t split_permille,
+                                                                      const uint32_t* __restrict__ was_heavy,
+                                                                      uint32_t* __restrict__ saved,
+                                                                      uint32_t* __restrict__ heavy_flag,
+                                                                      uint32_t* __restrict__ heavy_list,
+                                                                      uint32_t* __restrict__ heavy_n) {
     __shared__ uint32_t cnt[kCostBuckets][kReorderThreads];
     __shared__ uint32_t tot[kCostBuckets];
+    __shared__ unsigned long long csum[kReorderThreads];
+    __shared__ uint32_t nheavy;
     const uint32_t tid = threadIdx.x;
     const uint32_t per = (n + kReorderThreads - 1) / kReorderThreads;
     const uint32_t lo = tid * per, hi = (lo + per < n) ? lo + per : n;
@@ -652,6 +788,14 @@ __global__ void __launch_bounds__(kReorderThreads) rtx_reorder_kernel(uint32_t* 
         k = k > 2u * 6u ? k - 2u * 6u : 0u;        // costs below 2^6 (x16 cycles) share a class
         return (kCostBuckets - 1) - (k < kCostBuckets ? k : kCostBuckets - 1);
     };
+    // A tile rendered split this frame has no fresh one-piece cost: it keeps the one it had
+    // when it was last rendered whole (kept in `saved`).
+    for (uint32_t t = lo; t < hi; ++t) {
+        if (was_heavy && was_heavy[t])
+            cost[t] = saved[t];
+        else
+            saved[t] = cost[t];
+    }
     for (int k = 0; k < kCostBuckets; ++k) cnt[k][tid] = 0;
     for (uint32_t t = lo; t < hi; ++t) cnt[bucket(cost[t])][tid]++;
     __syncthreads();
@@ -670,7 +814,29 @@ __global__ void __launch_bounds__(kReorderThreads) rtx_reorder_kernel(uint32_t* 
         const uint32_t k = bucket(cost[t]);
         order[tot[k] + cnt[k][tid]++] = t;
     }
+    // heavy tiles
+    unsigned long long my = 0;
+    for (uint32_t t = lo; t < hi; ++t) my += cost[t];
+    csum[tid] = my;
+    if (tid == 0) nheavy = 0;
     __syncthreads();
+    for (uint32_t w = kReorderThreads / 2; w > 0; w >>= 1) {
+        if (tid < w) csum[tid] += csum[tid + w];
+        __syncthreads();
+    }
+    const bool force = split_slots == 0xffffffffu;
+    const unsigned long long thr =
+        (split_slots && !force) ? csum[0] * split_permille / (1000ull * (n < split_slots ? n : split_slots)) : ~0ull;
+    for (uint32_t t = lo; t < hi; ++t) {
+        uint32_t f = 0;
+        if (force || cost[t] > thr) {
+            const uint32_t k = atomicAdd(&nheavy, 1u);
+            if (k < static_cast<uint32_t>(kMaxHeavyTiles)) { heavy_list[k] = t; f = 1; }
+        }
+        heavy_flag[t] = f;
+    }
+    __syncthreads();
+    if (tid == 0) *heavy_n = nheavy < static_cast<uint32_t>(kMaxHeavyTiles) ? nheavy : kMaxHeavyTiles;
     for (uint32_t t = lo; t < hi; ++t) cost[t] = 0;
 }
 
@@ -694,12 +860,32 @@ struct rtx_ctx {
     // cost-ordered tile dispatch
     uint32_t* d_order = nullptr;
     uint32_t* d_cost = nullptr;
+    uint32_t* d_saved_cost = nullptr;   // last one-piece cost per tile
     uint32_t sched_cap = 0;
     std::string sched_key;
     bool sched_ready = false;
     bool sched_enabled = true;
     uint64_t sched_frame = 0;
     uint64_t scene_gen = 0;
+    // split rendering of heavy tiles: double-buffered flag/list sets (the reorder kernel
+    // fills the staging set; the host adopts it, with its count, at the next frame)
+    uint32_t* d_heavy_flag[2] = {nullptr, nullptr};
+    uint32_t* d_heavy_list[2] = {nullptr, nullptr};
+    uint32_t* d_heavy_n = nullptr;
+    uint32_t* h_heavy_n = nullptr;   // pinned
+    hipEvent_t ev_heavy = nullptr;
+    hipStream_t split_stream = nullptr;   // split launches run beside the main kernel
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int heavy_cur = 0;
+    uint32_t heavy_n = 0;
+    bool heavy_pending = false;
+    uint32_t split_mode = 1;         // 0 off, 1 auto, 2 force (RTX_SPLIT=0 / unset / force)
+    uint32_t split_slots = 0;        // concurrent 256-thread workgroups on this device
+    uint32_t split_permille = kSplitFactor * 1000;   // RTX_SPLIT_FACTOR (tuning)
+    uint32_t split_parts = kPartsPerMesh;            // RTX_SPLIT_PARTS (tuning)
+    bool split_ok = false;           // the uploaded scene admits split rendering
+    unsigned long long* d_hit_key = nullptr;
+    uint32_t* d_occ = nullptr;
     rtx_render_params last{};
     int last_views = 1;
     bool last_valid = false, last_rgb = false;
@@ -745,6 +931,51 @@ bool bvh_depth_ok(const rtx_mesh& m, std::string& why) {
     return true;
 }
 
+// Frontier of one re-laid-out mesh BVH for split rendering: start from the root and split
+// the part with the most triangles until kPartsPerMesh parts (or only leaves) remain.
+// Returns false when the tree's left-then-right DFS does not visit the triangles in
+// increasing index order — the property that makes the min-key merge of the parts equal
+// to the reference's first-found closest hit — so the scene is rendered unsplit.
+bool build_parts(const std::vector<float4>& nodes, uint32_t root, uint32_t mesh, uint32_t target,
+                 std::vector<int4>& parts) {
+    auto link = [&](uint32_t n) { uint32_t u; std::memcpy(&u, &nodes[2 * n].w, 4); return u; };
+    auto ntri = [&](uint32_t n) { uint32_t u; std::memcpy(&u, &nodes[2 * n + 1].w, 4); return u; };
+    // DFS leaf order and subtree triangle counts
+    std::vector<uint32_t> st{root}, post;
+    uint32_t next_tri = ~0u;
+    while (!st.empty()) {
+        const uint32_t n = st.back();
+        st.pop_back();
+        post.push_back(n);
+        if (ntri(n)) {
+            if (next_tri != ~0u && link(n) != next_tri) return false;
+            next_tri = link(n) + ntri(n);
+        } else {
+            st.push_back(link(n) + 1);
+            st.push_back(link(n));
+        }
+    }
+    std::vector<uint32_t> sub(nodes.size() / 2, 0);
+    for (auto it = post.rbegin(); it != post.rend(); ++it)
+        sub[*it] = ntri(*it) ? ntri(*it) : sub[link(*it)] + sub[link(*it) + 1];
+    struct P { uint32_t node, path, depth; };
+    std::vector<P> fr{{root, 0u, 0u}};
+    while (fr.size() < target) {
+        int best = -1;
+        for (size_t k = 0; k < fr.size(); ++k)
+            if (!ntri(fr[k].node) && fr[k].depth < 31 && (best < 0 || sub[fr[k].node] > sub[fr[best].node]))
+                best = static_cast<int>(k);
+        if (best < 0) break;
+        const P e = fr[best];
+        fr[best] = {link(e.node), e.path, e.depth + 1};
+        fr.insert(fr.begin() + best + 1, P{link(e.node) + 1, e.path | (1u << e.depth), e.depth + 1});
+    }
+    for (const P& e : fr)
+        parts.push_back(make_int4(static_cast<int>(mesh), static_cast<int>(e.node), static_cast<int>(e.path),
+                                  static_cast<int>(e.depth)));
+    return true;
+}
+
 }  // namespace
 
 extern "C" int rtx_abi_version(void) { return RTX_ABI_VERSION; }
@@ -760,13 +991,38 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     c->device = device_id;
     // RTX_TILE_ORDER=0 disables cost-ordered tile dispatch (identity order every frame)
     if (const char* e = std::getenv("RTX_TILE_ORDER")) c->sched_enabled = std::strcmp(e, "0") != 0;
+    // RTX_SPLIT=0 renders heavy tiles in one piece; RTX_SPLIT=force splits every tile
+    if (const char* e = std::getenv("RTX_SPLIT")) c->split_mode = std::strcmp(e, "0") == 0 ? 0u : (std::strcmp(e, "force") == 0 ? 2u : 1u);
+    if (const char* e = std::getenv("RTX_SPLIT_PARTS")) {
+        const int v = std::atoi(e);
+        if (v >= 1 && v <= kMaxParts) c->split_parts = static_cast<uint32_t>(v);
+    }
+    if (const char* e = std::getenv("RTX_SPLIT_FACTOR")) {
+        const double f = std::atof(e);
+        if (f > 0 && f < 1e6) c->split_permille = static_cast<uint32_t>(f * 1000.0);
+    }
+    const size_t heavy_px = static_cast<size_t>(kMaxHeavyTiles) * kBlockThreads;
+    int cus = 0, lo_prio = 0, hi_prio = 0;
     if (hipSetDevice(device_id) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->d_counters, sizeof(unsigned long long) * kNumCounters) != hipSuccess) {
-        delete c;
+        hipEventCreateWithFlags(&c->ev_heavy, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->split_stream, hipStreamNonBlocking, hi_prio) != hipSuccess ||
+        hipMalloc(&c->d_counters, sizeof(unsigned long long) * kNumCounters) != hipSuccess ||
+        hipMalloc(&c->d_heavy_n, 4) != hipSuccess || hipHostMalloc(&c->h_heavy_n, 4) != hipSuccess ||
+        hipMalloc(&c->d_heavy_list[0], 4 * kMaxHeavyTiles) != hipSuccess ||
+        hipMalloc(&c->d_heavy_list[1], 4 * kMaxHeavyTiles) != hipSuccess ||
+        hipMalloc(&c->d_hit_key, 8 * heavy_px) != hipSuccess || hipMalloc(&c->d_occ, 4 * heavy_px) != hipSuccess ||
+        hipMemset(c->d_hit_key, 0xff, 8 * heavy_px) != hipSuccess || hipMemset(c->d_occ, 0, 4 * heavy_px) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id) != hipSuccess) {
+        rtx_destroy(c);
         return RTX_E_DEVICE;
     }
+    // 256-thread workgroups resident at once: 7 per CU at the render kernel's occupancy
+    c->split_slots = static_cast<uint32_t>(cus > 0 ? cus : 1) * 7u;
     *out = c;
     return RTX_OK;
 }
@@ -781,6 +1037,19 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     (void)hipFree(c->d_counters);
     (void)hipFree(c->d_order);
     (void)hipFree(c->d_cost);
+    (void)hipFree(c->d_saved_cost);
+    for (int k = 0; k < 2; ++k) { (void)hipFree(c->d_heavy_flag[k]); (void)hipFree(c->d_heavy_list[k]); }
+    (void)hipFree(c->d_heavy_n);
+    if (c->h_heavy_n) (void)hipHostFree(c->h_heavy_n);
+    (void)hipFree(c->d_hit_key);
+    (void)hipFree(c->d_occ);
+    if (c->ev_heavy) (void)hipEventDestroy(c->ev_heavy);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->split_stream) {
+        (void)hipStreamSynchronize(c->split_stream);
+        (void)hipStreamDestroy(c->split_stream);
+    }
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -804,7 +1073,8 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     const uint32_t nm = s->n_materials;
     std::vector<float4> sph, pl, tri, nodes, lights, mats;
     std::vector<uint32_t> sph_mat;
-    std::vector<int4> meshes;
+    std::vector<int4> meshes, parts;
+    bool split_ok = s->n_lights <= static_cast<uint32_t>(kMaxSplitLights);
     for (uint32_t i = 0; i < s->n_spheres; ++i) {
         const rtx_sphere& p = s->spheres[i];
         if (p.material >= nm) return fail(c, RTX_E_INVALID, "sphere material out of range");
@@ -875,7 +1145,12 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
         }
         meshes.push_back(make_int4(static_cast<int>(root), static_cast<int>(m.n_nodes), m.cull_mode, m.material));
         (void)node0;
+        // ~48 triangles per part at least: finer parts of a small mesh cost more than they spread
+        const uint32_t target = std::max(2u, std::min(c->split_parts, ntri / 48u));
+        if (m.n_nodes && !build_parts(nodes, root, mi, target, parts)) split_ok = false;
     }
+    if (parts.size() > static_cast<size_t>(kMaxParts)) split_ok = false;
+    if (!split_ok) parts.clear();
     for (uint32_t i = 0; i < s->n_lights; ++i) {
         const rtx_light& l = s->lights[i];
         lights.push_back(f4(l.origin[0], l.origin[1], l.origin[2], bitsi(l.type)));
@@ -895,7 +1170,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
                   {pl.data(), pl.size() * 16, 0},         {tri.data(), tri.size() * 16, 0},
                   {nodes.data(), nodes.size() * 16, 0},
                   {meshes.data(), meshes.size() * 16, 0}, {lights.data(), lights.size() * 16, 0},
-                  {mats.data(), mats.size() * 16, 0}};
+                  {mats.data(), mats.size() * 16, 0},     {parts.data(), parts.size() * 16, 0}};
     size_t total = 0;
     for (auto& x : secs) { x.off = total; total += align256(x.n ? x.n : 16); }
     HIP_TRY(c, hipSetDevice(c->device));
@@ -919,10 +1194,13 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     d.meshes = reinterpret_cast<const int4*>(c->d_scene + secs[5].off);
     d.lights = reinterpret_cast<const float4*>(c->d_scene + secs[6].off);
     d.materials = reinterpret_cast<const float4*>(c->d_scene + secs[7].off);
+    d.parts = reinterpret_cast<const int4*>(c->d_scene + secs[8].off);
+    d.n_parts = static_cast<uint32_t>(parts.size());
     d.n_spheres = s->n_spheres; d.n_planes = s->n_planes; d.n_meshes = s->n_meshes;
     d.n_lights = s->n_lights; d.n_materials = nm;
     d.n_tris = static_cast<uint32_t>(tri.size() / 4); d.n_nodes = static_cast<uint32_t>(nodes.size() / 2);
     c->dev = d;
+    c->split_ok = split_ok && !parts.empty();
     c->has_scene = true;
     ++c->scene_gen;
     return RTX_OK;
@@ -996,11 +1274,16 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         (void)hipFree(c->d_order);
         (void)hipFree(c->d_cost);
+        for (int k = 0; k < 2; ++k) { (void)hipFree(c->d_heavy_flag[k]); c->d_heavy_flag[k] = nullptr; }
+        (void)hipFree(c->d_saved_cost);
+        c->d_saved_cost = nullptr;
         c->d_order = nullptr;
         c->d_cost = nullptr;
         c->sched_cap = 0;
         HIP_TRY(c, hipMalloc(&c->d_order, ntiles * 4));
         HIP_TRY(c, hipMalloc(&c->d_cost, ntiles * 4));
+        for (int k = 0; k < 2; ++k) HIP_TRY(c, hipMalloc(&c->d_heavy_flag[k], ntiles * 4));
+        HIP_TRY(c, hipMalloc(&c->d_saved_cost, ntiles * 4));
         c->sched_cap = ntiles;
         c->sched_key.clear();
     }
@@ -1008,12 +1291,27 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
                       "s" + std::to_string(p->stripe_rows) + "/" + std::to_string(p->stripe_first) + "/" +
                       std::to_string(p->stripe_step) + "g" + std::to_string(c->scene_gen) + "m" +
                       std::to_string(p->lighting_mode) + std::to_string(p->shadows_enabled);
-    if (key != c->sched_key) {   // new shape or scene: identity order, fresh costs
+    if (key != c->sched_key) {   // new shape or scene: identity order, fresh costs, no split
+        if (c->heavy_pending) HIP_TRY(c, hipEventSynchronize(c->ev_heavy));
+        c->heavy_pending = false;
+        c->heavy_n = 0;
         c->sched_key = key;
         c->sched_ready = false;
         c->sched_frame = 0;
         HIP_TRY(c, hipMemsetAsync(c->d_cost, 0, ntiles * 4, c->stream));
+    } else if (c->heavy_pending) {
+        // adopt the heavy set the last measured frame selected (one sync per measurement)
+        HIP_TRY(c, hipEventSynchronize(c->ev_heavy));
+        c->heavy_pending = false;
+        c->heavy_n = *c->h_heavy_n;
+        c->heavy_cur ^= 1;
     }
+    const bool split = c->split_mode != 0 && c->split_ok && c->sched_enabled && c->heavy_n > 0;
+    F.heavy_flag = split ? c->d_heavy_flag[c->heavy_cur] : nullptr;
+    F.heavy_list = c->d_heavy_list[c->heavy_cur];
+    F.heavy_n = split ? c->heavy_n : 0u;
+    F.hit_key = c->d_hit_key;
+    F.occ_bits = c->d_occ;
     // Measure tile costs on the first frame of a shape and then every kSchedPeriod frames;
     // the frames in between reuse the last order and pay nothing for scheduling.
     const bool measure = c->sched_enabled && (!c->sched_ready || c->sched_frame % kSchedPeriod == 0);
@@ -1029,16 +1327,44 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         FrameArgs G = F;   // the instrumented variant neither reads nor feeds the schedule
         G.order = nullptr;
         G.cost = nullptr;
-        hipLaunchKernelGGL(rtx_render_kernel<true>, grid, dim3(kBlockThreads), 0, c->stream, c->dev, G);
+        G.heavy_flag = nullptr;
+        hipLaunchKernelGGL((rtx_render_kernel<true, 0>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, G);
         HIP_TRY(c, hipGetLastError());
         return RTX_OK;
     }
-    hipLaunchKernelGGL(rtx_render_kernel<false>, grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
-    HIP_TRY(c, hipGetLastError());
-    if (F.cost) {
-        hipLaunchKernelGGL(rtx_reorder_kernel, dim3(1), dim3(kReorderThreads), 0, c->stream, F.cost, c->d_order,
-                           grid.x);
+    if (F.heavy_flag) {
+        // The heavy tiles, one BVH frontier part per workgroup (see the kernel), on a
+        // high-priority stream forked from the frame stream: they share no pixels with the
+        // main kernel, so the two run side by side and the join closes the frame.
+        const uint32_t nh = c->heavy_n, np = c->dev.n_parts;
+        hipStream_t s2 = c->split_stream;
+        HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
+        hipLaunchKernelGGL((rtx_render_kernel<false, 1>), dim3(nh, np, 1), dim3(kBlockThreads), 0, s2, c->dev, F);
         HIP_TRY(c, hipGetLastError());
+        if (F.shadows && c->dev.n_lights) {
+            hipLaunchKernelGGL((rtx_render_kernel<false, 2>), dim3(nh, np, c->dev.n_lights), dim3(kBlockThreads), 0,
+                               s2, c->dev, F);
+            HIP_TRY(c, hipGetLastError());
+        }
+        hipLaunchKernelGGL((rtx_render_kernel<false, 3>), dim3(nh, 1, 1), dim3(kBlockThreads), 0, s2, c->dev, F);
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipEventRecord(c->ev_join, s2));
+    }
+    hipLaunchKernelGGL((rtx_render_kernel<false, 0>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
+    HIP_TRY(c, hipGetLastError());
+    if (F.heavy_flag) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    if (F.cost) {
+        const uint32_t slots = (c->split_mode == 0 || !c->split_ok) ? 0u
+                               : (c->split_mode == 2 ? 0xffffffffu : c->split_slots);
+        const int stage = c->heavy_cur ^ 1;
+        hipLaunchKernelGGL(rtx_reorder_kernel, dim3(1), dim3(kReorderThreads), 0, c->stream, F.cost, c->d_order,
+                           grid.x, slots, c->split_permille, F.heavy_flag, c->d_saved_cost, c->d_heavy_flag[stage],
+                           c->d_heavy_list[stage], c->d_heavy_n);
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipMemcpyAsync(c->h_heavy_n, c->d_heavy_n, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ev_heavy, c->stream));
+        c->heavy_pending = true;
         c->sched_ready = true;
     }
     return RTX_OK;
@@ -1172,6 +1498,19 @@ extern "C" int rtx_count_work_ex(rtx_ctx* c, const rtx_camera* cam, const rtx_re
     return RTX_OK;
 }
 
+extern "C" int rtx_split_info(rtx_ctx* c, uint32_t* heavy_tiles, uint32_t* parts) {
+    if (!c) return RTX_E_INVALID;
+    if (c->heavy_pending) {   // a measured frame is in flight: report the set it selects
+        HIP_TRY(c, hipSetDevice(c->device));
+        HIP_TRY(c, hipEventSynchronize(c->ev_heavy));
+    }
+    const uint32_t n = c->heavy_pending ? *c->h_heavy_n : c->heavy_n;
+    const bool on = c->split_mode != 0 && c->split_ok && c->sched_enabled;
+    if (heavy_tiles) *heavy_tiles = on ? n : 0u;
+    if (parts) *parts = c->split_ok ? c->dev.n_parts : 0u;
+    return RTX_OK;
+}
+
 #if RTX_STAMPS
 // Diagnostic build only: render once with per-wave {start, end, hw ids} stamps.
 extern "C" int rtx_debug_stamps(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* out,
@@ -1183,12 +1522,16 @@ extern "C" int rtx_debug_stamps(rtx_ctx* c, const rtx_camera* cam, const rtx_ren
     const uint64_t nw = static_cast<uint64_t>(grid.x) * grid.y * grid.z * 4;
     *n_waves = nw;
     if (kStampWords * nw > capacity) return RTX_E_INVALID;
+    if (kStampWords * nw + 6 * kMaxParts > capacity) return RTX_E_INVALID;
     unsigned long long* d = nullptr;
-    HIP_TRY(c, hipMalloc(&d, kStampWords * nw * 8));
+    const size_t words = kStampWords * nw + 6 * kMaxParts;   // + per (phase 1/2, part) {sum, max, steps}
+    HIP_TRY(c, hipMalloc(&d, words * 8));
+    HIP_TRY(c, hipMemsetAsync(d, 0, words * 8, c->stream));
     F.stamps = d;
+    F.split_stamps = d + kStampWords * nw;
     rc = launch(c, F, grid, false);
     if (rc != RTX_OK) return rc;
-    HIP_TRY(c, hipMemcpyAsync(out, d, kStampWords * nw * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(out, d, words * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     (void)hipFree(d);
     return RTX_OK;

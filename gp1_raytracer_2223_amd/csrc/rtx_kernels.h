@@ -14,6 +14,15 @@ constexpr int kReorderThreads = 256;
 constexpr int kCostBuckets = 32;
 constexpr int kSchedPeriod = 64;      // frames between tile-cost measurements
 
+// Split rendering of heavy tiles: a tile whose measured cost exceeds
+// kSplitFactor x (frame cost / concurrent workgroup slots) is rendered by three extra
+// launches in which its BVH traversals are cut into subtree parts run by separate workgroups.
+constexpr int kPartsPerMesh = 64;      // target frontier size per mesh BVH
+constexpr int kMaxParts = 1024;        // all meshes together
+constexpr int kMaxHeavyTiles = 2048;   // heavy tiles per frame (hit-key buffer: 256 px each)
+constexpr int kSplitFactor = 2;
+constexpr int kMaxSplitLights = 32;    // occlusion bits per pixel
+
 // Work counters (SURVEY §8(d) cost model; same order as the oracle's).
 enum Counter {
     kPixels = 0, kSphere, kPlane, kSlab, kTri, kHit, kShadow, kOccluded,
@@ -46,7 +55,10 @@ struct DevScene {
     const int4* __restrict__ meshes;
     const float4* __restrict__ lights;
     const float4* __restrict__ materials;
-    uint32_t n_spheres, n_planes, n_meshes, n_lights, n_materials, n_tris, n_nodes, _pad;
+    // BVH frontier for split rendering: {mesh, node slot, path bits (bit d: right child at
+    // depth d+1), depth} — every triangle of every mesh lies under exactly one entry
+    const int4* __restrict__ parts;
+    uint32_t n_spheres, n_planes, n_meshes, n_lights, n_materials, n_tris, n_nodes, n_parts;
 };
 
 constexpr int kMaxViews = 8;   // views (camera positions) rendered by one launch
@@ -75,6 +87,13 @@ struct FrameArgs {
     float* __restrict__ out_rgb;     // may be null
     unsigned long long* __restrict__ counters;  // COUNT variant only
     unsigned long long* __restrict__ stamps;    // diagnostic RTX_STAMPS builds only (null otherwise)
+    unsigned long long* __restrict__ split_stamps;   // diagnostic: per (phase 1/2, part) {sum, max, steps}
+    // split rendering (null / unused when no tile is heavy)
+    const uint32_t* __restrict__ heavy_flag;    // per tile: non-zero = rendered by the split launches
+    const uint32_t* __restrict__ heavy_list;    // split launches: heavy index -> tile
+    uint32_t heavy_n;                           // entries of heavy_list in use
+    unsigned long long* __restrict__ hit_key;   // per heavy pixel: min {t bits, triangle}
+    uint32_t* __restrict__ occ_bits;            // per heavy pixel: bit l = mesh occludes light l
 };
 
 }  // namespace rtxd

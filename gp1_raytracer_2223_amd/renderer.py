@@ -75,6 +75,12 @@ class DeviceContext:
                   "rtx_time_frames", self.h)
         return ms.value
 
+    def split_info(self) -> tuple[int, int]:
+        """(heavy tiles the next frame splits, BVH frontier parts of the scene)."""
+        h, p = C.c_uint32(), C.c_uint32()
+        abi.check(self.lib.rtx_split_info(self.h, C.byref(h), C.byref(p)), "rtx_split_info", self.h)
+        return h.value, p.value
+
     def count_work(self, cam, params) -> np.ndarray:
         out = (C.c_uint64 * 12)()
         abi.check(self.lib.rtx_count_work(self.h, C.byref(cam), C.byref(params), out), "rtx_count_work", self.h)

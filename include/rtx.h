@@ -218,6 +218,13 @@ int rtx_count_work(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params*
  * [13] triangle tests executed per WAVE (packet work, one count per wave per step). */
 int rtx_count_work_ex(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
                       uint64_t* counts, int n_counts);
+/* Split rendering of heavy tiles (no reference counterpart: a scheduling detail of this
+ * path).  Tiles whose measured cost exceeds their share of the frame are re-rendered with
+ * their BVH traversals cut into `parts` subtree pieces run by separate workgroups; the
+ * pixels are identical either way.  Reports the heavy-tile count the next frame will use
+ * and the frontier size of the uploaded scene (0 = the scene is rendered unsplit).
+ * Environment: RTX_SPLIT=0 disables, RTX_SPLIT=force splits every tile (tests). */
+int rtx_split_info(rtx_ctx* ctx, uint32_t* heavy_tiles, uint32_t* parts);
 
 #ifdef __cplusplus
 }

@@ -102,3 +102,70 @@ def test_cost_ordered_dispatch_is_output_invariant(gpu_ctx, name):
         px, rgb = gpu_ctx.render(cam, p)
         assert np.array_equal(px, first)
         assert np.array_equal(rgb.view(np.uint32), first_rgb.view(np.uint32))
+
+
+@pytest.fixture(scope="module")
+def split_ctx():
+    """A context that splits EVERY tile (RTX_SPLIT=force) from its second frame on."""
+    import os
+    from gp1_raytracer_2223_amd.renderer import DeviceContext
+    os.environ["RTX_SPLIT"] = "force"
+    try:
+        ctx = DeviceContext(int(os.environ.get("RTX_TEST_DEVICE", "0")))
+    finally:
+        del os.environ["RTX_SPLIT"]
+    yield ctx
+    ctx.close()
+
+
+SPLIT_CASES = [("W4_Bunny", -1.0), ("W4_Bunny", 1.3), ("W4_Reference", -1.0), ("W4_Optional", -1.0),
+               ("Synthetic100k", -1.0), ("Bunny8Lights", -1.0), ("W4_Optional", 1.3)]
+
+
+@pytest.mark.parametrize("name,t", SPLIT_CASES)
+@pytest.mark.parametrize("mode,shadows", [(3, 1), (3, 0), (2, 1), (0, 1)])
+def test_split_rendering(split_ctx, gpu_ctx, name, t, mode, shadows):
+    """Heavy-tile split rendering (closest hit = min key over BVH frontier parts, occlusion
+    = OR over parts) gives the same pixels as the one-piece kernel and the oracle."""
+    hs = HostScene(name)
+    if t >= 0:
+        hs.update(t)
+    s, cam = hs.view()
+    p = abi.make_params(256, 144, mode, shadows)
+    split_ctx.upload(s)
+    split_ctx.render(cam, p)                      # measured frame: selects the heavy set
+    heavy, parts = split_ctx.split_info()
+    assert parts > 1 and heavy == 16 * 9, (heavy, parts)
+    spx, srgb = split_ctx.render(cam, p)          # rendered by the split launches
+    gpu_ctx.upload(s)
+    gpx, grgb = gpu_ctx.render(cam, p)
+    assert np.array_equal(spx, gpx), f"{name}: {(spx != gpx).sum()} pixels differ from the one-piece kernel"
+    assert np.array_equal(srgb.view(np.uint32), grgb.view(np.uint32))
+    rpx, rrgb = oracle_bind.render(s, cam, p)
+    _compare(f"{name}/split", spx, srgb, rpx, rrgb, exact=(name in POW_FREE) or mode in (0, 1))
+
+
+def test_split_rendering_views_and_stripes(split_ctx, gpu_ctx):
+    """Split tiles under the multi-view launch with stripe ownership (the bench's layout)."""
+    import ctypes as C
+    hs = HostScene("W4_Optional")
+    s, cam = hs.view()
+    W, H, N = 192, 160, 3
+    views = (abi.Camera * N)()
+    for f in range(N):
+        C.memmove(C.byref(views[f]), C.byref(cam), C.sizeof(abi.Camera))
+        views[f].origin[0] = cam.origin[0] + 0.05 * f
+    for ctx in (split_ctx, gpu_ctx):
+        ctx.upload(s)
+    for r in range(N):
+        p = abi.make_params(W, H, stripe_rows=16, stripe_first=r, stripe_step=N)
+        out = []
+        for ctx in (split_ctx, gpu_ctx):
+            for _ in range(2):   # frame 1 measures, frame 2 splits (split_ctx)
+                abi.check(ctx.lib.rtx_render_views_async(ctx.h, views, N, C.byref(p), 0), "views", ctx.h)
+            abi.check(ctx.lib.rtx_synchronize(ctx.h), "sync", ctx.h)
+            buf = np.zeros(N * W * H, np.uint32)
+            abi.check(ctx.lib.rtx_download(ctx.h, buf.ctypes.data_as(C.POINTER(C.c_uint32)), None), "dl", ctx.h)
+            out.append(buf)
+        assert split_ctx.split_info()[0] > 0
+        assert np.array_equal(out[0], out[1]), f"rank {r}: {(out[0] != out[1]).sum()} pixels differ"

@@ -14,7 +14,7 @@ import subprocess
 import pytest
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-KERNEL = "_Z17rtx_render_kernelILb0EEvN4rtxd8DevSceneENS0_9FrameArgsE"
+KERNEL = "_Z17rtx_render_kernelILb0ELi0EEvN4rtxd8DevSceneENS0_9FrameArgsE"
 
 
 def _code_object(tmp_path, lib):

@@ -26,12 +26,18 @@ ctx.upload(s)
 p = abi.make_params(W, H)
 for _ in range(5):
     ctx.time_frames(cam, p, 20)
-cap = 6 * ((W + 15) // 16) * ((H + 15) // 16) * 4
+heavy, nparts = ctx.split_info()
+print(f'heavy tiles {heavy}, parts {nparts}')
+cap = 6 * ((W + 15) // 16) * ((H + 15) // 16) * 4 + 6 * 1024
 buf = np.zeros(cap, np.uint64)
 nw = C.c_uint64()
 abi.check(lib.rtx_debug_stamps(ctx.h, C.byref(cam), C.byref(p), buf.ctypes.data_as(C.POINTER(C.c_uint64)),
                                cap, C.byref(nw)), "stamps", ctx.h)
-st = buf.reshape(-1, 6)[: nw.value]
+st = buf[: 6 * nw.value].reshape(-1, 6)
+split = buf[6 * nw.value: 6 * nw.value + 6 * 1024].reshape(2, 1024, 3)
+wave_id = np.arange(len(st))
+keep = st[:, 1] > 0   # heavy tiles' main-kernel waves exit at once (split rendering)
+st, wave_id = st[keep], wave_id[keep]
 t0 = st[:, 0].min()
 start = (st[:, 0] - t0) / 100.0   # s_memrealtime = 100 MHz -> us
 end = (st[:, 1] - t0) / 100.0
@@ -59,7 +65,7 @@ tiles_x = (W + 15) // 16
 order = np.argsort(-dur)[:12]
 print("  slowest waves: dur_us  node_steps  tri_steps  slab_eff  tri_eff  (px0, py0)")
 for w in order:
-    tile, wv = divmod(int(w), 4)
+    tile, wv = divmod(int(wave_id[w]), 4)
     ty, tx = divmod(tile, tiles_x)
     x0 = tx * 16 + (wv & 1) * 8
     y0 = ty * 16 + (wv >> 1) * 8
@@ -68,3 +74,14 @@ for w in order:
     print(f"    {dur[w]:9.1f} {nodes[w]:10d} {tris[w]:10d} {se:9.3f} {te:8.3f}  ({x0}, {y0})")
 us_per_step = dur / np.maximum(1, nodes + tris)
 print(f"  us per (node+tri) step: p50 {np.median(us_per_step):.3f}  slowest-wave {us_per_step[order[0]]:.3f}")
+for ph in range(2):
+    sp = split[ph, :nparts]
+    if sp[:, 0].sum() == 0:
+        continue
+    tot = sp[:, 0] / 100.0
+    mx = sp[:, 1] / 100.0
+    print(f"  split phase {ph + 1}: wave-us total {tot.sum():.0f}, per part mean {tot.mean():.0f} max {tot.max():.0f}; "
+          f"slowest wave {mx.max():.1f} us (part {int(mx.argmax())}); steps total {int(sp[:, 2].sum())}")
+    top = np.argsort(-tot)[:6]
+    print("    heaviest parts (part: wave-us, max wave us, steps):",
+          ", ".join(f"{int(k)}: {tot[k]:.0f}/{mx[k]:.0f}/{int(sp[k, 2])}" for k in top))
