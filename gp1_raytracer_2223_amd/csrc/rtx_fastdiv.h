@@ -8,8 +8,9 @@
 // RN(1/b) is verified EXHAUSTIVELY on the hardware for every b in the domain
 // (tools/validate_fastdiv.hip, all 2^32 inputs), and the quotient step is Markstein's
 // theorem (y = RN(1/b), q0 within 1 ulp, exact residual by FMA) — additionally checked
-// on 2^33 random and near-halfway pairs by the same tool.  Callers fall back to `/`
-// (wave-uniform branch) whenever any lane leaves the domain.
+// on 2^33 random and near-halfway pairs by the same tool.  Lanes outside the domain
+// (zeros, tiny or huge magnitudes, inf, NaN) take the IEEE `/` in a divergent branch that
+// is skipped whenever no lane needs it.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -41,6 +42,25 @@ __device__ __forceinline__ float div_rn(float a, float b, float y) {
     const float q = a * y;
     const float r = fmaf(-b, q, a);
     return fmaf(r, y, q);
+}
+
+// RN(1/b) for every b.
+__device__ __forceinline__ float rcp_exact(float b) {
+    float y = rcp_rn(b);
+    if (__builtin_expect(!fast_rcp_ok(b), 0)) y = 1.f / b;
+    return y;
+}
+
+// (x, y, z) / m, each correctly rounded, for m = |(x, y, z)| as computed by the caller.
+__device__ __forceinline__ void div3_exact(float& x, float& y, float& z, float m) {
+    const float r = rcp_rn(m);
+    const float qx = div_rn(x, m, r), qy = div_rn(y, m, r), qz = div_rn(z, m, r);
+    const float lo = 0x1p-60f;
+    if (__builtin_expect(!(fast_rcp_ok(m) && fabsf(x) >= lo && fabsf(y) >= lo && fabsf(z) >= lo), 0)) {
+        x = x / m; y = y / m; z = z / m;
+    } else {
+        x = qx; y = qy; z = qz;
+    }
 }
 
 }  // namespace rtxd

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "rtx.h"
+#include "rtx_fastdiv.h"
 #include "rtx_kernels.h"
 
 using namespace rtxd;
@@ -104,7 +105,7 @@ __device__ __forceinline__ Ray make_ray(float ox, float oy, float oz, float dx, 
                                         float tmax) {
     Ray r;
     r.ox = ox; r.oy = oy; r.oz = oz; r.dx = dx; r.dy = dy; r.dz = dz;
-    r.ix = 1.f / dx; r.iy = 1.f / dy; r.iz = 1.f / dz;
+    r.ix = rcp_exact(dx); r.iy = rcp_exact(dy); r.iz = rcp_exact(dz);
     r.tmin = tmin; r.tmax = tmax;
     return r;
 }
@@ -161,7 +162,10 @@ __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const flo
     const float hz = r.dx * C.y - r.dy * C.x;
     const float a = B.x * hx + B.y * hy + B.z * hz;
     rej = fmaxf(rej, FLT_EPSILON - fabsf(a));
-    const float ai = 1.f / a;
+    // RN(1/a): lanes with |a| < EPS are rejected above whatever ai is, so only huge, inf
+    // and NaN a need the IEEE sequence (NaN gives NaN either way)
+    float ai = rcp_rn(a);
+    if (__builtin_expect(fabsf(a) > 0x1p60f, 0)) ai = 1.f / a;
     const float sx = r.ox - A.x, sy = r.oy - A.y, sz = r.oz - A.z;
     const float u = ai * (sx * hx + sy * hy + sz * hz);
     rej = fmaxf(rej, fmaxf(-u, u - 1.f));
@@ -514,7 +518,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     float dy = V.right[1] * cx + V.up[1] * cy + V.forward[1] * 1.f;
     float dz = V.right[2] * cx + V.up[2] * cy + V.forward[2] * 1.f;
     const float dm = sqrtf(dx * dx + dy * dy + dz * dz);
-    dx /= dm; dy /= dm; dz /= dm;
+    div3_exact(dx, dy, dz, dm);   // dx /= dm; ... (Vector3::Normalize)
     const Ray vr = make_ray(V.origin[0], V.origin[1], V.origin[2], dx, dy, dz, 0.0001f, FLT_MAX);
     const unsigned long long active = ballot(valid);
     const bool fast = (ballot(valid && !finite_inv(vr)) == 0);
@@ -618,7 +622,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
             const bool known = (ltype == RTX_LIGHT_POINT || ltype == RTX_LIGHT_DIRECTIONAL);
             float lx = known ? L0.x - oox : 0.f, ly = known ? L0.y - ooy : 0.f, lz = known ? L0.z - ooz : 0.f;
             const float mag = sqrtf(lx * lx + ly * ly + lz * lz);
-            lx /= mag; ly /= mag; lz /= mag;
+            div3_exact(lx, ly, lz, mag);
             bool occ = false;
             if (F.shadows) {
                 // Scene::DoesHit (Scene.cpp:68-96) on Ray{originOffset, l, 1e-4, |l|}; `live` =

@@ -1,5 +1,5 @@
 // validate_fastdiv.hip — exhaustive / randomized proof-by-test of the cheap
-// correctly-rounded reciprocal and quotient used by the render kernel (tools/rtx_fastdiv.h; evaluated, not adopted — see profiles/r01/ablate_history.md)
+// correctly-rounded reciprocal and quotient used by the render kernel (gp1_raytracer_2223_amd/csrc/rtx_fastdiv.h)
 // against the compiler's IEEE-correct 1.f/x and a/b on THIS hardware (gfx950).
 //
 //   rcp:  all 2^32 bit patterns; inside the fast domain the result must equal 1.f/x
