@@ -470,25 +470,31 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     uint4* stk = stkE[wave];
     unsigned long long* sT = stkT[COUNT ? wave : 0];
 
-    // Work unit = one 16x16 tile of one view.  The dispatch order is a permutation
-    // (F.order, null = identity) that rtx_reorder_kernel derives from the previous frame's
-    // measured per-tile cost, so the heavy tiles start first and do not form a tail;
-    // which tile a block renders never changes a pixel's value.
+    // Work unit = one 8x8 wave tile of one view; the 4 waves of a workgroup are independent
+    // (no barrier) and take 4 consecutive entries of the dispatch order.  The order is a
+    // permutation (F.order, null = identity) that rtx_reorder_kernel derives from the
+    // previous frame's measured per-tile cost: heavy tiles start first and do not form a
+    // tail, and the 4 waves of a workgroup have similar cost, so a finished wave seldom
+    // waits for its siblings to release the workgroup's slot.  Which wave renders a tile
+    // never changes a pixel's value.
     const uint32_t b = blockIdx.x;
-    uint32_t tile, hb = b, part = 0, light = 0;
+    const uint32_t widx = b * (kBlockThreads / 64) + wave;   // wave index in the launch
+    uint32_t tile, part = 0, light = 0;
     if (PHASE == 0) {
-        tile = F.order ? ldc(F.order, b) : b;
+        if (widx >= F.n_tiles) return;
+        tile = F.order ? ldc(F.order, widx) : widx;
         if (F.heavy_flag && ldc(F.heavy_flag, tile)) return;   // rendered by the split launches
     } else {
-        // grid (heavy tiles, parts, lights), tile fastest: every heavy tile's part 0 is
+        // grid (heavy tiles / 4, parts, lights), tile fastest: every heavy tile's part 0 is
         // dispatched first, the big top-of-tree parts before the small ones.  (Pinning a
         // part to one XCD for L2 locality was measured slower: the heavy parts then load a
         // few XCDs only.)
+        if (widx >= F.heavy_n) return;
         part = blockIdx.y;
         light = blockIdx.z;
-        tile = ldc(F.heavy_list, hb);
+        tile = ldc(F.heavy_list, widx);
     }
-    const uint32_t slot = hb * kBlockThreads + threadIdx.x;    // heavy-pixel slot (PHASE > 0)
+    const uint32_t slot = widx * 64u + lane;                 // heavy-pixel slot (PHASE > 0)
     const uint32_t per_view = F.tiles_x * F.tiles_y;
     const uint32_t view = tile / per_view;
     const uint32_t rem = tile - view * per_view;
@@ -503,8 +509,8 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         const uint32_t k = gy / F.groups_per_stripe, sub = gy % F.groups_per_stripe;
         gy = (first + k * F.stripe_step) * F.groups_per_stripe + sub;
     }
-    const int px = static_cast<int>(bx * kTile + (wave & 1u) * 8u + (lane & 7u));
-    const int py = static_cast<int>(gy * kTile + (wave >> 1) * 8u + (lane >> 3));
+    const int px = static_cast<int>(bx * kWaveTile + (lane & 7u));
+    const int py = static_cast<int>(gy * kWaveTile + (lane >> 3));
     const bool valid = px < static_cast<int>(F.width) && py < static_cast<int>(F.height);
     Counts cnt;
     if (COUNT || RTX_STAMPS) for (int k = 0; k < kNumCounters; ++k) cnt.c[k] = 0;
@@ -734,7 +740,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
 #if RTX_STAMPS
     if (PHASE == 0 && lane == 0 && F.stamps) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-        const size_t w = static_cast<size_t>(tile) * 4 + wave;
+        const size_t w = tile;
         unsigned hw;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         unsigned xcc;
@@ -884,7 +890,7 @@ struct rtx_ctx {
     uint32_t heavy_n = 0;
     bool heavy_pending = false;
     uint32_t split_mode = 1;         // 0 off, 1 auto, 2 force (RTX_SPLIT=0 / unset / force)
-    uint32_t split_slots = 0;        // concurrent 256-thread workgroups on this device
+    uint32_t split_slots = 0;        // concurrent render waves on this device
     uint32_t split_permille = kSplitFactor * 1000;   // RTX_SPLIT_FACTOR (tuning)
     uint32_t split_parts = kPartsPerMesh;            // RTX_SPLIT_PARTS (tuning)
     bool split_ok = false;           // the uploaded scene admits split rendering
@@ -1005,7 +1011,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
         const double f = std::atof(e);
         if (f > 0 && f < 1e6) c->split_permille = static_cast<uint32_t>(f * 1000.0);
     }
-    const size_t heavy_px = static_cast<size_t>(kMaxHeavyTiles) * kBlockThreads;
+    const size_t heavy_px = static_cast<size_t>(kMaxHeavyTiles) * 64;   // pixels of the heavy wave tiles
     int cus = 0, lo_prio = 0, hi_prio = 0;
     if (hipSetDevice(device_id) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -1025,8 +1031,8 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
         rtx_destroy(c);
         return RTX_E_DEVICE;
     }
-    // 256-thread workgroups resident at once: 7 per CU at the render kernel's occupancy
-    c->split_slots = static_cast<uint32_t>(cus > 0 ? cus : 1) * 7u;
+    // waves resident at once: 7 per SIMD, 4 SIMDs per CU at the render kernel's occupancy
+    c->split_slots = static_cast<uint32_t>(cus > 0 ? cus : 1) * 28u;
     *out = c;
     return RTX_OK;
 }
@@ -1223,7 +1229,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     if (p->format.rshift > 24 || p->format.gshift > 24 || p->format.bshift > 24)
         return fail(c, RTX_E_INVALID, "bad pixel format");
     const bool striped = p->stripe_rows != 0 && p->stripe_step > 1;
-    if (striped && (p->stripe_rows % kTile != 0 || p->stripe_first >= p->stripe_step))
+    if (striped && (p->stripe_rows % 16 != 0 || p->stripe_first >= p->stripe_step))
         return fail(c, RTX_E_INVALID, "stripe_rows must be a multiple of 16 and stripe_first < stripe_step");
     const size_t npx = static_cast<size_t>(p->width) * p->height * static_cast<size_t>(n_views);
     HIP_TRY(c, hipSetDevice(c->device));
@@ -1255,24 +1261,25 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     F.width = p->width; F.height = p->height;
     F.mode = p->lighting_mode; F.shadows = p->shadows_enabled ? 1 : 0;
     F.rshift = p->format.rshift; F.gshift = p->format.gshift; F.bshift = p->format.bshift; F.amask = p->format.amask;
-    const uint32_t groups = (p->height + kTile - 1) / kTile;
+    const uint32_t groups = (p->height + kWaveTile - 1) / kWaveTile;
     uint32_t gy = groups;
     if (striped) {
         // every view owns the same number of stripes only if the stripe count divides
         // evenly; size the grid for the largest owner and let the kernel skip the rest
-        const uint32_t gps = p->stripe_rows / kTile;
+        const uint32_t gps = p->stripe_rows / kWaveTile;
         const uint32_t nstripes = (groups + gps - 1) / gps;
         const uint32_t owned = (nstripes + p->stripe_step - 1) / p->stripe_step;
         F.groups_per_stripe = gps; F.stripe_first = p->stripe_first; F.stripe_step = p->stripe_step;
         gy = owned * gps;
     }
-    F.tiles_x = (p->width + kTile - 1) / kTile;
+    F.tiles_x = (p->width + kWaveTile - 1) / kWaveTile;
     F.tiles_y = gy;
     F.out_px = c->d_px;
     F.out_rgb = want_rgb ? c->d_rgb : nullptr;
     F.counters = c->d_counters;
     const uint32_t ntiles = F.tiles_x * gy * static_cast<uint32_t>(n_views);
-    grid = dim3(ntiles, 1, 1);
+    F.n_tiles = ntiles;
+    grid = dim3((ntiles + 3) / 4, 1, 1);
     // Cost-ordered dispatch (see the kernel): keep one order/cost pair per launch shape.
     if (ntiles > c->sched_cap) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1340,7 +1347,7 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         // The heavy tiles, one BVH frontier part per workgroup (see the kernel), on a
         // high-priority stream forked from the frame stream: they share no pixels with the
         // main kernel, so the two run side by side and the join closes the frame.
-        const uint32_t nh = c->heavy_n, np = c->dev.n_parts;
+        const uint32_t nh = (c->heavy_n + 3) / 4, np = c->dev.n_parts;   // 4 heavy wave tiles per workgroup
         hipStream_t s2 = c->split_stream;
         HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
@@ -1363,7 +1370,7 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
                                : (c->split_mode == 2 ? 0xffffffffu : c->split_slots);
         const int stage = c->heavy_cur ^ 1;
         hipLaunchKernelGGL(rtx_reorder_kernel, dim3(1), dim3(kReorderThreads), 0, c->stream, F.cost, c->d_order,
-                           grid.x, slots, c->split_permille, F.heavy_flag, c->d_saved_cost, c->d_heavy_flag[stage],
+                           F.n_tiles, slots, c->split_permille, F.heavy_flag, c->d_saved_cost, c->d_heavy_flag[stage],
                            c->d_heavy_list[stage], c->d_heavy_n);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipMemcpyAsync(c->h_heavy_n, c->d_heavy_n, 4, hipMemcpyDeviceToHost, c->stream));
@@ -1523,7 +1530,7 @@ extern "C" int rtx_debug_stamps(rtx_ctx* c, const rtx_camera* cam, const rtx_ren
     dim3 grid;
     int rc = prepare(c, cam, 1, p, false, F, grid);
     if (rc != RTX_OK) return rc;
-    const uint64_t nw = static_cast<uint64_t>(grid.x) * grid.y * grid.z * 4;
+    const uint64_t nw = F.n_tiles;   // one record per wave tile
     *n_waves = nw;
     if (kStampWords * nw > capacity) return RTX_E_INVALID;
     if (kStampWords * nw + 6 * kMaxParts > capacity) return RTX_E_INVALID;

@@ -8,18 +8,18 @@ namespace rtxd {
 // Per-wave DFS stack entries in LDS (node index + 64-bit lane mask).  The host checks
 // every uploaded BVH's depth against this before accepting the scene.
 constexpr int kStackDepth = 64;
-constexpr int kBlockThreads = 256;     // 4 waves = a 16 x 16 pixel tile (8 x 8 per wave)
-constexpr int kTile = 16;
+constexpr int kBlockThreads = 256;     // 4 independent waves, each an 8 x 8 pixel "wave tile"
+constexpr int kWaveTile = 8;
 constexpr int kReorderThreads = 256;
 constexpr int kCostBuckets = 32;
 constexpr int kSchedPeriod = 64;      // frames between tile-cost measurements
 
-// Split rendering of heavy tiles: a tile whose measured cost exceeds
-// kSplitFactor x (frame cost / concurrent workgroup slots) is rendered by three extra
+// Split rendering of heavy tiles: a wave tile whose measured cost exceeds
+// kSplitFactor x (frame cost / concurrent wave slots) is rendered by three extra
 // launches in which its BVH traversals are cut into subtree parts run by separate workgroups.
 constexpr int kPartsPerMesh = 64;      // target frontier size per mesh BVH
 constexpr int kMaxParts = 1024;        // all meshes together
-constexpr int kMaxHeavyTiles = 2048;   // heavy tiles per frame (hit-key buffer: 256 px each)
+constexpr int kMaxHeavyTiles = 8192;   // heavy wave tiles per frame (hit-key buffer: 64 px each)
 constexpr int kSplitFactor = 2;
 constexpr int kMaxSplitLights = 32;    // occlusion bits per pixel
 
@@ -78,9 +78,10 @@ struct FrameArgs {
     uint32_t width, height;
     int32_t mode, shadows;
     uint32_t rshift, gshift, bshift, amask;
-    uint32_t groups_per_stripe;   // stripe_rows / 16 (0 => whole image)
+    uint32_t groups_per_stripe;   // stripe_rows / 8 (0 => whole image)
     uint32_t stripe_first, stripe_step;
-    uint32_t tiles_x, tiles_y;    // 16x16 tiles per view row / per view column (owned)
+    uint32_t tiles_x, tiles_y;    // 8x8 wave tiles per view row / per view column (owned)
+    uint32_t n_tiles;             // wave tiles in the launch (all views)
     const uint32_t* __restrict__ order;   // dispatch permutation of the tiles (null = identity)
     uint32_t* __restrict__ cost;          // per-tile cost of this frame (null = not measured)
     uint32_t* __restrict__ out_px;   // view v at out_px + v * width * height

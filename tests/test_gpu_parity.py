@@ -135,7 +135,7 @@ def test_split_rendering(split_ctx, gpu_ctx, name, t, mode, shadows):
     split_ctx.upload(s)
     split_ctx.render(cam, p)                      # measured frame: selects the heavy set
     heavy, parts = split_ctx.split_info()
-    assert parts > 1 and heavy == 16 * 9, (heavy, parts)
+    assert parts > 1 and heavy == 32 * 18, (heavy, parts)   # every 8x8 wave tile
     spx, srgb = split_ctx.render(cam, p)          # rendered by the split launches
     gpu_ctx.upload(s)
     gpx, grgb = gpu_ctx.render(cam, p)

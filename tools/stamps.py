@@ -61,14 +61,13 @@ lane_slab = (st[:, 5] >> 32).astype(np.int64)
 lane_tri = (st[:, 5] & 0xffffffff).astype(np.int64)
 print(f"  wave node-pair steps: mean {nodes.mean():.0f} p50 {np.median(nodes):.0f} max {nodes.max()}; "
       f"tri steps: mean {tris.mean():.0f} max {tris.max()}")
-tiles_x = (W + 15) // 16
+tiles_x = (W + 7) // 8
 order = np.argsort(-dur)[:12]
 print("  slowest waves: dur_us  node_steps  tri_steps  slab_eff  tri_eff  (px0, py0)")
 for w in order:
-    tile, wv = divmod(int(wave_id[w]), 4)
-    ty, tx = divmod(tile, tiles_x)
-    x0 = tx * 16 + (wv & 1) * 8
-    y0 = ty * 16 + (wv >> 1) * 8
+    ty, tx = divmod(int(wave_id[w]), tiles_x)
+    x0 = tx * 8
+    y0 = ty * 8
     se = lane_slab[w] / max(1, 128 * nodes[w])
     te = lane_tri[w] / max(1, 64 * tris[w])
     print(f"    {dur[w]:9.1f} {nodes[w]:10d} {tris[w]:10d} {se:9.3f} {te:8.3f}  ({x0}, {y0})")
