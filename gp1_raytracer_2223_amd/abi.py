@@ -119,6 +119,8 @@ def load_host() -> C.CDLL:
         lib.rtx_host_scene_update.restype = C.c_int
         lib.rtx_host_scene_view.argtypes = [VP, C.POINTER(Scene), C.POINTER(Camera)]
         lib.rtx_host_scene_view.restype = C.c_int
+        lib.rtx_host_scene_animated.argtypes = [VP]
+        lib.rtx_host_scene_animated.restype = C.c_int
         lib.rtx_host_camera_set.argtypes = [VP, C.POINTER(C.c_float), C.c_float, C.c_float, C.c_float]
         lib.rtx_host_camera_set.restype = C.c_int
         lib.rtx_host_parse_obj.argtypes = [C.c_char_p, C.POINTER(C.c_float), C.POINTER(C.c_uint32),

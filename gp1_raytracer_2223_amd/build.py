@@ -48,7 +48,7 @@ def build_host(force: bool = False) -> Path:
     srcs = [CSRC / "host" / "scene.cpp", CSRC / "host" / "host_api.cpp"]
     deps = srcs + list((CSRC / "host").glob("*.h")) + [INC / "rtx.h", INC / "rtx_host.h"]
     if force or _stale(out, deps):
-        _run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
+        _run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared", "-pthread",
               "-Wall", "-Wextra", f"-I{INC}", *srcs, "-o", out, "-ldl"])
     return out
 

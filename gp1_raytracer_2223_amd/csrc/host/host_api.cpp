@@ -68,6 +68,11 @@ extern "C" int rtx_host_scene_view(rtx_host_scene* s, rtx_scene* out_scene, rtx_
     return RTX_OK;
 }
 
+extern "C" int rtx_host_scene_animated(const rtx_host_scene* s) {
+    if (!s) return RTX_E_INVALID;
+    return s->scene->Animated() ? 1 : 0;
+}
+
 extern "C" int rtx_host_camera_set(rtx_host_scene* s, const float origin[3], float fov_degrees, float pitch,
                                    float yaw) {
     if (!s || !origin) return RTX_E_INVALID;

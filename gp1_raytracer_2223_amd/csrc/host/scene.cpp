@@ -5,6 +5,7 @@
 #include <cstring>
 #include <fstream>
 #include <random>
+#include <thread>
 #include <utility>
 
 namespace rtx {
@@ -55,18 +56,111 @@ void TriangleMesh::BuildBVH() {
     root.firstIdx = 0;
     root.idxCount = static_cast<uint32_t>(indices.size());
     nodesUsed = 1;
-    UpdateNodeBounds(0);
-    Subdivide(0);
+    tc_.resize(indices.size() / 3);
+    for (size_t k = 0; k < tc_.size(); ++k) {
+        const Vec3& v0 = transformedPositions[indices[3 * k]];
+        const Vec3& v1 = transformedPositions[indices[3 * k + 1]];
+        const Vec3& v2 = transformedPositions[indices[3 * k + 2]];
+        tc_[k] = {(v0 + v1 + v2) * 0.3333f, v0, v1, v2, Vec3::Min(Vec3::Min(v0, v1), v2), Vec3::Max(Vec3::Max(v0, v1), v2)};
+    }
+    // build the tree (subtrees in parallel), then number it as the reference's recursive
+    // Subdivide would have (DataTypes.h:310-372)
+    tmp_.resize(2 * tc_.size() + 1);
+    tmpUsed_ = 1;
+    tmp_[0] = {0u, root.idxCount, {}, {}, -1, -1};
+    Bounds(tmp_[0]);
+    SubdivideTmp(0, 0);
+    root.minAABB = tmp_[0].mn;
+    root.maxAABB = tmp_[0].mx;
+    Emit(0, 0);
 }
 
-void TriangleMesh::UpdateNodeBounds(uint32_t nodeIdx) {
-    BVHNode& node = nodes[nodeIdx];
-    node.minAABB = kMaxVector;
-    node.maxAABB = kMinVector;
-    for (uint32_t i = node.firstIdx; i < node.firstIdx + node.idxCount; ++i) {
-        node.minAABB = Vec3::Min(node.minAABB, transformedPositions[indices[i]]);
-        node.maxAABB = Vec3::Max(node.maxAABB, transformedPositions[indices[i]]);
+void TriangleMesh::Bounds(TmpNode& n) const {
+    Vec3 mn = kMaxVector, mx = kMinVector;
+    for (uint32_t k = n.first / 3; k < (n.first + n.count) / 3; ++k) {   // UpdateNodeBounds, index order
+        const TriCache& t = tc_[k];
+        mn = Vec3::Min(mn, t.v0); mx = Vec3::Max(mx, t.v0);
+        mn = Vec3::Min(mn, t.v1); mx = Vec3::Max(mx, t.v1);
+        mn = Vec3::Min(mn, t.v2); mx = Vec3::Max(mx, t.v2);
     }
+    n.mn = mn;
+    n.mx = mx;
+}
+
+// Subdivide (DataTypes.h:310-372) on a tree node; touches only its own index range, so
+// sibling subtrees run concurrently.
+void TriangleMesh::SubdivideTmp(uint32_t t, int depth) {
+    TmpNode& n = tmp_[t];
+    if (n.count <= 8) return;
+    BVHNode view;
+    view.firstIdx = n.first;
+    view.idxCount = n.count;
+    view.minAABB = n.mn;
+    view.maxAABB = n.mx;
+    int axis = 0;
+    float splitPos = 0.f;
+    const float splitCost = FindBestSplitPlane(view, axis, splitPos);
+    const float noSplitCost = CalculateNodeCost(view);
+    if (splitCost >= noSplitCost) return;
+
+    // in-place partition (DataTypes.h:335-363): permutes indices, normals and
+    // transformedNormals together
+    int i = static_cast<int>(n.first);
+    int j = i + static_cast<int>(n.count) - 1;
+    while (i <= j) {
+        const Vec3& c = tc_[static_cast<uint32_t>(i) / 3].c;
+        if (c[axis] < splitPos) {
+            i += 3;
+        } else {
+            std::swap(tc_[i / 3], tc_[(j - 2) / 3]);
+            std::swap(normals[i / 3], normals[(j - 2) / 3]);
+            std::swap(transformedNormals[i / 3], transformedNormals[(j - 2) / 3]);
+            std::swap(indices[i], indices[j - 2]);
+            std::swap(indices[i + 1], indices[j - 1]);
+            std::swap(indices[i + 2], indices[j]);
+            j -= 3;
+        }
+    }
+    const int leftCount = i - static_cast<int>(n.first);
+    if (leftCount == 0 || static_cast<uint32_t>(leftCount) == n.count) return;
+
+    const uint32_t L = __atomic_fetch_add(&tmpUsed_, 2u, __ATOMIC_RELAXED), R = L + 1;
+    tmp_[L] = {n.first, static_cast<uint32_t>(leftCount), {}, {}, -1, -1};
+    tmp_[R] = {static_cast<uint32_t>(i), n.count - static_cast<uint32_t>(leftCount), {}, {}, -1, -1};
+    Bounds(tmp_[L]);
+    Bounds(tmp_[R]);
+    n.l = static_cast<int32_t>(L);
+    n.r = static_cast<int32_t>(R);
+    // large subtrees: the left one on another thread (its ranges are disjoint from ours)
+    if (depth < 3 && tmp_[L].count >= 3 * 256 && tmp_[R].count >= 3 * 256) {
+        std::thread th([this, L, depth] { SubdivideTmp(L, depth + 1); });
+        SubdivideTmp(R, depth + 1);
+        th.join();
+    } else {
+        SubdivideTmp(L, depth + 1);
+        SubdivideTmp(R, depth + 1);
+    }
+}
+
+// Number the built tree exactly as the reference's recursion allocates it: a split node
+// takes the next two slots for its children, then the left subtree is numbered before
+// the right one.  Writes the same node fields the reference writes (leaves keep the rest).
+void TriangleMesh::Emit(uint32_t t, uint32_t nodeIdx) {
+    const TmpNode& n = tmp_[t];
+    if (n.l < 0) return;
+    const uint32_t L = nodesUsed++, R = nodesUsed++;
+    const TmpNode& a = tmp_[static_cast<uint32_t>(n.l)];
+    const TmpNode& b = tmp_[static_cast<uint32_t>(n.r)];
+    nodes[nodeIdx].leftNode = L;
+    nodes[L].firstIdx = a.first;
+    nodes[L].idxCount = a.count;
+    nodes[R].firstIdx = b.first;
+    nodes[R].idxCount = b.count;
+    nodes[nodeIdx].idxCount = 0;
+    nodes[L].minAABB = a.mn; nodes[L].maxAABB = a.mx;
+    nodes[R].minAABB = b.mn; nodes[R].maxAABB = b.mx;
+    Emit(static_cast<uint32_t>(n.l), L);
+    Emit(static_cast<uint32_t>(n.r), R);
 }
 
 float TriangleMesh::CalculateNodeCost(const BVHNode& node) {
@@ -78,34 +172,47 @@ float TriangleMesh::CalculateNodeCost(const BVHNode& node) {
 // Binned SAH, 8 bins (DataTypes.h:378-456), including the reference's quirks: centroid
 // scale 0.3333f, centroid bounds starting at {FLT_MAX, FLT_MIN}, and 0*inf = NaN costs
 // for empty sides (never accepted by the strict < comparison).
+// Same float operations in the same order per axis as the reference; the three axes share
+// one pass over the node's triangles and the centroids come from the build cache.
 float TriangleMesh::FindBestSplitPlane(const BVHNode& node, int& axis, float& splitPos) const {
     float bestCost = FLT_MAX;
-    for (int axisIdx = 0; axisIdx < 3; ++axisIdx) {
-        float minBounds = FLT_MAX;
-        float maxBounds = FLT_MIN;
-        for (uint32_t idx = 0; idx < node.idxCount; idx += 3) {
-            const Vec3 c = Centroid(node.firstIdx + idx);
-            minBounds = fmin_ref(minBounds, c[axisIdx]);
-            maxBounds = fmax_ref(maxBounds, c[axisIdx]);
+    const uint32_t k0 = node.firstIdx / 3, k1 = (node.firstIdx + node.idxCount) / 3;
+    float minB[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, maxB[3] = {FLT_MIN, FLT_MIN, FLT_MIN};
+    for (uint32_t k = k0; k < k1; ++k) {
+        const Vec3& c = tc_[k].c;
+        for (int a = 0; a < 3; ++a) {
+            minB[a] = fmin_ref(minB[a], c[a]);
+            maxB[a] = fmax_ref(maxB[a], c[a]);
         }
-        const float boundsDifference = maxBounds - minBounds;
-        if (fabsf(boundsDifference) < FLT_EPSILON) continue;
-
-        constexpr int kBins = 8, kPlanes = kBins - 1;
-        AABB binBounds[kBins];
-        uint32_t binCount[kBins] = {0, 0, 0, 0, 0, 0, 0, 0};
-        float scale = kBins / boundsDifference;
-        for (uint32_t idx = 0; idx < node.idxCount; idx += 3) {
-            const uint32_t off = node.firstIdx + idx;
-            const Vec3& v0 = transformedPositions[indices[off]];
-            const Vec3& v1 = transformedPositions[indices[off + 1]];
-            const Vec3& v2 = transformedPositions[indices[off + 2]];
-            const Vec3 c = (v0 + v1 + v2) * 0.3333f;
-            int b = static_cast<int>((c[axisIdx] - minBounds) * scale);
+    }
+    constexpr int kBins = 8, kPlanes = kBins - 1;
+    AABB bins[3][kBins];
+    uint32_t counts[3][kBins] = {};
+    float scales[3];
+    bool live[3];
+    for (int a = 0; a < 3; ++a) {
+        const float d = maxB[a] - minB[a];
+        live[a] = !(fabsf(d) < FLT_EPSILON);
+        scales[a] = kBins / d;
+    }
+    for (uint32_t k = k0; k < k1; ++k) {
+        const TriCache& t = tc_[k];
+        for (int a = 0; a < 3; ++a) {
+            if (!live[a]) continue;
+            int b = static_cast<int>((t.c[a] - minB[a]) * scales[a]);
             if (kPlanes < b) b = kPlanes;   // std::min(amountOfPlaneBins, b)
-            binCount[b] += 3;
-            binBounds[b].Grow(v0); binBounds[b].Grow(v1); binBounds[b].Grow(v2);
+            counts[a][b] += 3;
+            bins[a][b].minAABB = Vec3::Min(bins[a][b].minAABB, t.lo);
+            bins[a][b].maxAABB = Vec3::Max(bins[a][b].maxAABB, t.hi);
         }
+    }
+    for (int axisIdx = 0; axisIdx < 3; ++axisIdx) {
+        if (!live[axisIdx]) continue;
+        const float minBounds = minB[axisIdx];
+        const float boundsDifference = maxB[axisIdx] - minBounds;
+        const AABB* binBounds = bins[axisIdx];
+        const uint32_t* binCount = counts[axisIdx];
+        float scale;
         float leftArea[kPlanes]{}, rightArea[kPlanes]{};
         int leftCount[kPlanes]{}, rightCount[kPlanes]{};
         int leftSum = 0, rightSum = 0;
@@ -132,50 +239,6 @@ float TriangleMesh::FindBestSplitPlane(const BVHNode& node, int& axis, float& sp
         }
     }
     return bestCost;
-}
-
-void TriangleMesh::Subdivide(uint32_t nodeIdx) {
-    if (nodes[nodeIdx].idxCount <= 8) return;
-    int axis = 0;
-    float splitPos = 0.f;
-    const float splitCost = FindBestSplitPlane(nodes[nodeIdx], axis, splitPos);
-    const float noSplitCost = CalculateNodeCost(nodes[nodeIdx]);
-    if (splitCost >= noSplitCost) return;
-
-    // In-place partition (DataTypes.h:335-363): permutes indices, normals and
-    // transformedNormals together.
-    const BVHNode node = nodes[nodeIdx];
-    int i = static_cast<int>(node.firstIdx);
-    int j = i + static_cast<int>(node.idxCount) - 1;
-    while (i <= j) {
-        const Vec3 c = Centroid(static_cast<uint32_t>(i));
-        if (c[axis] < splitPos) {
-            i += 3;
-        } else {
-            std::swap(normals[i / 3], normals[(j - 2) / 3]);
-            std::swap(transformedNormals[i / 3], transformedNormals[(j - 2) / 3]);
-            std::swap(indices[i], indices[j - 2]);
-            std::swap(indices[i + 1], indices[j - 1]);
-            std::swap(indices[i + 2], indices[j]);
-            j -= 3;
-        }
-    }
-    const int leftCount = i - static_cast<int>(node.firstIdx);
-    if (leftCount == 0 || static_cast<uint32_t>(leftCount) == node.idxCount) return;
-
-    const uint32_t leftNodeIdx = nodesUsed++;
-    const uint32_t rightNodeIdx = nodesUsed++;
-    nodes[nodeIdx].leftNode = leftNodeIdx;
-    nodes[leftNodeIdx].firstIdx = node.firstIdx;
-    nodes[leftNodeIdx].idxCount = static_cast<uint32_t>(leftCount);
-    nodes[rightNodeIdx].firstIdx = static_cast<uint32_t>(i);
-    nodes[rightNodeIdx].idxCount = node.idxCount - static_cast<uint32_t>(leftCount);
-    nodes[nodeIdx].idxCount = 0;
-
-    UpdateNodeBounds(leftNodeIdx);
-    UpdateNodeBounds(rightNodeIdx);
-    Subdivide(leftNodeIdx);
-    Subdivide(rightNodeIdx);
 }
 
 // ---------------------------------------------------------------- Camera
@@ -555,6 +618,7 @@ public:
         ThreeLights();
         return true;
     }
+    bool Animated() const override { return true; }
     void Update(float t) override {
         const float yaw = Yaw(t);
         for (auto& m : m_Meshes) { m->RotateY(yaw); m->UpdateTransforms(); }
@@ -581,6 +645,7 @@ public:
         ThreeLights();
         return true;
     }
+    bool Animated() const override { return true; }
     void Update(float t) override {
         m_Meshes[0]->RotateY(Yaw(t));
         m_Meshes[0]->UpdateTransforms();
@@ -624,6 +689,7 @@ public:
         ThreeLights();
         return true;
     }
+    bool Animated() const override { return true; }
     void Update(float t) override {
         m_Meshes[0]->RotateY(Yaw(t));
         m_Meshes[0]->UpdateTransforms();

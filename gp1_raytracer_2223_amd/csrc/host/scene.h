@@ -62,14 +62,26 @@ struct TriangleMesh {
     void BuildBVH();                                                      // :294-308
 
 private:
-    void UpdateNodeBounds(uint32_t nodeIdx);
-    void Subdivide(uint32_t nodeIdx);
+    // Build tree before numbering: the subtrees are built in parallel, then numbered in
+    // the reference's allocation order (children pairs in DFS order of the splits).
+    struct TmpNode { uint32_t first, count; Vec3 mn, mx; int32_t l, r; };
+    std::vector<TmpNode> tmp_;
+    uint32_t tmpUsed_{0};   // bumped with __atomic_fetch_add by the build tasks
+    void Bounds(TmpNode& n) const;
+    void SubdivideTmp(uint32_t t, int depth);
+    void Emit(uint32_t t, uint32_t nodeIdx);
     float FindBestSplitPlane(const BVHNode& node, int& axis, float& splitPos) const;
     static float CalculateNodeCost(const BVHNode& node);
     Vec3 Centroid(uint32_t i) const {
         return (transformedPositions[indices[i]] + transformedPositions[indices[i + 1]] +
                 transformedPositions[indices[i + 2]]) * 0.3333f;
     }
+    // Build-time cache, permuted with the triangles: centroid (the reference recomputes
+    // the same expression at every use, DataTypes.h:348,414,435), the 3 vertices, and the
+    // triangle's box (bins grow by it: min/max are exact, so only the sign of a zero
+    // could depend on the grouping, and no SAH cost can observe that).
+    struct TriCache { Vec3 c, v0, v1, v2, lo, hi; };
+    std::vector<TriCache> tc_;
 };
 
 // dae::Camera (source/Camera.h): the ray-generation state only (Update is input).
@@ -104,6 +116,7 @@ public:
     virtual ~Scene() = default;
     virtual bool Initialize() = 0;
     virtual void Update(float totalTime) { (void)totalTime; }   // animated meshes only
+    virtual bool Animated() const { return false; }             // Update moves geometry
     Camera& GetCamera() { return m_Camera; }
     const std::string& Name() const { return sceneName; }
     const std::string& Error() const { return m_Error; }

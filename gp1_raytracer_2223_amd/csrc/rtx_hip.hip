@@ -857,8 +857,20 @@ struct rtx_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::string err;
     // scene image in HBM (one allocation, 256-B aligned sections)
-    char* d_scene = nullptr;
+    // Two scene images (device + pinned staging), alternated by uploads: an upload packs
+    // into the image no queued frame reads and copies it asynchronously, so the host can
+    // prepare the next animated frame while the GPU renders this one.
+    struct SceneBuf {
+        char* d = nullptr;
+        char* h = nullptr;
+        size_t cap = 0;
+        hipEvent_t done = nullptr;   // recorded after the last frame that reads this image
+        bool pending = false;
+    };
+    SceneBuf sb[2];
+    int sb_cur = -1;
     size_t scene_bytes = 0;
+    std::string scene_sig;   // topology of the uploaded scene (keeps the tile schedule across re-uploads)
     DevScene dev{};
     bool has_scene = false;
     // frame buffer in HBM
@@ -1017,6 +1029,8 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_heavy, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->sb[0].done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->sb[1].done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess ||
@@ -1041,7 +1055,11 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    (void)hipFree(c->d_scene);
+    for (auto& B : c->sb) {
+        (void)hipFree(B.d);
+        if (B.h) (void)hipHostFree(B.h);
+        if (B.done) (void)hipEventDestroy(B.done);
+    }
     (void)hipFree(c->d_px);
     (void)hipFree(c->d_rgb);
     (void)hipFree(c->d_counters);
@@ -1184,27 +1202,44 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     size_t total = 0;
     for (auto& x : secs) { x.off = total; total += align256(x.n ? x.n : 16); }
     HIP_TRY(c, hipSetDevice(c->device));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (total > c->scene_bytes || !c->d_scene) {
-        (void)hipFree(c->d_scene);
-        c->d_scene = nullptr;
-        c->scene_bytes = 0;
-        HIP_TRY(c, hipMalloc(&c->d_scene, total));
+    const int k = c->sb_cur < 0 ? 0 : (c->sb_cur ^ 1);
+    rtx_ctx::SceneBuf& B = c->sb[k];
+    if (B.pending) {   // frames queued against image k (two uploads ago) must be done with it
+        HIP_TRY(c, hipEventSynchronize(B.done));
+        B.pending = false;
     }
-    c->scene_bytes = total;
+    if (total > B.cap) {
+        (void)hipFree(B.d);
+        if (B.h) (void)hipHostFree(B.h);
+        B.d = nullptr;
+        B.h = nullptr;
+        B.cap = 0;
+        HIP_TRY(c, hipMalloc(&B.d, total));
+        HIP_TRY(c, hipHostMalloc(&B.h, total));
+        B.cap = total;
+    }
+    std::memset(B.h, 0, total);
     for (auto& x : secs)
-        if (x.n) HIP_TRY(c, hipMemcpyAsync(c->d_scene + x.off, x.p, x.n, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+        if (x.n) std::memcpy(B.h + x.off, x.p, x.n);
+    HIP_TRY(c, hipMemcpyAsync(B.d, B.h, total, hipMemcpyHostToDevice, c->stream));
+    if (c->sb_cur >= 0) {   // every frame queued so far reads the previous image
+        rtx_ctx::SceneBuf& O = c->sb[c->sb_cur];
+        HIP_TRY(c, hipEventRecord(O.done, c->stream));
+        O.pending = true;
+    }
+    c->sb_cur = k;
+    c->scene_bytes = total;
+    char* base = B.d;
     DevScene d{};
-    d.spheres = reinterpret_cast<const float4*>(c->d_scene + secs[0].off);
-    d.sphere_mat = reinterpret_cast<const uint32_t*>(c->d_scene + secs[1].off);
-    d.planes = reinterpret_cast<const float4*>(c->d_scene + secs[2].off);
-    d.tris = reinterpret_cast<const Tri*>(c->d_scene + secs[3].off);
-    d.nodes = reinterpret_cast<const float4*>(c->d_scene + secs[4].off);
-    d.meshes = reinterpret_cast<const int4*>(c->d_scene + secs[5].off);
-    d.lights = reinterpret_cast<const float4*>(c->d_scene + secs[6].off);
-    d.materials = reinterpret_cast<const float4*>(c->d_scene + secs[7].off);
-    d.parts = reinterpret_cast<const int4*>(c->d_scene + secs[8].off);
+    d.spheres = reinterpret_cast<const float4*>(base + secs[0].off);
+    d.sphere_mat = reinterpret_cast<const uint32_t*>(base + secs[1].off);
+    d.planes = reinterpret_cast<const float4*>(base + secs[2].off);
+    d.tris = reinterpret_cast<const Tri*>(base + secs[3].off);
+    d.nodes = reinterpret_cast<const float4*>(base + secs[4].off);
+    d.meshes = reinterpret_cast<const int4*>(base + secs[5].off);
+    d.lights = reinterpret_cast<const float4*>(base + secs[6].off);
+    d.materials = reinterpret_cast<const float4*>(base + secs[7].off);
+    d.parts = reinterpret_cast<const int4*>(base + secs[8].off);
     d.n_parts = static_cast<uint32_t>(parts.size());
     d.n_spheres = s->n_spheres; d.n_planes = s->n_planes; d.n_meshes = s->n_meshes;
     d.n_lights = s->n_lights; d.n_materials = nm;
@@ -1213,6 +1248,8 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     c->split_ok = split_ok && !parts.empty();
     c->has_scene = true;
     ++c->scene_gen;
+    c->scene_sig = std::to_string(d.n_spheres) + "/" + std::to_string(d.n_planes) + "/" + std::to_string(d.n_meshes) +
+                   "/" + std::to_string(d.n_tris) + "/" + std::to_string(d.n_lights) + "/" + std::to_string(nm);
     return RTX_OK;
 }
 
@@ -1300,7 +1337,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     }
     std::string key = std::to_string(p->width) + "x" + std::to_string(p->height) + "v" + std::to_string(n_views) +
                       "s" + std::to_string(p->stripe_rows) + "/" + std::to_string(p->stripe_first) + "/" +
-                      std::to_string(p->stripe_step) + "g" + std::to_string(c->scene_gen) + "m" +
+                      std::to_string(p->stripe_step) + "g" + c->scene_sig + "m" +
                       std::to_string(p->lighting_mode) + std::to_string(p->shadows_enabled);
     if (key != c->sched_key) {   // new shape or scene: identity order, fresh costs, no split
         if (c->heavy_pending) HIP_TRY(c, hipEventSynchronize(c->ev_heavy));

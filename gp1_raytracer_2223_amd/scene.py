@@ -45,6 +45,14 @@ class HostScene:
     def update(self, total_time: float) -> None:
         abi.check(self._lib.rtx_host_scene_update(self._h, float(total_time)), "rtx_host_scene_update")
 
+    @property
+    def animated(self) -> bool:
+        """Update(t) moves geometry (re-upload after it)."""
+        r = self._lib.rtx_host_scene_animated(self._h)
+        if r < 0:
+            abi.check(r, "rtx_host_scene_animated")
+        return bool(r)
+
     def set_camera(self, origin, fov_degrees: float = 45.0, pitch: float = 0.0, yaw: float = 0.0) -> None:
         o = (C.c_float * 3)(*origin)
         abi.check(self._lib.rtx_host_camera_set(self._h, o, fov_degrees, pitch, yaw), "rtx_host_camera_set")

@@ -29,6 +29,9 @@ int rtx_host_scene_update(rtx_host_scene* s, float total_time);
 /* Flat view (pointers into the scene; valid until the next update/destroy) and the
  * camera after CalculateCameraToWorld(). */
 int rtx_host_scene_view(rtx_host_scene* s, rtx_scene* out_scene, rtx_camera* out_camera);
+/* 1 if Update(t) moves geometry (the W4 scenes rotate their meshes, Scene.cpp:391-400,
+ * 431-437) and the scene must be re-uploaded after it, 0 if not, < 0 on error. */
+int rtx_host_scene_animated(const rtx_host_scene* s);
 /* Camera controls (Camera.h): origin, fov in degrees (SetCameraFOV), pitch/yaw in
  * radians (CalculateForwardVector). */
 int rtx_host_camera_set(rtx_host_scene* s, const float origin[3], float fov_degrees, float pitch, float yaw);
