@@ -109,3 +109,10 @@ def test_catalogue_complete():
     for name in RENDERABLE:
         s, cam = HostScene(name).view()
         assert s.n_materials >= 1
+
+
+def test_animated_flag():
+    """Update(t) moves geometry exactly for the scenes whose reference Update rotates meshes."""
+    from gp1_raytracer_2223_amd.scene import ANIMATED, RENDERABLE
+    for name in RENDERABLE:
+        assert HostScene(name).animated == (name in ANIMATED), name

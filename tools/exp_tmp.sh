@@ -1,6 +1,7 @@
 cd $GRAFT_REPO_ROOT
 timeout -k 10 900 python -m pytest tests -m gpu -q -x 2>&1 | tail -2 || exit 1
-cd gpurun_out && mkdir -p bm && cd bm
-for sc in W4_Bunny W4_Optional Bunny8Lights; do
-echo "== $sc"; timeout -k 10 60 ../../gp1_raytracer_2223_amd/lib/rtx_render $sc 1920 1080 --benchmark 3 | grep "AVG\|frames" || exit 1
+E=gp1_raytracer_2223_amd/lib/exp
+for lib in $E/librtx_hip_prev.so $E/librtx_hip_new.so $E/librtx_hip_prev.so $E/librtx_hip_new.so; do
+echo "== $lib"
+RTX_HIP_LIB=$lib ABLATE_SCENES=W4_Bunny,W3,Bunny8Lights,W4_Optional,W4_Reference ABLATE_MODES=combined+shadows timeout -k 10 250 python tools/ablate.py 20 || exit 1
 done
