@@ -181,7 +181,9 @@ def main() -> int:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={N}; using {N}", file=sys.stderr)
     hs = HostScene(args.scene)
     scene, cam = hs.view()
-    ctx = DeviceContext(d.local)
+    # RTX_BENCH_DEVICE pins every rank to one device: rehearsing the N-rank path on a
+    # one-GPU machine (the driver's multi-GPU runs leave it unset: rank r -> device LOCAL_RANK)
+    ctx = DeviceContext(int(os.environ.get("RTX_BENCH_DEVICE", d.local)))
     ctx.upload(scene)
     views = make_views(cam, N)
     params = abi.make_params(args.width, args.height, stripe_rows=16 if N > 1 else 0,
@@ -271,7 +273,7 @@ def main() -> int:
                      "frac": round(achieved / FP32_PEAK_TFLOPS, 5), "traffic": traffic,
                      "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                      "hbm_gbs": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic and kernel_ms > 0 else None,
-                     "kernel": "rtx_render_kernel<false>", "kernel_ms": round(kernel_ms, 5),
+                     "kernel": "rtx_render_kernel<false, 0> (+ split phases 1-3 when tiles are heavy)", "kernel_ms": round(kernel_ms, 5),
                      "flop_per_launch": flop, "pixels_per_launch": pixels_per_rank,
                      "flop_per_pixel": round(flop / max(pixels_per_rank, 1), 2),
                      "note": "FP32 VALU-bound path (no dense contraction, 4 B/pixel of HBM output); "
