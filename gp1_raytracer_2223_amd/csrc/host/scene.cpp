@@ -1,7 +1,9 @@
 // scene.cpp — host scene model (see scene.h).  Build with -ffp-contract=off.
 #include "scene.h"
 
+#include <cctype>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <random>
@@ -738,7 +740,155 @@ public:
 
 }  // namespace
 
+// ---------------------------------------------------------------- scene files
+// Data-driven scenes: a text file, one directive per line, built
+// with the same builders, in file order, as the catalogue scenes above are built from
+// Scene.cpp.  Grammar (floats by strtof; '#' starts a comment):
+//   camera <ox> <oy> <oz> <fov degrees>
+//   material solid <r> <g> <b>                        Material_SolidColor
+//   material lambert <r> <g> <b> <kd>                 Material_Lambert
+//   material lambert_phong <r> <g> <b> <kd> <ks> <exp> Material_LambertPhong
+//   material cook_torrance <r> <g> <b> <metal> <rough> Material_CookTorrence
+//   sphere <cx> <cy> <cz> <radius> <material>
+//   plane <ox> <oy> <oz> <nx> <ny> <nz> <material>
+//   mesh <stem> <material> <front|back|none> [scale x y z] [translate x y z] [spin]
+//   light point <x> <y> <z> <intensity> <r> <g> <b>
+//   light directional <dx> <dy> <dz> <intensity> <r> <g> <b>
+// Material indices count from 0 = the scene's built-in red SolidColor (Scene.cpp:9-10);
+// the file's materials are 1, 2, ... in order.  A mesh <stem> is <asset dir>/<stem>.rtxmesh
+// or .obj (the reference harness reads Resources/<stem>.obj); `spin` meshes rotate in
+// Update(t) like the W4 scenes (yaw = (cos t + 1)/2 * 2 pi, Scene.cpp:391-400).
+class SceneFile final : public CatalogueScene {
+public:
+    SceneFile(std::string assetDir, std::string path) : CatalogueScene(std::move(assetDir)), m_Path(std::move(path)) {}
+    bool Initialize() override {
+        sceneName = "file:" + m_Path;
+        std::ifstream in(m_Path);
+        if (!in) { m_Error = "cannot open scene file " + m_Path; return false; }
+        std::string line;
+        int lineNo = 0;
+        while (std::getline(in, line)) {
+            ++lineNo;
+            const size_t hash = line.find('#');
+            if (hash != std::string::npos) line.resize(hash);
+            std::vector<std::string> tok;
+            {
+                size_t i = 0;
+                while (i < line.size()) {
+                    while (i < line.size() && std::isspace(static_cast<unsigned char>(line[i]))) ++i;
+                    size_t j = i;
+                    while (j < line.size() && !std::isspace(static_cast<unsigned char>(line[j]))) ++j;
+                    if (j > i) tok.push_back(line.substr(i, j - i));
+                    i = j;
+                }
+            }
+            if (tok.empty()) continue;
+            if (!Directive(tok)) {
+                m_Error = m_Path + ":" + std::to_string(lineNo) + ": " + (m_Error.empty() ? "bad directive" : m_Error);
+                return false;
+            }
+        }
+        return true;
+    }
+    bool Animated() const override { return !m_Spin.empty(); }
+    void Update(float t) override {
+        for (TriangleMesh* m : m_Spin) { m->RotateY(Yaw(t)); m->UpdateTransforms(); }
+    }
+
+private:
+    static bool F(const std::vector<std::string>& t, size_t i, float& out) {
+        if (i >= t.size()) return false;
+        char* end = nullptr;
+        out = std::strtof(t[i].c_str(), &end);
+        return end && *end == 0;
+    }
+    bool Floats(const std::vector<std::string>& t, size_t i, size_t n, float* out) {
+        for (size_t k = 0; k < n; ++k)
+            if (!F(t, i + k, out[k])) { m_Error = "expected a number at field " + std::to_string(i + k); return false; }
+        return true;
+    }
+    bool MatIndex(const std::vector<std::string>& t, size_t i, uint8_t& out) {
+        float v;
+        if (!F(t, i, v) || v < 0.f || v != static_cast<float>(static_cast<int>(v)) ||
+            static_cast<size_t>(v) >= m_Materials.size()) {
+            m_Error = "material index out of range";
+            return false;
+        }
+        out = static_cast<uint8_t>(v);
+        return true;
+    }
+    bool Directive(const std::vector<std::string>& t) {
+        const std::string& d = t[0];
+        float v[8];
+        if (d == "camera") {
+            if (t.size() != 5 || !Floats(t, 1, 4, v)) return false;
+            m_Camera.origin = {v[0], v[1], v[2]};
+            m_Camera.SetCameraFOV(v[3]);
+            return true;
+        }
+        if (d == "material" && t.size() >= 2) {
+            if (m_Materials.size() >= 256) { m_Error = "more than 256 materials"; return false; }
+            const std::string& k = t[1];
+            if (k == "solid" && t.size() == 5 && Floats(t, 2, 3, v)) { AddMaterial(SolidColor({v[0], v[1], v[2]})); return true; }
+            if (k == "lambert" && t.size() == 6 && Floats(t, 2, 4, v)) { AddMaterial(Lambert({v[0], v[1], v[2]}, v[3])); return true; }
+            if (k == "lambert_phong" && t.size() == 8 && Floats(t, 2, 6, v)) {
+                AddMaterial(LambertPhong({v[0], v[1], v[2]}, v[3], v[4], v[5]));
+                return true;
+            }
+            if (k == "cook_torrance" && t.size() == 7 && Floats(t, 2, 5, v)) {
+                AddMaterial(CookTorrance({v[0], v[1], v[2]}, v[3], v[4]));
+                return true;
+            }
+            return false;
+        }
+        if (d == "sphere") {
+            uint8_t m;
+            if (t.size() != 6 || !Floats(t, 1, 4, v) || !MatIndex(t, 5, m)) return false;
+            AddSphere({v[0], v[1], v[2]}, v[3], m);
+            return true;
+        }
+        if (d == "plane") {
+            uint8_t m;
+            if (t.size() != 8 || !Floats(t, 1, 6, v) || !MatIndex(t, 7, m)) return false;
+            AddPlane({v[0], v[1], v[2]}, {v[3], v[4], v[5]}, m);
+            return true;
+        }
+        if (d == "light" && t.size() == 9 && Floats(t, 2, 7, v)) {
+            if (t[1] == "point") { AddPointLight({v[0], v[1], v[2]}, v[3], {v[4], v[5], v[6]}); return true; }
+            if (t[1] == "directional") { AddDirectionalLight({v[0], v[1], v[2]}, v[3], {v[4], v[5], v[6]}); return true; }
+            return false;
+        }
+        if (d == "mesh" && t.size() >= 4) {
+            uint8_t m;
+            if (!MatIndex(t, 2, m)) return false;
+            int32_t cull;
+            if (t[3] == "front") cull = RTX_CULL_FRONT;
+            else if (t[3] == "back") cull = RTX_CULL_BACK;
+            else if (t[3] == "none") cull = RTX_CULL_NONE;
+            else { m_Error = "cull must be front|back|none"; return false; }
+            TriangleMesh* mesh = AddTriangleMesh(cull, m);
+            if (!LoadMesh(mesh, t[1])) return false;
+            bool spin = false;
+            for (size_t i = 4; i < t.size();) {
+                if (t[i] == "scale" && Floats(t, i + 1, 3, v)) { mesh->Scale({v[0], v[1], v[2]}); i += 4; }
+                else if (t[i] == "translate" && Floats(t, i + 1, 3, v)) { mesh->Translate({v[0], v[1], v[2]}); i += 4; }
+                else if (t[i] == "spin") { spin = true; ++i; }
+                else { m_Error = "unknown mesh option " + t[i]; return false; }
+            }
+            mesh->AllocateNodes();   // pBVHNodes = new BVHNode[indices.size()]
+            mesh->UpdateAABB();
+            mesh->UpdateTransforms();
+            if (spin) m_Spin.push_back(mesh);
+            return true;
+        }
+        return false;
+    }
+    std::string m_Path;
+    std::vector<TriangleMesh*> m_Spin;
+};
+
 std::unique_ptr<Scene> MakeScene(const std::string& name, const std::string& assetDir) {
+    if (name.rfind("file:", 0) == 0) return std::make_unique<SceneFile>(assetDir, name.substr(5));
     std::unique_ptr<Scene> s;
     if (name == "W1") s = std::make_unique<SceneW1>(assetDir);
     else if (name == "W2") s = std::make_unique<SceneW2>(assetDir);

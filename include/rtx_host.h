@@ -17,9 +17,12 @@ extern "C" {
 typedef struct rtx_host_scene rtx_host_scene;
 
 /* Build a catalogue scene (W1, W2, W3, W3_Test, W4_Test, W4_Reference, W4_Bunny,
- * W4_Optional, Synthetic100k, Bunny8Lights) — Scene_*::Initialize().  Mesh assets are
- * looked up in `asset_dir` as <stem>.rtxmesh, then <stem>.obj.  On failure returns an
- * error code and, if err/err_len are given, the reason. */
+ * W4_Optional, Synthetic100k, Bunny8Lights) — Scene_*::Initialize() — or, for a name
+ * "file:<path>", the scene described by a scene file (text, one directive per line:
+ * camera / material / sphere / plane / mesh / light; grammar in csrc/host/scene.cpp and
+ * DESIGN.md, examples in scenes/*.rtxscene).  Mesh assets are looked up in `asset_dir`
+ * as <stem>.rtxmesh, then <stem>.obj.  On failure returns an error code and, if
+ * err/err_len are given, the reason (for scene files with the line number). */
 int rtx_host_scene_create(const char* name, const char* asset_dir, rtx_host_scene** out, char* err,
                           size_t err_len);
 void rtx_host_scene_destroy(rtx_host_scene* s);

@@ -23,6 +23,7 @@
 // Scenes are constructed with cwd = the directory holding Resources/*.obj.
 
 #include <algorithm>
+#include <cctype>
 #include <atomic>
 #include <cfloat>
 #include <chrono>
@@ -145,7 +146,105 @@ static void add_extra_lights(Scene* s) {
     }
 }
 
+// Scene file (gp1_raytracer_2223_amd/csrc/host/scene.cpp, "scene files"): the same
+// grammar built with the REFERENCE's own classes and builders, so file-defined scenes
+// are pinned against the reference like the catalogue scenes.
+class Scene_File final : public Scene {
+public:
+    explicit Scene_File(std::string path) : m_Path(std::move(path)) {}
+    void Initialize() override {
+        std::ifstream in(m_Path);
+        if (!in) { std::fprintf(stderr, "cannot open %s\n", m_Path.c_str()); std::exit(2); }
+        std::string line;
+        while (std::getline(in, line)) {
+            const size_t hash = line.find('#');
+            if (hash != std::string::npos) line.resize(hash);
+            std::vector<std::string> t;
+            size_t i = 0;
+            while (i < line.size()) {
+                while (i < line.size() && std::isspace(static_cast<unsigned char>(line[i]))) ++i;
+                size_t j = i;
+                while (j < line.size() && !std::isspace(static_cast<unsigned char>(line[j]))) ++j;
+                if (j > i) t.push_back(line.substr(i, j - i));
+                i = j;
+            }
+            if (t.empty()) continue;
+            if (!Directive(t)) { std::fprintf(stderr, "bad directive in %s: %s\n", m_Path.c_str(), line.c_str()); std::exit(2); }
+        }
+    }
+    std::vector<TriangleMesh*> m_Spin;
+
+private:
+    static float F(const std::string& s) { return std::strtof(s.c_str(), nullptr); }
+    bool Directive(const std::vector<std::string>& t) {
+        const std::string& d = t[0];
+        if (d == "camera" && t.size() == 5) {
+            m_Camera.origin = {F(t[1]), F(t[2]), F(t[3])};
+            m_Camera.SetCameraFOV(F(t[4]));
+            return true;
+        }
+        if (d == "material" && t.size() >= 2) {
+            const ColorRGB c = t.size() >= 5 ? ColorRGB{F(t[2]), F(t[3]), F(t[4])} : ColorRGB{};
+            if (t[1] == "solid" && t.size() == 5) { AddMaterial(new Material_SolidColor(c)); return true; }
+            if (t[1] == "lambert" && t.size() == 6) { AddMaterial(new Material_Lambert(c, F(t[5]))); return true; }
+            if (t[1] == "lambert_phong" && t.size() == 8) {
+                AddMaterial(new Material_LambertPhong(c, F(t[5]), F(t[6]), F(t[7])));
+                return true;
+            }
+            if (t[1] == "cook_torrance" && t.size() == 7) {
+                AddMaterial(new Material_CookTorrence(c, F(t[5]), F(t[6])));
+                return true;
+            }
+            return false;
+        }
+        if (d == "sphere" && t.size() == 6) {
+            AddSphere({F(t[1]), F(t[2]), F(t[3])}, F(t[4]), static_cast<unsigned char>(std::atoi(t[5].c_str())));
+            return true;
+        }
+        if (d == "plane" && t.size() == 8) {
+            AddPlane({F(t[1]), F(t[2]), F(t[3])}, {F(t[4]), F(t[5]), F(t[6])},
+                     static_cast<unsigned char>(std::atoi(t[7].c_str())));
+            return true;
+        }
+        if (d == "light" && t.size() == 9) {
+            const Vector3 v{F(t[2]), F(t[3]), F(t[4])};
+            const ColorRGB c{F(t[6]), F(t[7]), F(t[8])};
+            if (t[1] == "point") { AddPointLight(v, F(t[5]), c); return true; }
+            if (t[1] == "directional") { AddDirectionalLight(v, F(t[5]), c); return true; }
+            return false;
+        }
+        if (d == "mesh" && t.size() >= 4) {
+            TriangleCullMode cull;
+            if (t[3] == "front") cull = TriangleCullMode::FrontFaceCulling;
+            else if (t[3] == "back") cull = TriangleCullMode::BackFaceCulling;
+            else if (t[3] == "none") cull = TriangleCullMode::NoCulling;
+            else return false;
+            TriangleMesh* m = AddTriangleMesh(cull, static_cast<unsigned char>(std::atoi(t[2].c_str())));
+            Utils::ParseOBJ("Resources/" + t[1] + ".obj", m->positions, m->normals, m->indices);
+            bool spin = false;
+            for (size_t i = 4; i < t.size();) {
+                if (t[i] == "scale" && i + 3 < t.size()) { m->Scale({F(t[i + 1]), F(t[i + 2]), F(t[i + 3])}); i += 4; }
+                else if (t[i] == "translate" && i + 3 < t.size()) { m->Translate({F(t[i + 1]), F(t[i + 2]), F(t[i + 3])}); i += 4; }
+                else if (t[i] == "spin") { spin = true; ++i; }
+                else return false;
+            }
+            m->pBVHNodes = new BVHNode[m->indices.size()];
+            m->UpdateAABB();
+            m->UpdateTransforms();
+            if (spin) m_Spin.push_back(m);
+            return true;
+        }
+        return false;
+    }
+    std::string m_Path;
+};
+
 static std::unique_ptr<Scene> make_scene(const std::string& name) {
+    if (name.rfind("file:", 0) == 0) {
+        auto f = std::make_unique<Scene_File>(name.substr(5));
+        f->Initialize();
+        return f;
+    }
     std::unique_ptr<Scene> s;
     if (name == "W1") s = std::make_unique<Scene_W1>();
     else if (name == "W2") s = std::make_unique<Scene_W2>();
@@ -166,6 +265,10 @@ static std::unique_ptr<Scene> make_scene(const std::string& name) {
 static void apply_time(Scene* s, const std::string& name, float t) {
     if (t < 0.f) return;
     const auto yawAngle{(cosf(t) + 1.f) / 2.f * PI_2};
+    if (name.rfind("file:", 0) == 0) {
+        for (const auto m : static_cast<Scene_File*>(s)->m_Spin) { m->RotateY(yawAngle); m->UpdateTransforms(); }
+        return;
+    }
     if (name == "W4_Reference") {
         auto* r = static_cast<Scene_W4_ReferenceScene*>(s);
         for (const auto m : r->m_Meshes) { m->RotateY(yawAngle); m->UpdateTransforms(); }

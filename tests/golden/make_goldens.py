@@ -14,8 +14,12 @@ the reference's own functions:
   config_<name>_<W>x<H>.npz   full-resolution BASELINE configs: SHA-256 of the uint32
                         frame and of the float RGB plane + 4096 seeded sample pixels (index, uint32, rgb)
   prims.npz             primitive / BRDF known-answer vectors (GeometryUtils, Material::Shade)
+  scene_file_<stem>[_t].npz, frame_file_<stem>_128x72_m<mode>s<sh>[_t].npz
+                        the same for the scene files in scenes/*.rtxscene, built by the
+                        harness with the reference's own classes
 
-Usage:  python tests/golden/make_goldens.py
+Usage:  python tests/golden/make_goldens.py [--scene-files-only]
+
 """
 from __future__ import annotations
 
@@ -56,8 +60,29 @@ def tname(t: float) -> str:
     return "" if t < 0 else f"_t{t:g}"
 
 
+SCENE_FILES = sorted((HERE.parents[1] / "scenes").glob("*.rtxscene"))
+FILE_FRAMES = [(3, 1), (0, 1), (2, 0), (1, 1)]
+
+
+def scene_files() -> None:
+    for f in SCENE_FILES:
+        name = f"file:{f}"
+        for t in (-1.0, 1.3):
+            d = run("scene", name, t)
+            np.savez_compressed(HERE / f"scene_file_{f.stem}{tname(t)}.npz", **d)
+            for mode, sh in FILE_FRAMES:
+                d = run("render", name, t, 128, 72, mode, sh, 8)
+                np.savez_compressed(HERE / f"frame_file_{f.stem}_128x72_m{mode}s{sh}{tname(t)}.npz",
+                                    pixels=d["pixels"], rgb=d["rgb"])
+        print("scene file", f.name, flush=True)
+
+
 def main() -> None:
     assert HARNESS.exists(), "build oracle/_ref first (python -m gp1_raytracer_2223_amd.build)"
+    if "--scene-files-only" in sys.argv:
+        scene_files()
+        return
+    scene_files()
     for obj in sorted(REF_SRC.glob("Resources/*.obj")):
         d = run("obj", obj.relative_to(REF_SRC))
         np.savez_compressed(HERE / f"obj_{obj.stem}.npz", **d)

@@ -2,6 +2,8 @@
 identical inputs.  Tolerance (BASELINE.json north_star): per-channel max-abs <= 1e-4 on
 the post-MaxToOne float colour, and the uint32 buffer within 1 LSB per channel.  Paths
 without powf (Lambert / SolidColor scenes) are required bit-exact."""
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -169,3 +171,23 @@ def test_split_rendering_views_and_stripes(split_ctx, gpu_ctx):
             out.append(buf)
         assert split_ctx.split_info()[0] > 0
         assert np.array_equal(out[0], out[1]), f"rank {r}: {(out[0] != out[1]).sum()} pixels differ"
+
+
+SCENE_FILES = sorted((Path(__file__).resolve().parents[1] / "scenes").glob("*.rtxscene"))
+
+
+@pytest.mark.parametrize("path", SCENE_FILES, ids=lambda p: p.stem)
+@pytest.mark.parametrize("t", [-1.0, 1.3])
+@pytest.mark.parametrize("mode,shadows", [(3, 1), (1, 1), (2, 0)])
+def test_scene_file_parity(gpu_ctx, path, t, mode, shadows):
+    """Scenes defined by scene files (scenes/*.rtxscene, pinned to the reference by
+    tests/golden/*file_*) render on the GPU like the oracle."""
+    hs = HostScene(f"file:{path}")
+    if t >= 0:
+        hs.update(t)
+    s, cam = hs.view()
+    p = abi.make_params(256, 144, mode, shadows)
+    gpu_ctx.upload(s)
+    gpx, grgb = gpu_ctx.render(cam, p)
+    rpx, rrgb = oracle_bind.render(s, cam, p)
+    _compare(f"{path.stem}/m{mode}s{shadows}", gpx, grgb, rpx, rrgb, exact=mode in (0, 1) or path.stem == "w4_bunny")

@@ -2,6 +2,7 @@
 construction: world-space triangles, BVH node arrays and the BVH-permuted triangle order
 must be bit-identical (tests/golden/scene_*.npz, obj_*.npz)."""
 import hashlib
+import re
 from pathlib import Path
 
 import numpy as np
@@ -35,7 +36,8 @@ def test_scene_matches_reference(path):
     if "_t" in stem:
         stem, ts = stem.rsplit("_t", 1)
         t = float(ts)
-    hs = HostScene(stem)
+    from test_oracle_golden import scene_name
+    hs = HostScene(scene_name(stem))
     if t >= 0:
         hs.update(t)
     a = hs.arrays()
@@ -116,3 +118,36 @@ def test_animated_flag():
     from gp1_raytracer_2223_amd.scene import ANIMATED, RENDERABLE
     for name in RENDERABLE:
         assert HostScene(name).animated == (name in ANIMATED), name
+
+
+def test_scene_file_equals_catalogue_scene():
+    """scenes/w4_bunny.rtxscene builds exactly the catalogue's W4_Bunny (Initialize and t = 1.3)."""
+    from test_oracle_golden import scene_name
+    a, b = HostScene("W4_Bunny"), HostScene(scene_name("file_w4_bunny"))
+    for t in (-1.0, 1.3):
+        if t >= 0:
+            a.update(t)
+            b.update(t)
+        x, y = a.arrays(), b.arrays()
+        for k in x:
+            if k == "meshes":
+                for m, n in zip(x[k], y[k]):
+                    for kk in m:
+                        assert np.array_equal(_u(m[kk]), _u(n[kk])), kk
+            else:
+                assert np.array_equal(_u(x[k]), _u(y[k])), k
+
+
+@pytest.mark.parametrize("text,msg", [
+    ("camera 0 1 2\n", ":1:"),
+    ("material lambert 1 1 1\n", ":1:"),
+    ("sphere 0 0 0 1 7\n", "material index out of range"),
+    ("plane 0 0 0 0 1 0 0\nmesh no_such_mesh 0 back\n", "mesh asset not found"),
+    ("mesh lowpoly_bunny2 0 sideways\n", "cull must be"),
+    ("wobble 1 2 3\n", ":1: bad directive"),
+])
+def test_scene_file_errors(tmp_path, text, msg):
+    f = tmp_path / "bad.rtxscene"
+    f.write_text(text)
+    with pytest.raises(RuntimeError, match=re.escape(msg) if msg.startswith(":") else msg):
+        HostScene(f"file:{f}")

@@ -14,8 +14,15 @@ from gp1_raytracer_2223_amd.scene import HostScene
 G = Path(__file__).resolve().parent / "golden"
 
 
+def scene_name(name: str) -> str:
+    """Golden name -> host scene name: file_<stem> is scenes/<stem>.rtxscene."""
+    if name.startswith("file_"):
+        return f"file:{G.parents[1] / 'scenes' / name[5:]}.rtxscene"
+    return name
+
+
 def _scene(name, t):
-    hs = HostScene(name)
+    hs = HostScene(scene_name(name))
     if t >= 0:
         hs.update(t)
     return hs
