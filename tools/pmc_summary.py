@@ -1,4 +1,8 @@
-"""Summarise a tools/profile.sh output dir: mean counter value per dispatch of the render kernel."""
+"""Summarise a tools/profile.sh output dir: mean counter value per dispatch of the render kernel.
+
+Usage: python tools/pmc_summary.py <prof dir> [version tag]
+With a version tag the output is the full record bench.py reads (profiles/r01/pmc_summary.json):
+config of the default bench command, HBM bytes per launch = (2 x FETCH_SIZE + WRITE_SIZE) KB."""
 import collections
 import csv
 import glob
@@ -27,4 +31,15 @@ if "SQ_THREAD_CYCLES_VALU" in out and "SQ_ACTIVE_INST_VALU" in out:
 if "SQ_WAIT_ANY" in out and "SQ_WAVE_CYCLES" in out:
     for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
         derived[k + "_frac_of_wave_cycles"] = round(out[k] / out["SQ_WAVE_CYCLES"], 3)
-print(json.dumps({"counters": out, "derived": derived, "dispatch": meta}, indent=1))
+rec = {"counters": out, "derived": derived, "dispatch": meta}
+if len(sys.argv) > 2:
+    rec = {"kernel": "rtx_render_kernel<false, 0>",
+           "config": {"scene": "W4_Bunny", "width": 1920, "height": 1080, "views": 1},
+           "command": "rocprofv3 --pmc <group> -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline "
+                      "(tools/profile.sh, one group per pass)",
+           **rec,
+           "hbm_bytes_per_launch": int(round((2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024)),
+           "hbm_note": "2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes); FETCH_SIZE doubled per MI355X_MICROARCH.md "
+                       "(gfx950 tallies 128-B reads at 64 B). WRITE_SIZE = 4 B/pixel frame store.",
+           "kernel_version": sys.argv[2] + " (profiles/r01/ablate_history.md)"}
+print(json.dumps(rec, indent=1))
