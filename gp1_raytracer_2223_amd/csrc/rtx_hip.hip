@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cfloat>
 #include <cstdio>
 #include <cstdlib>
@@ -88,8 +89,10 @@ __device__ __forceinline__ uint32_t ldc(const uint32_t* base, uint32_t i) {
     return ((const RTX_CONST uint32_t*)base)[i];
 }
 // one 64-byte record (Tri, NodePair): a single s_load_dwordx16 when the index is uniform
-__device__ __forceinline__ void ldc64(const void* base, uint32_t i, float4& a, float4& b, float4& c, float4& d) {
-    const cf16 v = ((const RTX_CONST cf16*)base)[i];
+// 64-byte record at a BYTE offset: the offset goes into the SGPR-offset field of
+// s_load_dwordx16, so walking a link costs no scalar address arithmetic.
+__device__ __forceinline__ void ldcb64(const void* base, uint32_t off, float4& a, float4& b, float4& c, float4& d) {
+    const cf16 v = *(const RTX_CONST cf16*)((const RTX_CONST char*)base + off);
     a = make_float4(v[0], v[1], v[2], v[3]);
     b = make_float4(v[4], v[5], v[6], v[7]);
     c = make_float4(v[8], v[9], v[10], v[11]);
@@ -153,6 +156,10 @@ __device__ __forceinline__ unsigned long long plane_same_sign(float num, float d
 // `cs` is the mesh's cull sign: -1 FrontFaceCulling (reject cullDot < 0), +1
 // BackFaceCulling (reject cullDot > 0), 0 NoCulling (the term 0*cullDot never exceeds 0);
 // shadow rays pass -cs, which is the reference's front/back swap.
+#ifndef RTX_TRI_NOFIX
+#define RTX_TRI_NOFIX 1
+#endif
+template <bool FAST>
 __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const float4 C, float cs, const Ray& r,
                                        float& t) {
     const float cullDot = A.w * r.dx + B.w * r.dy + C.w * r.dz;
@@ -163,9 +170,11 @@ __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const flo
     const float a = B.x * hx + B.y * hy + B.z * hz;
     rej = fmaxf(rej, FLT_EPSILON - fabsf(a));
     // RN(1/a): lanes with |a| < EPS are rejected above whatever ai is, so only huge, inf
-    // and NaN a need the IEEE sequence (NaN gives NaN either way)
+    // and NaN a need the IEEE sequence (NaN gives NaN either way).  FAST: every direction
+    // is finite with |d| < 2 and the scene's |e1||e2| <= 2^56 (DevScene::tri_fast), so
+    // |a| <= |e1||d||e2| < 2^60 and rcp_rn is exact without the check.
     float ai = rcp_rn(a);
-    if (__builtin_expect(fabsf(a) > 0x1p60f, 0)) ai = 1.f / a;
+    if (!(FAST && RTX_TRI_NOFIX) && __builtin_expect(fabsf(a) > 0x1p60f, 0)) ai = 1.f / a;
     const float sx = r.ox - A.x, sy = r.oy - A.y, sz = r.oz - A.z;
     const float u = ai * (sx * hx + sy * hy + sz * hz);
     rej = fmaxf(rej, fmaxf(-u, u - 1.f));
@@ -184,8 +193,14 @@ __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const flo
 // direction is finite (decided once per ray batch with a ballot).
 // Returned as a wave lane mask: one v_cmp per condition straight into SGPRs (a ballot
 // of the && would materialise the bool in a VGPR and compare it again).
+#ifndef RTX_OPAQUE_MR
+#define RTX_OPAQUE_MR 1
+#endif
+#ifndef RTX_SLAB_FOLD
+#define RTX_SLAB_FOLD 1
+#endif
 template <bool FAST>
-__device__ __forceinline__ unsigned long long slab_mask(const float4 mn, const float4 mx, const Ray& r, float& tEnter) {
+__device__ __forceinline__ unsigned long long slab_mask(const float4 mn, const float4 mx, const Ray& r) {
     const float tx1 = (mn.x - r.ox) * r.ix, tx2 = (mx.x - r.ox) * r.ix;
     const float ty1 = (mn.y - r.oy) * r.iy, ty2 = (mx.y - r.oy) * r.iy;
     const float tz1 = (mn.z - r.oz) * r.iz, tz2 = (mx.z - r.oz) * r.iz;
@@ -193,6 +208,9 @@ __device__ __forceinline__ unsigned long long slab_mask(const float4 mn, const f
     if (FAST) {
         tMin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
         tMax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+        // no NaN here: tMax > 0 && tMax >= tMin  <=>  tMax >= max(tMin, smallest denormal)
+        // (f32 denormals are kept, .amdhsa_float_denorm_mode_32 = 3): one compare, no s_and
+        if (RTX_SLAB_FOLD) return ballot(tMax >= fmaxf(tMin, 0x1p-149f));
     } else {
         tMin = smin(tx1, tx2);
         tMax = smax(tx1, tx2);
@@ -201,17 +219,15 @@ __device__ __forceinline__ unsigned long long slab_mask(const float4 mn, const f
         tMin = smax(tMin, smin(tz1, tz2));
         tMax = smin(tMax, smax(tz1, tz2));
     }
-    tEnter = tMin;
     return ballot(tMax > 0) & ballot(tMax >= tMin);
 }
-template <bool FAST>
-__device__ __forceinline__ unsigned long long slab_mask(const float4 mn, const float4 mx, const Ray& r) {
-    float t;
-    return slab_mask<FAST>(mn, mx, r, t);
-}
 
+// FAST-path condition for one ray: every inverse direction component finite AND non-zero
+// (so the direction itself is finite too).  v_cmp_class: +-normal, +-denormal.
 __device__ __forceinline__ bool finite_inv(const Ray& r) {
-    return fabsf(r.ix) <= FLT_MAX && fabsf(r.iy) <= FLT_MAX && fabsf(r.iz) <= FLT_MAX;
+    constexpr int kFiniteNonZero = 0x198;
+    return __builtin_amdgcn_classf(r.ix, kFiniteNonZero) && __builtin_amdgcn_classf(r.iy, kFiniteNonZero) &&
+           __builtin_amdgcn_classf(r.iz, kFiniteNonZero);
 }
 
 __device__ __forceinline__ float cull_sign(int cull, bool shadow) {
@@ -253,11 +269,11 @@ __device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t lin
             if (RTX_STAMPS && !COUNT && lane == 0) cnt.c[kTri] += ntri * __popcll(ANY ? (m & live) : m);
             const bool in = (m >> lane) & 1ull;
             for (uint32_t k = 0; k < ntri; ++k) {
-                const uint32_t ti = link + k;
+                const uint32_t ti = link + k * 64u;   // byte offset of the triangle record
                 Tri T;
-                ldc64(S.tris, ti, T.a, T.b, T.c, T.d);
+                ldcb64(S.tris, ti, T.a, T.b, T.c, T.d);
                 float t;
-                const float rej = tri_t(T.a, T.b, T.c, cs, r, t);
+                const float rej = tri_t<FAST>(T.a, T.b, T.c, cs, r, t);
                 if (ANY) {
                     if (COUNT && ((m & live) >> lane) & 1ull) cnt.c[kTri]++;
                     live &= ~(ballot(!(rej > 0.f)) & ballot(!(t >= r.tmax)) & m);
@@ -278,16 +294,25 @@ __device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t lin
             if ((COUNT || RTX_STAMPS) && lane == 0) cnt.c[kWaveNodeTests]++;
             if (RTX_STAMPS && !COUNT && lane == 0) cnt.c[kSlab] += 2 * __popcll(m);
             NodePair P;
-            ldc64(S.nodes, link >> 1, P.l0, P.l1, P.r0, P.r1);
+            ldcb64(S.nodes, link, P.l0, P.l1, P.r0, P.r1);
             const unsigned long long ml = slab_mask<FAST>(P.l0, P.l1, r) & m;
             const unsigned long long mr = slab_mask<FAST>(P.r0, P.r1, r) & m;
             const bool in = COUNT && ((m >> lane) & 1ull);
             if (COUNT && in) cnt.c[kSlab]++;               // left child's test
             if (COUNT && !ANY && in) cnt.c[kSlab]++;       // right child's (closest: always reached)
             if (ml) {
-                if (mr || (COUNT && ANY)) {                // any-hit COUNT: right is counted at pop
+#if RTX_OPAQUE_MR
+                // an opaque copy keeps this test local to the block: a `mr != 0` shared with
+                // the test below is hoisted and carried across blocks as a VGPR boolean
+                // (s_cselect + v_cndmask + v_cmp per node pair)
+                unsigned long long mrl = mr;
+                asm("" : "+s"(mrl));
+#else
+                const unsigned long long mrl = mr;
+#endif
+                if (mrl || (COUNT && ANY)) {               // any-hit COUNT: right is counted at pop
                     stk[sp] = make_uint4(__float_as_uint(P.r0.w), __float_as_uint(P.r1.w),
-                                         static_cast<uint32_t>(mr), static_cast<uint32_t>(mr >> 32));
+                                         static_cast<uint32_t>(mrl), static_cast<uint32_t>(mrl >> 32));
                     if (COUNT && ANY) sT[sp] = m;
                     ++sp;
                 }
@@ -355,7 +380,7 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, uns
     const uint32_t path = static_cast<uint32_t>(E.z);
     for (int d = 0; d < E.w && m; ++d) {
         NodePair P;
-        ldc64(S.nodes, link >> 1, P.l0, P.l1, P.r0, P.r1);
+        ldcb64(S.nodes, link, P.l0, P.l1, P.r0, P.r1);
         const bool right = (path >> d) & 1u;
         const float4 c0 = right ? P.r0 : P.l0, c1 = right ? P.r1 : P.l1;
         m &= slab_mask<FAST>(c0, c1, r);
@@ -527,7 +552,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     div3_exact(dx, dy, dz, dm);   // dx /= dm; ... (Vector3::Normalize)
     const Ray vr = make_ray(V.origin[0], V.origin[1], V.origin[2], dx, dy, dz, 0.0001f, FLT_MAX);
     const unsigned long long active = ballot(valid);
-    const bool fast = (ballot(valid && !finite_inv(vr)) == 0);
+    const bool fast = (ballot(valid && !finite_inv(vr)) == 0) && S.tri_fast;
 
     // ---- Scene::GetClosestHit (Scene.cpp:29-66)
     float best_t = FLT_MAX, sc_t = FLT_MAX;
@@ -607,7 +632,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
             mat = __float_as_uint(p0.w);
         } else {
             Tri T;
-            ldc64(S.tris, best_idx, T.a, T.b, T.c, T.d);
+            ldcb64(S.tris, best_idx, T.a, T.b, T.c, T.d);   // best_idx: byte offset
             nx = T.a.w; ny = T.b.w; nz = T.c.w;
             mat = __float_as_uint(T.d.x);
         }
@@ -635,7 +660,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                 // lanes still without an occluder (first hit wins, order irrelevant for a bool)
                 const Ray sr = make_ray(oox, ooy, ooz, lx, ly, lz, 0.0001f, mag);
                 unsigned long long live = hitmask;
-                const bool sfast = (wballot(did && !finite_inv(sr)) == 0);
+                const bool sfast = (wballot(did && !finite_inv(sr)) == 0) && S.tri_fast;
                 if (COUNT && did) cnt.c[kShadow]++;
                 for (uint32_t i = 0; i < (PHASE == 2 ? 0u : S.n_spheres) && live; ++i) {
                     const float4 s = ldc(S.spheres, i);
@@ -1103,6 +1128,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     std::vector<uint32_t> sph_mat;
     std::vector<int4> meshes, parts;
     bool split_ok = s->n_lights <= static_cast<uint32_t>(kMaxSplitLights);
+    double max_ee = 0.0;   // max |e1| * |e2| over the triangles (DevScene::tri_fast)
     for (uint32_t i = 0; i < s->n_spheres; ++i) {
         const rtx_sphere& p = s->spheres[i];
         if (p.material >= nm) return fail(c, RTX_E_INVALID, "sphere material out of range");
@@ -1133,9 +1159,14 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
             const float* v2 = m.positions + 3 * i2;
             const float* n = m.normals + 3 * k;
             // edge1 = v1 - v0, edge2 = v2 - v0 (Utils.h:139-140), same binary32 ops as on device
+            const float4 e1 = f4(v1[0] - v0[0], v1[1] - v0[1], v1[2] - v0[2], n[1]);
+            const float4 e2 = f4(v2[0] - v0[0], v2[1] - v0[1], v2[2] - v0[2], n[2]);
             tri.push_back(f4(v0[0], v0[1], v0[2], n[0]));
-            tri.push_back(f4(v1[0] - v0[0], v1[1] - v0[1], v1[2] - v0[2], n[1]));
-            tri.push_back(f4(v2[0] - v0[0], v2[1] - v0[1], v2[2] - v0[2], n[2]));
+            tri.push_back(e1);
+            tri.push_back(e2);
+            const double ee = std::sqrt(double(e1.x) * e1.x + double(e1.y) * e1.y + double(e1.z) * e1.z) *
+                              std::sqrt(double(e2.x) * e2.x + double(e2.y) * e2.y + double(e2.z) * e2.z);
+            max_ee = (ee > max_ee || ee != ee) ? ee : max_ee;   // NaN sticks
             tri.push_back(f4(bits(m.material), 0.f, 0.f, 0.f));
         }
         uint32_t root = 0;
@@ -1179,6 +1210,16 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     }
     if (parts.size() > static_cast<size_t>(kMaxParts)) split_ok = false;
     if (!split_ok) parts.clear();
+    // Device links are byte offsets (s_load with an SGPR offset, no address arithmetic):
+    // inner node -> its child pair (2 slots x 32 B), leaf -> its first 64-B triangle.
+    if (tri.size() * 16 >= (1ull << 32) || nodes.size() * 16 >= (1ull << 32))
+        return fail(c, RTX_E_INVALID, "scene too large for 32-bit record offsets");
+    for (size_t n = 0; n < nodes.size(); n += 2) {
+        uint32_t link, cnt;
+        std::memcpy(&link, &nodes[n].w, 4);
+        std::memcpy(&cnt, &nodes[n + 1].w, 4);
+        nodes[n].w = bits(cnt ? link * 64u : link * 32u);
+    }
     for (uint32_t i = 0; i < s->n_lights; ++i) {
         const rtx_light& l = s->lights[i];
         lights.push_back(f4(l.origin[0], l.origin[1], l.origin[2], bitsi(l.type)));
@@ -1243,6 +1284,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     d.n_parts = static_cast<uint32_t>(parts.size());
     d.n_spheres = s->n_spheres; d.n_planes = s->n_planes; d.n_meshes = s->n_meshes;
     d.n_lights = s->n_lights; d.n_materials = nm;
+    d.tri_fast = max_ee <= 0x1p56 ? 1u : 0u;
     d.n_tris = static_cast<uint32_t>(tri.size() / 4); d.n_nodes = static_cast<uint32_t>(nodes.size() / 2);
     c->dev = d;
     c->split_ok = split_ok && !parts.empty();

@@ -59,6 +59,9 @@ struct DevScene {
     // depth d+1), depth} — every triangle of every mesh lies under exactly one entry
     const int4* __restrict__ parts;
     uint32_t n_spheres, n_planes, n_meshes, n_lights, n_materials, n_tris, n_nodes, n_parts;
+    // every triangle has |e1| * |e2| <= 2^56: with |d| < 2, Moller-Trumbore's determinant
+    // stays inside the exact fast-reciprocal domain (rtx_fastdiv.h)
+    uint32_t tri_fast;
 };
 
 constexpr int kMaxViews = 8;   // views (camera positions) rendered by one launch
