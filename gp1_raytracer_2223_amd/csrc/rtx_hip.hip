@@ -88,9 +88,26 @@ __device__ __forceinline__ int4 ldc(const int4* base, uint32_t i) {
 __device__ __forceinline__ uint32_t ldc(const uint32_t* base, uint32_t i) {
     return ((const RTX_CONST uint32_t*)base)[i];
 }
-// one 64-byte record (Tri, NodePair): a single s_load_dwordx16 when the index is uniform
-// 64-byte record at a BYTE offset: the offset goes into the SGPR-offset field of
-// s_load_dwordx16, so walking a link costs no scalar address arithmetic.
+typedef float cf8 __attribute__((ext_vector_type(8)));
+// A wave-uniform value the optimiser cannot see through: a loop counter passed through it
+// stays a 32-bit SGPR offset instead of being widened into a 64-bit pointer induction
+// (which costs an s_add_u32/s_addc_u32 pair per record).
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+    asm("" : "+s"(x));
+    return x;
+}
+// Records at a BYTE offset: the offset goes into the SGPR-offset field of s_load, so a
+// loop over records or a link walk costs no scalar address arithmetic.
+__device__ __forceinline__ float4 ldcb16(const void* base, uint32_t off) {
+    const cf4 v = *(const RTX_CONST cf4*)((const RTX_CONST char*)base + off);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void ldcb32(const void* base, uint32_t off, float4& a, float4& b) {
+    const cf8 v = *(const RTX_CONST cf8*)((const RTX_CONST char*)base + off);
+    a = make_float4(v[0], v[1], v[2], v[3]);
+    b = make_float4(v[4], v[5], v[6], v[7]);
+}
+// 64-byte record (Tri, NodePair): one s_load_dwordx16
 __device__ __forceinline__ void ldcb64(const void* base, uint32_t off, float4& a, float4& b, float4& c, float4& d) {
     const cf16 v = *(const RTX_CONST cf16*)((const RTX_CONST char*)base + off);
     a = make_float4(v[0], v[1], v[2], v[3]);
@@ -556,9 +573,10 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
 
     // ---- Scene::GetClosestHit (Scene.cpp:29-66)
     float best_t = FLT_MAX, sc_t = FLT_MAX;
-    uint32_t best_kind = 0, best_idx = 0;   // kind: 0 none, 1 sphere, 2 plane, 3 triangle
-    for (uint32_t i = 0; i < S.n_spheres; ++i) {
-        const float4 s = ldc(S.spheres, i);
+    // kind: 0 none, 1 sphere, 2 plane, 3 triangle; best_idx: the record's BYTE offset
+    uint32_t best_kind = 0, best_idx = 0;
+    for (uint32_t i = 0; i < S.n_spheres * 16u; i += 16u) {
+        const float4 s = ldcb16(S.spheres, opaque(i));
         if (COUNT && valid) cnt.c[kSphere]++;
         float t;
         const bool h = valid && sphere_t(s, vr, t);
@@ -568,8 +586,9 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         best_kind = b ? 1u : best_kind;
         best_idx = b ? i : best_idx;
     }
-    for (uint32_t i = 0; i < ((RTX_ABL_PPLANE) ? 0u : S.n_planes); ++i) {
-        const float4 p0 = ldc(S.planes, 2 * i), p1 = ldc(S.planes, 2 * i + 1);
+    for (uint32_t i = 0; i < ((RTX_ABL_PPLANE) ? 0u : S.n_planes * 32u); i += 32u) {
+        float4 p0, p1;
+        ldcb32(S.planes, opaque(i), p0, p1);
         if (COUNT && valid) cnt.c[kPlane]++;
         const float num = plane_num(p0, p1, vr), den = plane_den(p1, vr);
         if (!(plane_same_sign(num, den) & active)) continue;   // no lane can have t >= tmin > 0
@@ -621,13 +640,14 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     if (did) {
         hx = vr.ox + vr.dx * best_t; hy = vr.oy + vr.dy * best_t; hz = vr.oz + vr.dz * best_t;
         if (best_kind == 1) {
-            const float4 s = ldc(S.spheres, best_idx);
+            const float4 s = ldcb16(S.spheres, best_idx);
             nx = hx - s.x; ny = hy - s.y; nz = hz - s.z;
             const float m = sqrtf(nx * nx + ny * ny + nz * nz);   // closestHit.normal.Normalize()
             nx /= m; ny /= m; nz /= m;
-            mat = ldc(S.sphere_mat, best_idx);
+            mat = ldc(S.sphere_mat, best_idx >> 4);
         } else if (best_kind == 2) {
-            const float4 p0 = ldc(S.planes, 2 * best_idx), p1 = ldc(S.planes, 2 * best_idx + 1);
+            float4 p0, p1;
+            ldcb32(S.planes, best_idx, p0, p1);
             nx = p1.x; ny = p1.y; nz = p1.z;
             mat = __float_as_uint(p0.w);
         } else {
@@ -662,22 +682,27 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                 unsigned long long live = hitmask;
                 const bool sfast = (wballot(did && !finite_inv(sr)) == 0) && S.tri_fast;
                 if (COUNT && did) cnt.c[kShadow]++;
-                for (uint32_t i = 0; i < (PHASE == 2 ? 0u : S.n_spheres) && live; ++i) {
-                    const float4 s = ldc(S.spheres, i);
+                // (single-condition loops with a separate exit test: a `&& live` loop
+                // condition is carried as a VGPR boolean by the compiler)
+                for (uint32_t i = 0; i < (PHASE == 2 ? 0u : S.n_spheres * 16u); i += 16u) {
+                    if (!live) break;
+                    const float4 s = ldcb16(S.spheres, opaque(i));
                     if (COUNT && ((live >> lane) & 1ull)) cnt.c[kSphere]++;
                     float t;
                     live &= ~wballot(sphere_t(s, sr, t));
                 }
-                for (uint32_t i = 0; i < ((RTX_ABL_SPLANE || PHASE == 2) ? 0u : S.n_planes) && live; ++i) {
-                    const float4 p0 = ldc(S.planes, 2 * i), p1 = ldc(S.planes, 2 * i + 1);
+                for (uint32_t i = 0; i < ((RTX_ABL_SPLANE || PHASE == 2) ? 0u : S.n_planes * 32u); i += 32u) {
+                    float4 p0, p1;
+                    ldcb32(S.planes, opaque(i), p0, p1);
                     if (COUNT && ((live >> lane) & 1ull)) cnt.c[kPlane]++;
                     const float num = plane_num(p0, p1, sr), den = plane_den(p1, sr);
                     const unsigned long long cand = plane_same_sign(num, den) & live;
-                    if (!cand) continue;
+                    if (!cand) continue;   // also taken once no lane is live
                     const float t = num / den;
                     live &= ~(ballot(t >= sr.tmin) & ballot(t < sr.tmax) & cand);
                 }
-                for (uint32_t mi = 0; mi < ((RTX_ABL_SMESH || PHASE != 0) ? 0u : S.n_meshes) && live; ++mi) {
+                for (uint32_t mi = 0; mi < ((RTX_ABL_SMESH || PHASE != 0) ? 0u : S.n_meshes); ++mi) {
+                    if (!live) break;
                     float st = 0.f;
                     uint32_t stri = 0;
                     if (sfast)
@@ -1212,7 +1237,8 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     if (!split_ok) parts.clear();
     // Device links are byte offsets (s_load with an SGPR offset, no address arithmetic):
     // inner node -> its child pair (2 slots x 32 B), leaf -> its first 64-B triangle.
-    if (tri.size() * 16 >= (1ull << 32) || nodes.size() * 16 >= (1ull << 32))
+    if (tri.size() * 16 >= (1ull << 32) || nodes.size() * 16 >= (1ull << 32) || sph.size() * 16 >= (1ull << 32) ||
+        pl.size() * 16 >= (1ull << 32))
         return fail(c, RTX_E_INVALID, "scene too large for 32-bit record offsets");
     for (size_t n = 0; n < nodes.size(); n += 2) {
         uint32_t link, cnt;
