@@ -51,12 +51,25 @@ __device__ __forceinline__ float rcp_exact(float b) {
     return y;
 }
 
+// RN(1/x), RN(1/y), RN(1/z) with ONE domain test for the three (v_min3/v_max3 of the
+// magnitudes): the IEEE fallback runs only in lanes where some component is outside.
+__device__ __forceinline__ void rcp3_exact(float x, float y, float z, float& rx, float& ry, float& rz) {
+    rx = rcp_rn(x); ry = rcp_rn(y); rz = rcp_rn(z);
+    const float lo = fminf(fminf(fabsf(x), fabsf(y)), fabsf(z));
+    const float hi = fmaxf(fmaxf(fabsf(x), fabsf(y)), fabsf(z));
+    // a NaN component (dropped by v_min/v_max) gives NaN on both paths
+    if (__builtin_expect(!(lo >= 0x1p-60f && hi <= 0x1p60f), 0)) {
+        rx = 1.f / x; ry = 1.f / y; rz = 1.f / z;
+    }
+}
+
 // (x, y, z) / m, each correctly rounded, for m = |(x, y, z)| as computed by the caller.
 __device__ __forceinline__ void div3_exact(float& x, float& y, float& z, float m) {
     const float r = rcp_rn(m);
     const float qx = div_rn(x, m, r), qy = div_rn(y, m, r), qz = div_rn(z, m, r);
-    const float lo = 0x1p-60f;
-    if (__builtin_expect(!(fast_rcp_ok(m) && fabsf(x) >= lo && fabsf(y) >= lo && fabsf(z) >= lo), 0)) {
+    // a NaN component (dropped by v_min) gives NaN on both paths; inf makes m inf -> IEEE
+    const float lo = fminf(fminf(fabsf(x), fabsf(y)), fabsf(z));
+    if (__builtin_expect(!(fast_rcp_ok(m) && lo >= 0x1p-60f), 0)) {
         x = x / m; y = y / m; z = z / m;
     } else {
         x = qx; y = qy; z = qz;

@@ -66,7 +66,6 @@ __device__ __forceinline__ unsigned long long uni64(unsigned long long x) {
     return (static_cast<unsigned long long>(hi) << 32) | lo;
 }
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-__device__ __forceinline__ unsigned long long wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 // Scene records are immutable for a whole launch: they are read through the constant
 // address space, so every wave-uniform read is an s_load through the scalar cache.  With
@@ -102,6 +101,10 @@ __device__ __forceinline__ float4 ldcb16(const void* base, uint32_t off) {
     const cf4 v = *(const RTX_CONST cf4*)((const RTX_CONST char*)base + off);
     return make_float4(v.x, v.y, v.z, v.w);
 }
+__device__ __forceinline__ int4 ldcb16i(const void* base, uint32_t off) {
+    const ci4 v = *(const RTX_CONST ci4*)((const RTX_CONST char*)base + off);
+    return make_int4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ void ldcb32(const void* base, uint32_t off, float4& a, float4& b) {
     const cf8 v = *(const RTX_CONST cf8*)((const RTX_CONST char*)base + off);
     a = make_float4(v[0], v[1], v[2], v[3]);
@@ -125,22 +128,25 @@ __device__ __forceinline__ Ray make_ray(float ox, float oy, float oz, float dx, 
                                         float tmax) {
     Ray r;
     r.ox = ox; r.oy = oy; r.oz = oz; r.dx = dx; r.dy = dy; r.dz = dz;
-    r.ix = rcp_exact(dx); r.iy = rcp_exact(dy); r.iz = rcp_exact(dz);
+    rcp3_exact(dx, dy, dz, r.ix, r.iy, r.iz);
     r.tmin = tmin; r.tmax = tmax;
     return r;
 }
 
-// HitTest_Sphere (Utils.h:52-66) — t and the accept test; hit data is rebuilt later.
-// Branch-free: sqrtf of a negative argument is computed and discarded.
-__device__ __forceinline__ bool sphere_t(const float4 s, const Ray& r, float& t) {
+// HitTest_Sphere (Utils.h:52-66) in two steps, so that the square root (16 VALU when
+// correctly rounded) runs only when some lane's ray passes within the radius:
+//   sphere_perp: squared distance of the centre from the ray line (reject if r^2 < perp)
+//   sphere_t:    t = proj - sqrt(r^2 - perp) and the [tmin, tmax] test
+struct SphereProj {
+    float proj, perp;
+};
+__device__ __forceinline__ SphereProj sphere_perp(const float4 s, const Ray& r) {
     const float ovx = s.x - r.ox, ovy = s.y - r.oy, ovz = s.z - r.oz;
     const float ovs = ovx * ovx + ovy * ovy + ovz * ovz;
     const float proj = r.dx * ovx + r.dy * ovy + r.dz * ovz;
-    const float perp = ovs - proj * proj;
-    const float dist = sqrtf(s.w - perp);
-    t = proj - dist;
-    return !(s.w < perp) && !(t < r.tmin || t > r.tmax);
+    return {proj, ovs - proj * proj};
 }
+__device__ __forceinline__ float sphere_t(const float4 s, const SphereProj& q) { return q.proj - sqrtf(s.w - q.perp); }
 
 // HitTest_Plane (Utils.h:84-97): t = num / den.  With tmin > 0 (every ray here), a hit
 // needs t > 0, i.e. num and den non-zero with the same sign: RN(num/den) carries the exact
@@ -216,11 +222,13 @@ __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const flo
 #ifndef RTX_SLAB_FOLD
 #define RTX_SLAB_FOLD 1
 #endif
+// Node record (32 B): a = {min.x, min.y, min.z, max.x}, b = {max.y, max.z, link, ntri}:
+// link and triangle count are adjacent, one 64-bit SGPR pair the traversal selects whole.
 template <bool FAST>
-__device__ __forceinline__ unsigned long long slab_mask(const float4 mn, const float4 mx, const Ray& r) {
-    const float tx1 = (mn.x - r.ox) * r.ix, tx2 = (mx.x - r.ox) * r.ix;
-    const float ty1 = (mn.y - r.oy) * r.iy, ty2 = (mx.y - r.oy) * r.iy;
-    const float tz1 = (mn.z - r.oz) * r.iz, tz2 = (mx.z - r.oz) * r.iz;
+__device__ __forceinline__ unsigned long long slab_mask(const float4 a, const float4 b, const Ray& r) {
+    const float tx1 = (a.x - r.ox) * r.ix, tx2 = (a.w - r.ox) * r.ix;
+    const float ty1 = (a.y - r.oy) * r.iy, ty2 = (b.x - r.oy) * r.iy;
+    const float tz1 = (a.z - r.oz) * r.iz, tz2 = (b.y - r.oz) * r.iz;
     float tMin, tMax;
     if (FAST) {
         tMin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
@@ -241,20 +249,28 @@ __device__ __forceinline__ unsigned long long slab_mask(const float4 mn, const f
 
 // FAST-path condition for one ray: every inverse direction component finite AND non-zero
 // (so the direction itself is finite too).  v_cmp_class: +-normal, +-denormal.
-__device__ __forceinline__ bool finite_inv(const Ray& r) {
+// As a lane mask: one ballot per v_cmp_class (a ballot of the combined bool would be
+// materialised in a VGPR and compared again).
+__device__ __forceinline__ unsigned long long finite_inv_mask(const Ray& r) {
     constexpr int kFiniteNonZero = 0x198;
-    return __builtin_amdgcn_classf(r.ix, kFiniteNonZero) && __builtin_amdgcn_classf(r.iy, kFiniteNonZero) &&
-           __builtin_amdgcn_classf(r.iz, kFiniteNonZero);
+    return ballot(__builtin_amdgcn_classf(r.ix, kFiniteNonZero)) & ballot(__builtin_amdgcn_classf(r.iy, kFiniteNonZero)) &
+           ballot(__builtin_amdgcn_classf(r.iz, kFiniteNonZero));
 }
 
-__device__ __forceinline__ float cull_sign(int cull, bool shadow) {
-    const float cs = cull == RTX_CULL_FRONT ? -1.f : (cull == RTX_CULL_BACK ? 1.f : 0.f);
+// The mesh record carries its cull sign as float bits (set at upload: -1 FrontFaceCulling,
+// +1 BackFaceCulling, 0 NoCulling); shadow rays use the negation, the reference's swap.
+__device__ __forceinline__ float cull_sign(int cs_bits, bool shadow) {
+    const float cs = __int_as_float(cs_bits);
     return shadow ? -cs : cs;
 }
 
 struct alignas(64) NodePair {
-    float4 l0, l1, r0, r1;   // left child {min, link}, {max, ntri}; right child likewise
+    float4 l0, l1, r0, r1;   // left child (a, b) then right child (a, b), see slab_mask
 };
+// (link, ntri) of a child as one 64-bit value: link low, count high
+__device__ __forceinline__ unsigned long long link_ntri(const float4 b) {
+    return (static_cast<unsigned long long>(__float_as_uint(b.w)) << 32) | __float_as_uint(b.z);
+}
 
 struct Counts {
     uint32_t c[kNumCounters];
@@ -328,19 +344,19 @@ __device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t lin
                 const unsigned long long mrl = mr;
 #endif
                 if (mrl || (COUNT && ANY)) {               // any-hit COUNT: right is counted at pop
-                    stk[sp] = make_uint4(__float_as_uint(P.r0.w), __float_as_uint(P.r1.w),
+                    stk[sp] = make_uint4(__float_as_uint(P.r1.z), __float_as_uint(P.r1.w),
                                          static_cast<uint32_t>(mrl), static_cast<uint32_t>(mrl >> 32));
                     if (COUNT && ANY) sT[sp] = m;
                     ++sp;
                 }
-                link = __float_as_uint(P.l0.w);
+                link = __float_as_uint(P.l1.z);
                 ntri = __float_as_uint(P.l1.w);
                 m = ml;
                 continue;
             }
             if (COUNT && ANY && in) cnt.c[kSlab]++;        // right child's test, reached now
             if (mr) {
-                link = __float_as_uint(P.r0.w);
+                link = __float_as_uint(P.r1.z);
                 ntri = __float_as_uint(P.r1.w);
                 m = mr;
                 continue;
@@ -366,18 +382,89 @@ __device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t lin
     }
 }
 
+#ifndef RTX_LEAN_WALK
+#define RTX_LEAN_WALK 1
+#endif
+// bvh_walk without counters, shaped for the scalar unit: one inner loop descends through
+// inner nodes with scalar selects (no i1 value crosses a block, so nothing is carried as a
+// VGPR boolean or a lane-mask flow variable), a dead end leaves it as an empty "leaf", and
+// the pop loop is the only other path.  Same visits, tests and order as bvh_walk.
+template <bool ANY, bool FAST>
+__device__ void bvh_walk_lean(const DevScene& S, float cs, const Ray& r, uint32_t link, uint32_t ntri,
+                              unsigned long long m, unsigned long long mask, uint32_t lane, uint4* stk, float& sc_t,
+                              uint32_t& sc_tri, unsigned long long& live, const uint32_t* occ_word, uint32_t occ_bit) {
+    uint32_t sp = 0;
+    for (;;) {
+        while (ntri == 0) {
+            NodePair P;
+            ldcb64(S.nodes, link, P.l0, P.l1, P.r0, P.r1);
+            const unsigned long long ml = slab_mask<FAST>(P.l0, P.l1, r) & m;
+            const unsigned long long mr = slab_mask<FAST>(P.r0, P.r1, r) & m;
+            if (ml != 0 && mr != 0) {   // both: descend left, the right child waits on the stack
+                stk[sp] = make_uint4(__float_as_uint(P.r1.z), __float_as_uint(P.r1.w), static_cast<uint32_t>(mr),
+                                     static_cast<uint32_t>(mr >> 32));
+                ++sp;
+            }
+            // next (link, ntri): left, else right, else a dead end taken as an empty leaf
+            // (ntri = 1 with m = 0) — two 64-bit scalar selects
+            unsigned long long nx = mr ? link_ntri(P.r1) : (1ull << 32);
+            nx = ml ? link_ntri(P.l1) : nx;
+            m = ml ? ml : mr;
+            link = static_cast<uint32_t>(nx);
+            ntri = static_cast<uint32_t>(nx >> 32);
+        }
+        if (m) {
+            const bool in = (m >> lane) & 1ull;
+            for (uint32_t k = 0; k < ntri; ++k) {
+                const uint32_t ti = link + k * 64u;
+                Tri T;
+                ldcb64(S.tris, ti, T.a, T.b, T.c, T.d);
+                float t;
+                const float rej = tri_t<FAST>(T.a, T.b, T.c, cs, r, t);
+                if (ANY) {
+                    live &= ~(ballot(!(rej > 0.f)) & ballot(!(t >= r.tmax)) & m);
+                } else {
+                    const bool u = in & !(rej > 0.f) & !(t >= r.tmax) & (t < sc_t);
+                    sc_t = u ? t : sc_t;
+                    sc_tri = u ? ti : sc_tri;
+                }
+            }
+            if (ANY && occ_word) {
+                const uint32_t o = __hip_atomic_load(occ_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                live &= ~ballot((o & occ_bit) != 0u);
+            }
+            if (ANY && (live & mask) == 0) return;
+        }
+        for (;;) {
+            if (sp == 0) return;
+            --sp;
+            const uint4 e = stk[sp];
+            link = uni(e.x);
+            ntri = uni(e.y);
+            m = (static_cast<unsigned long long>(uni(e.w)) << 32) | uni(e.z);
+            if (ANY) m &= live;
+            if (m) break;
+        }
+    }
+}
+
 template <bool ANY, bool FAST, bool COUNT>
 __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, unsigned long long mask, uint32_t lane,
                               uint4* stk, unsigned long long* sT, float& sc_t, uint32_t& sc_tri,
                               unsigned long long& live, Counts& cnt) {
     if (M.y == 0) return;
     // root (odd global index; every child pair starts at an even one, 64-B aligned)
-    const float4 b0 = ldc(S.nodes, 2 * M.x), b1 = ldc(S.nodes, 2 * M.x + 1);
+    float4 b0, b1;
+    ldcb32(S.nodes, static_cast<uint32_t>(M.x), b0, b1);   // M.x: the root's byte offset
     if (COUNT && ((mask >> lane) & 1ull)) cnt.c[kSlab]++;
     const unsigned long long m = slab_mask<FAST>(b0, b1, r) & mask;
     if (m == 0) return;
-    bvh_walk<ANY, FAST, COUNT>(S, cull_sign(M.z, ANY), r, __float_as_uint(b0.w), __float_as_uint(b1.w), m, mask, lane,
-                               stk, sT, sc_t, sc_tri, live, cnt);
+    if (RTX_LEAN_WALK && !COUNT && !RTX_STAMPS)
+        bvh_walk_lean<ANY, FAST>(S, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask, lane,
+                                 stk, sc_t, sc_tri, live, nullptr, 0u);
+    else
+        bvh_walk<ANY, FAST, COUNT>(S, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask,
+                                   lane, stk, sT, sc_t, sc_tri, live, cnt);
 }
 
 // One part of a split traversal: the lanes that reach frontier node E (slab tests of the
@@ -390,10 +477,11 @@ template <bool ANY, bool FAST>
 __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, unsigned long long mask, uint32_t lane,
                               uint4* stk, float& sc_t, uint32_t& sc_tri, unsigned long long& live, Counts& cnt,
                               const uint32_t* occ_word = nullptr, uint32_t occ_bit = 0) {
-    const int4 M = ldc(S.meshes, static_cast<uint32_t>(E.x));
-    const float4 b0 = ldc(S.nodes, 2 * M.x), b1 = ldc(S.nodes, 2 * M.x + 1);
+    const int4 M = ldcb16i(S.meshes, static_cast<uint32_t>(E.x) * 16u);
+    float4 b0, b1;
+    ldcb32(S.nodes, static_cast<uint32_t>(M.x), b0, b1);   // M.x: the root's byte offset
     unsigned long long m = slab_mask<FAST>(b0, b1, r) & mask;
-    uint32_t link = __float_as_uint(b0.w), ntri = __float_as_uint(b1.w);
+    uint32_t link = __float_as_uint(b1.z), ntri = __float_as_uint(b1.w);
     const uint32_t path = static_cast<uint32_t>(E.z);
     for (int d = 0; d < E.w && m; ++d) {
         NodePair P;
@@ -401,12 +489,16 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, uns
         const bool right = (path >> d) & 1u;
         const float4 c0 = right ? P.r0 : P.l0, c1 = right ? P.r1 : P.l1;
         m &= slab_mask<FAST>(c0, c1, r);
-        link = __float_as_uint(c0.w);
+        link = __float_as_uint(c1.z);
         ntri = __float_as_uint(c1.w);
     }
     if (m == 0) return;
-    bvh_walk<ANY, FAST, false>(S, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, nullptr, sc_t, sc_tri, live,
-                               cnt, occ_word, occ_bit);
+    if (RTX_LEAN_WALK && !RTX_STAMPS)
+        bvh_walk_lean<ANY, FAST>(S, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, sc_t, sc_tri, live,
+                                 occ_word, occ_bit);
+    else
+        bvh_walk<ANY, FAST, false>(S, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, nullptr, sc_t, sc_tri,
+                                   live, cnt, occ_word, occ_bit);
 }
 
 struct RGB {
@@ -569,7 +661,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     div3_exact(dx, dy, dz, dm);   // dx /= dm; ... (Vector3::Normalize)
     const Ray vr = make_ray(V.origin[0], V.origin[1], V.origin[2], dx, dy, dz, 0.0001f, FLT_MAX);
     const unsigned long long active = ballot(valid);
-    const bool fast = (ballot(valid && !finite_inv(vr)) == 0) && S.tri_fast;
+    const bool fast = (active & ~finite_inv_mask(vr)) == 0 && S.tri_fast;
 
     // ---- Scene::GetClosestHit (Scene.cpp:29-66)
     float best_t = FLT_MAX, sc_t = FLT_MAX;
@@ -578,10 +670,13 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     for (uint32_t i = 0; i < S.n_spheres * 16u; i += 16u) {
         const float4 s = ldcb16(S.spheres, opaque(i));
         if (COUNT && valid) cnt.c[kSphere]++;
-        float t;
-        const bool h = valid && sphere_t(s, vr, t);
+        const SphereProj q = sphere_perp(s, vr);
+        const unsigned long long near = ballot(!(s.w < q.perp)) & active;
+        if (!near) continue;
+        const float t = sphere_t(s, q);
+        const bool h = ((near >> lane) & 1ull) & !(t < vr.tmin) & !(t > vr.tmax);
         sc_t = h ? t : sc_t;
-        const bool b = h && t < best_t;
+        const bool b = h & (t < best_t);
         best_t = b ? t : best_t;
         best_kind = b ? 1u : best_kind;
         best_idx = b ? i : best_idx;
@@ -595,14 +690,14 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         const float t = num / den;
         const bool h = valid & (t >= vr.tmin) & (t < vr.tmax);
         sc_t = h ? t : sc_t;
-        const bool b = h && t < best_t;
+        const bool b = h & (t < best_t);
         best_t = b ? t : best_t;
         best_kind = b ? 2u : best_kind;
         best_idx = b ? i : best_idx;
     }
     if (PHASE == 0) {
         for (uint32_t mi = 0; mi < ((RTX_ABL_PMESH) ? 0u : S.n_meshes); ++mi) {
-            const int4 M = ldc(S.meshes, mi);
+            const int4 M = ldcb16i(S.meshes, opaque(mi * 16u));
             uint32_t sc_tri = 0;
             unsigned long long unused = 0;
             if (fast)
@@ -668,7 +763,8 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         const float vx = -dx, vy = -dy, vz = -dz;
         const uint32_t l_first = PHASE == 2 ? light : 0u, l_end = PHASE == 2 ? light + 1 : S.n_lights;
         for (uint32_t li = l_first; li < l_end; ++li) {
-            const float4 L0 = ldc(S.lights, 2 * li), L1 = ldc(S.lights, 2 * li + 1);
+            float4 L0, L1;
+            ldcb32(S.lights, opaque(li * 32u), L0, L1);
             const int ltype = __float_as_int(L0.w);
             const bool known = (ltype == RTX_LIGHT_POINT || ltype == RTX_LIGHT_DIRECTIONAL);
             float lx = known ? L0.x - oox : 0.f, ly = known ? L0.y - ooy : 0.f, lz = known ? L0.z - ooz : 0.f;
@@ -680,7 +776,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                 // lanes still without an occluder (first hit wins, order irrelevant for a bool)
                 const Ray sr = make_ray(oox, ooy, ooz, lx, ly, lz, 0.0001f, mag);
                 unsigned long long live = hitmask;
-                const bool sfast = (wballot(did && !finite_inv(sr)) == 0) && S.tri_fast;
+                const bool sfast = (hitmask & ~finite_inv_mask(sr)) == 0 && S.tri_fast;
                 if (COUNT && did) cnt.c[kShadow]++;
                 // (single-condition loops with a separate exit test: a `&& live` loop
                 // condition is carried as a VGPR boolean by the compiler)
@@ -688,8 +784,11 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                     if (!live) break;
                     const float4 s = ldcb16(S.spheres, opaque(i));
                     if (COUNT && ((live >> lane) & 1ull)) cnt.c[kSphere]++;
-                    float t;
-                    live &= ~wballot(sphere_t(s, sr, t));
+                    const SphereProj q = sphere_perp(s, sr);
+                    const unsigned long long near = ballot(!(s.w < q.perp)) & live;
+                    if (!near) continue;
+                    const float t = sphere_t(s, q);
+                    live &= ~(near & ballot(!(t < sr.tmin)) & ballot(!(t > sr.tmax)));
                 }
                 for (uint32_t i = 0; i < ((RTX_ABL_SPLANE || PHASE == 2) ? 0u : S.n_planes * 32u); i += 32u) {
                     float4 p0, p1;
@@ -706,9 +805,9 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                     float st = 0.f;
                     uint32_t stri = 0;
                     if (sfast)
-                        mesh_traverse<true, true, COUNT>(S, ldc(S.meshes, mi), sr, live, lane, stk, sT, st, stri, live, cnt);
+                        mesh_traverse<true, true, COUNT>(S, ldcb16i(S.meshes, opaque(mi * 16u)), sr, live, lane, stk, sT, st, stri, live, cnt);
                     else
-                        mesh_traverse<true, false, COUNT>(S, ldc(S.meshes, mi), sr, live, lane, stk, sT, st, stri, live,
+                        mesh_traverse<true, false, COUNT>(S, ldcb16i(S.meshes, opaque(mi * 16u)), sr, live, lane, stk, sT, st, stri, live,
                                                           cnt);
                 }
                 if (PHASE == 2) {
@@ -724,7 +823,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                     if (did && !((live >> lane) & 1ull)) atomicOr(&F.occ_bits[slot], 1u << li);
                     continue;
                 }
-                occ = did && !((live >> lane) & 1ull);
+                occ = did & !((live >> lane) & 1ull);
                 if (PHASE == 3) occ = occ || (did && ((F.occ_bits[slot] >> li) & 1u));
             }
             if (!did) continue;
@@ -980,6 +1079,7 @@ int fail(rtx_ctx* c, int code, const std::string& msg) {
 inline float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
 inline float bits(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 inline float bitsi(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
+inline int32_t bitsi_f(float f) { int32_t i; std::memcpy(&i, &f, 4); return i; }
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // Deepest DFS stack a wave can need for this BVH (pending right siblings on a path).
@@ -1010,7 +1110,7 @@ bool bvh_depth_ok(const rtx_mesh& m, std::string& why) {
 // to the reference's first-found closest hit — so the scene is rendered unsplit.
 bool build_parts(const std::vector<float4>& nodes, uint32_t root, uint32_t mesh, uint32_t target,
                  std::vector<int4>& parts) {
-    auto link = [&](uint32_t n) { uint32_t u; std::memcpy(&u, &nodes[2 * n].w, 4); return u; };
+    auto link = [&](uint32_t n) { uint32_t u; std::memcpy(&u, &nodes[2 * n + 1].z, 4); return u; };
     auto ntri = [&](uint32_t n) { uint32_t u; std::memcpy(&u, &nodes[2 * n + 1].w, 4); return u; };
     // DFS leaf order and subtree triangle counts
     std::vector<uint32_t> st{root}, post;
@@ -1223,11 +1323,14 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
                     work.push_back({nd.left_node + 1, link + 1});
                     work.push_back({nd.left_node, link});
                 }
-                nodes[2 * dst] = f4(nd.min[0], nd.min[1], nd.min[2], bits(link));
-                nodes[2 * dst + 1] = f4(nd.max[0], nd.max[1], nd.max[2], bits(cnt));
+                // device layout: {min.xyz, max.x}, {max.yz, link, ntri} (slab_mask)
+                nodes[2 * dst] = f4(nd.min[0], nd.min[1], nd.min[2], nd.max[0]);
+                nodes[2 * dst + 1] = f4(nd.max[1], nd.max[2], bits(link), bits(cnt));
             }
         }
-        meshes.push_back(make_int4(static_cast<int>(root), static_cast<int>(m.n_nodes), m.cull_mode, m.material));
+        const float cs = m.cull_mode == RTX_CULL_FRONT ? -1.f : (m.cull_mode == RTX_CULL_BACK ? 1.f : 0.f);
+        // {root node byte offset, node count, cull sign bits, material}
+        meshes.push_back(make_int4(static_cast<int>(root * 32u), static_cast<int>(m.n_nodes), bitsi_f(cs), m.material));
         (void)node0;
         // ~48 triangles per part at least: finer parts of a small mesh cost more than they spread
         const uint32_t target = std::max(2u, std::min(c->split_parts, ntri / 48u));
@@ -1242,9 +1345,9 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
         return fail(c, RTX_E_INVALID, "scene too large for 32-bit record offsets");
     for (size_t n = 0; n < nodes.size(); n += 2) {
         uint32_t link, cnt;
-        std::memcpy(&link, &nodes[n].w, 4);
+        std::memcpy(&link, &nodes[n + 1].z, 4);
         std::memcpy(&cnt, &nodes[n + 1].w, 4);
-        nodes[n].w = bits(cnt ? link * 64u : link * 32u);
+        nodes[n + 1].z = bits(cnt ? link * 64u : link * 32u);
     }
     for (uint32_t i = 0; i < s->n_lights; ++i) {
         const rtx_light& l = s->lights[i];
