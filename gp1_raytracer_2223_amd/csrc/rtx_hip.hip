@@ -222,13 +222,14 @@ __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const flo
 #ifndef RTX_SLAB_FOLD
 #define RTX_SLAB_FOLD 1
 #endif
-// Node record (32 B): a = {min.x, min.y, min.z, max.x}, b = {max.y, max.z, link, ntri}:
-// link and triangle count are adjacent, one 64-bit SGPR pair the traversal selects whole.
+// Node record (32 B): a = {min.x, max.x, min.y, max.y}, b = {min.z, max.z, link, ntri};
+// link and triangle count are adjacent (one 64-bit SGPR pair).  (Packed f32 for the
+// (min, max) pairs was measured 15-35 % slower: profiles/r01/ablate_history.md.)
 template <bool FAST>
 __device__ __forceinline__ unsigned long long slab_mask(const float4 a, const float4 b, const Ray& r) {
-    const float tx1 = (a.x - r.ox) * r.ix, tx2 = (a.w - r.ox) * r.ix;
-    const float ty1 = (a.y - r.oy) * r.iy, ty2 = (b.x - r.oy) * r.iy;
-    const float tz1 = (a.z - r.oz) * r.iz, tz2 = (b.y - r.oz) * r.iz;
+    const float tx1 = (a.x - r.ox) * r.ix, tx2 = (a.y - r.ox) * r.ix;
+    const float ty1 = (a.z - r.oy) * r.iy, ty2 = (a.w - r.oy) * r.iy;
+    const float tz1 = (b.x - r.oz) * r.iz, tz2 = (b.y - r.oz) * r.iz;
     float tMin, tMax;
     if (FAST) {
         tMin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
@@ -1323,9 +1324,9 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
                     work.push_back({nd.left_node + 1, link + 1});
                     work.push_back({nd.left_node, link});
                 }
-                // device layout: {min.xyz, max.x}, {max.yz, link, ntri} (slab_mask)
-                nodes[2 * dst] = f4(nd.min[0], nd.min[1], nd.min[2], nd.max[0]);
-                nodes[2 * dst + 1] = f4(nd.max[1], nd.max[2], bits(link), bits(cnt));
+                // device layout: {min.x, max.x, min.y, max.y}, {min.z, max.z, link, ntri} (slab_mask)
+                nodes[2 * dst] = f4(nd.min[0], nd.max[0], nd.min[1], nd.max[1]);
+                nodes[2 * dst + 1] = f4(nd.min[2], nd.max[2], bits(link), bits(cnt));
             }
         }
         const float cs = m.cull_mode == RTX_CULL_FRONT ? -1.f : (m.cull_mode == RTX_CULL_BACK ? 1.f : 0.f);
