@@ -20,7 +20,7 @@ typedef struct rtx_host_scene rtx_host_scene;
  * W4_Optional, Synthetic100k, Bunny8Lights) — Scene_*::Initialize() — or, for a name
  * "file:<path>", the scene described by a scene file (text, one directive per line:
  * camera / material / sphere / plane / mesh / light; grammar in csrc/host/scene.cpp and
- * DESIGN.md, examples in scenes/*.rtxscene).  Mesh assets are looked up in `asset_dir`
+ * DESIGN.md, examples in scenes/ as *.rtxscene). Mesh assets are looked up in `asset_dir`
  * as <stem>.rtxmesh, then <stem>.obj.  On failure returns an error code and, if
  * err/err_len are given, the reason (for scene files with the line number). */
 int rtx_host_scene_create(const char* name, const char* asset_dir, rtx_host_scene** out, char* err,

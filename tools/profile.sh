@@ -16,7 +16,8 @@ PMCLIST=${PMC_GROUPS:-"FETCH_SIZE|WRITE_SIZE|SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SAL
 IFS='|' read -ra GRPS <<< "$PMCLIST"
 for grp in "${GRPS[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py --steps ${PMC_STEPS:-20} --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i ($grp) failed"; tail -5 $OUT/pmc$i.log; }
+  # one counter group per pass, hard-killed if the profiler stalls; stop at the first failure
+  timeout -s KILL 90 rocprofv3 --pmc $grp -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py --steps ${PMC_STEPS:-20} --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i ($grp) failed: stopping"; tail -5 $OUT/pmc$i.log; exit 1; }
 done
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 find $OUT -name "*.csv" | head -50
