@@ -57,12 +57,16 @@ def build_hip(force: bool = False) -> Path:
     LIB.mkdir(exist_ok=True)
     out = LIB / "librtx_hip.so"
     srcs = [CSRC / "rtx_hip.hip"]
-    deps = srcs + list(CSRC.glob("*.h")) + [INC / "rtx.h"]
+    deps = srcs + list(CSRC.glob("*.h")) + [INC / "rtx.h", Path(__file__)]   # flags live here
     if force or _stale(out, deps):
         # -fno-slp-vectorize: the SLP packer turns independent f32 ops into v_pk_* plus
         # v_mov shuffles; measured 8 % slower on the render kernel (profiles/r01/ablate_*.txt).
+        # -structurizecfg-skip-uniform-regions: wave-uniform loops and branches (every loop of
+        # the BVH walk) stay plain s_cbranch_scc instead of being structurized into SGPR
+        # lane-mask phis (s_cselect -1/0 + s_and vcc, exec per exit): -6 % SALU per wave.
         _run([HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-O3", "-ffp-contract=off",
               "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize",
+              "-mllvm", "-structurizecfg-skip-uniform-regions=true",
               "-DRTX_MIN_WAVES_PER_EU=6", "-fPIC", "-shared",
               "-Wall", f"-I{INC}", f"-I{CSRC}", *srcs, "-o", out])
     return out

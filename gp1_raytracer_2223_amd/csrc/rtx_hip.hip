@@ -225,13 +225,34 @@ __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const flo
 // Node record (32 B): a = {min.x, max.x, min.y, max.y}, b = {min.z, max.z, link, ntri};
 // link and triangle count are adjacent (one 64-bit SGPR pair).  (Packed f32 for the
 // (min, max) pairs was measured 15-35 % slower: profiles/r01/ablate_history.md.)
-template <bool FAST>
+// SLAB selects the formulation (all three give the reference's pass/fail bit):
+//   kSlabExact  std::min/std::max restated (NaN-safe), any direction;
+//   kSlabFast   v_min/v_max_f32, which differ from std::min/std::max only when an operand
+//               is NaN; a NaN slab value needs (box - origin) * inv with an infinite inv
+//               component, so it is taken only when every live lane's inverse direction is
+//               finite (decided once per ray batch with a ballot);
+//   kSlabOct    kSlabFast for a ray batch whose inverse directions have ONE sign per axis
+//               (an octant), against the node copy mirrored for that octant (see
+//               octant_ray): the near and far planes are known, so min/max of each pair
+//               disappears (below).
+// Returned as a wave lane mask: one v_cmp per condition straight into SGPRs (a ballot
+// of the && would materialise the bool in a VGPR and compare it again).
+enum { kSlabExact = 0, kSlabFast = 1, kSlabOct = 2 };
+template <int SLAB>
 __device__ __forceinline__ unsigned long long slab_mask(const float4 a, const float4 b, const Ray& r) {
     const float tx1 = (a.x - r.ox) * r.ix, tx2 = (a.y - r.ox) * r.ix;
     const float ty1 = (a.z - r.oy) * r.iy, ty2 = (a.w - r.oy) * r.iy;
     const float tz1 = (b.x - r.oz) * r.iz, tz2 = (b.y - r.oz) * r.iz;
     float tMin, tMax;
-    if (FAST) {
+    if (SLAB == kSlabOct) {
+        // Octant copy: per axis the record holds (near, far) with near <= far in the
+        // mirrored frame, r.o is the mirrored origin and r.i = |inv| > 0, so rounding
+        // monotonicity gives t_near <= t_far per axis (the pair's min and max), and each
+        // value equals the reference's up to the sign of a zero (negation is exact).
+        tMin = fmaxf(fmaxf(fmaxf(tx1, ty1), tz1), 0x1p-149f);
+        tMax = fminf(fminf(tx2, ty2), tz2);
+        return ballot(tMax >= tMin);
+    } else if (SLAB == kSlabFast) {
         tMin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
         tMax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
         // no NaN here: tMax > 0 && tMax >= tMin  <=>  tMax >= max(tMin, smallest denormal)
@@ -246,6 +267,29 @@ __device__ __forceinline__ unsigned long long slab_mask(const float4 a, const fl
         tMax = smin(tMax, smax(tz1, tz2));
     }
     return ballot(tMax > 0) & ballot(tMax >= tMin);
+}
+
+// Octant of a FAST ray batch (every live inverse direction finite and non-zero): bit k set
+// when axis k's inverse direction is negative for every lane in `mask` (non-empty), -1
+// when the lanes disagree on some axis.  One code per lane from the sign bits, compared
+// against the first masked lane's: a few VALU and one compare, no per-axis scalar logic.
+__device__ __forceinline__ int batch_octant(const Ray& r, unsigned long long mask) {
+    const uint32_t code = (__float_as_uint(r.ix) >> 31) | ((__float_as_uint(r.iy) >> 31) << 1) |
+                          ((__float_as_uint(r.iz) >> 31) << 2);
+    const uint32_t first = static_cast<uint32_t>(__builtin_ctzll(mask));
+    const uint32_t c0 = __builtin_amdgcn_readlane(code, first);
+    return (ballot(code == c0) & mask) == mask ? static_cast<int>(c0) : -1;
+}
+// The slab view of a ray in octant `oct`'s mirrored frame: a mirrored axis negates the
+// origin (the node copy stores (-hi, -lo) there), every inverse direction becomes |inv|.
+// (-hi - (-o)) * |inv| == (hi - o) * inv exactly: negation commutes with RN.
+__device__ __forceinline__ Ray octant_ray(const Ray& r, int oct) {
+    Ray q = r;
+    q.ox = (oct & 1) ? -r.ox : r.ox;
+    q.oy = (oct & 2) ? -r.oy : r.oy;
+    q.oz = (oct & 4) ? -r.oz : r.oz;
+    q.ix = fabsf(r.ix); q.iy = fabsf(r.iy); q.iz = fabsf(r.iz);
+    return q;
 }
 
 // FAST-path condition for one ray: every inverse direction component finite AND non-zero
@@ -329,8 +373,8 @@ __device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t lin
             if (RTX_STAMPS && !COUNT && lane == 0) cnt.c[kSlab] += 2 * __popcll(m);
             NodePair P;
             ldcb64(S.nodes, link, P.l0, P.l1, P.r0, P.r1);
-            const unsigned long long ml = slab_mask<FAST>(P.l0, P.l1, r) & m;
-            const unsigned long long mr = slab_mask<FAST>(P.r0, P.r1, r) & m;
+            const unsigned long long ml = slab_mask<FAST ? kSlabFast : kSlabExact>(P.l0, P.l1, r) & m;
+            const unsigned long long mr = slab_mask<FAST ? kSlabFast : kSlabExact>(P.r0, P.r1, r) & m;
             const bool in = COUNT && ((m >> lane) & 1ull);
             if (COUNT && in) cnt.c[kSlab]++;               // left child's test
             if (COUNT && !ANY && in) cnt.c[kSlab]++;       // right child's (closest: always reached)
@@ -386,21 +430,53 @@ __device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t lin
 #ifndef RTX_LEAN_WALK
 #define RTX_LEAN_WALK 1
 #endif
+#ifndef RTX_ASM_SELECT
+#define RTX_ASM_SELECT 1
+#endif
+#ifndef RTX_OCTANT
+#define RTX_OCTANT 1
+#endif
 // bvh_walk without counters, shaped for the scalar unit: one inner loop descends through
 // inner nodes with scalar selects (no i1 value crosses a block, so nothing is carried as a
 // VGPR boolean or a lane-mask flow variable), a dead end leaves it as an empty "leaf", and
 // the pop loop is the only other path.  Same visits, tests and order as bvh_walk.
-template <bool ANY, bool FAST>
-__device__ void bvh_walk_lean(const DevScene& S, float cs, const Ray& r, uint32_t link, uint32_t ntri,
-                              unsigned long long m, unsigned long long mask, uint32_t lane, uint4* stk, float& sc_t,
-                              uint32_t& sc_tri, unsigned long long& live, const uint32_t* occ_word, uint32_t occ_bit) {
+// `nb` is the node copy the slab form reads (the octant's mirrored copy for kSlabOct) and
+// `q` the ray as the slab test sees it (octant_ray), `r` the ray of the triangle tests.
+template <bool ANY, int SLAB>
+__device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, const Ray& r, const Ray& q, uint32_t link,
+                              uint32_t ntri, unsigned long long m, unsigned long long mask, uint32_t lane, uint4* stk,
+                              float& sc_t, uint32_t& sc_tri, unsigned long long& live, const uint32_t* occ_word,
+                              uint32_t occ_bit) {
+    constexpr bool FAST = SLAB != kSlabExact;
     uint32_t sp = 0;
     for (;;) {
         while (ntri == 0) {
             NodePair P;
-            ldcb64(S.nodes, link, P.l0, P.l1, P.r0, P.r1);
-            const unsigned long long ml = slab_mask<FAST>(P.l0, P.l1, r) & m;
-            const unsigned long long mr = slab_mask<FAST>(P.r0, P.r1, r) & m;
+            ldcb64(nb, link, P.l0, P.l1, P.r0, P.r1);
+            const unsigned long long ml = slab_mask<SLAB>(P.l0, P.l1, q) & m;
+            const unsigned long long mr = slab_mask<SLAB>(P.r0, P.r1, q) & m;
+#if RTX_ASM_SELECT
+            // next (link, ntri): left, else right, else a dead end taken as an empty leaf
+            // (ntri = 1 with m = 0); `both` = mr if the left child is taken too (the right
+            // one then waits on the stack).  Written as 64-bit s_cselects on one SCC each:
+            // the compiler materialises every `x != 0` as a -1/0 SGPR pair and ANDs them.
+            unsigned long long nx, both;
+            asm("s_cmp_lg_u64 %[mr], 0\n\t"
+                "s_cselect_b64 %[nx], %[lr], %[dead]\n\t"
+                "s_cmp_lg_u64 %[ml], 0\n\t"
+                "s_cselect_b64 %[nx], %[ll], %[nx]\n\t"
+                "s_cselect_b64 %[both], %[mr], 0\n\t"
+                "s_cselect_b64 %[m], %[ml], %[mr]"
+                : [nx] "=&s"(nx), [both] "=&s"(both), [m] "=&s"(m)
+                : [mr] "s"(mr), [ml] "s"(ml), [lr] "s"(link_ntri(P.r1)), [ll] "s"(link_ntri(P.l1)),
+                  [dead] "s"(1ull << 32)
+                : "scc");
+            if (both) {
+                stk[sp] = make_uint4(__float_as_uint(P.r1.z), __float_as_uint(P.r1.w), static_cast<uint32_t>(mr),
+                                     static_cast<uint32_t>(mr >> 32));
+                ++sp;
+            }
+#else
             if (ml != 0 && mr != 0) {   // both: descend left, the right child waits on the stack
                 stk[sp] = make_uint4(__float_as_uint(P.r1.z), __float_as_uint(P.r1.w), static_cast<uint32_t>(mr),
                                      static_cast<uint32_t>(mr >> 32));
@@ -411,8 +487,10 @@ __device__ void bvh_walk_lean(const DevScene& S, float cs, const Ray& r, uint32_
             unsigned long long nx = mr ? link_ntri(P.r1) : (1ull << 32);
             nx = ml ? link_ntri(P.l1) : nx;
             m = ml ? ml : mr;
+#endif
             link = static_cast<uint32_t>(nx);
-            ntri = static_cast<uint32_t>(nx >> 32);
+            // opaque: a 32-bit s_cmp for the loop test (else it becomes a 64-bit v_cmp on nx)
+            ntri = RTX_ASM_SELECT ? opaque(static_cast<uint32_t>(nx >> 32)) : static_cast<uint32_t>(nx >> 32);
         }
         if (m) {
             const bool in = (m >> lane) & 1ull;
@@ -449,20 +527,29 @@ __device__ void bvh_walk_lean(const DevScene& S, float cs, const Ray& r, uint32_
     }
 }
 
-template <bool ANY, bool FAST, bool COUNT>
-__device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, unsigned long long mask, uint32_t lane,
-                              uint4* stk, unsigned long long* sT, float& sc_t, uint32_t& sc_tri,
+// SLAB = kSlabOct: `oct` is the batch's octant (batch_octant), else ignored.
+template <bool ANY, int SLAB, bool COUNT>
+__device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int oct, unsigned long long mask,
+                              uint32_t lane, uint4* stk, unsigned long long* sT, float& sc_t, uint32_t& sc_tri,
                               unsigned long long& live, Counts& cnt) {
+    constexpr bool FAST = SLAB != kSlabExact;
     if (M.y == 0) return;
+    const bool OCT = SLAB == kSlabOct && !COUNT && !RTX_STAMPS;
+    const float4* nb = OCT ? reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.nodes) +
+                                                             static_cast<uint32_t>(oct) * S.oct_bytes)
+                           : S.nodes;
+    const Ray q = OCT ? octant_ray(r, oct) : r;
     // root (odd global index; every child pair starts at an even one, 64-B aligned)
     float4 b0, b1;
-    ldcb32(S.nodes, static_cast<uint32_t>(M.x), b0, b1);   // M.x: the root's byte offset
+    ldcb32(nb, static_cast<uint32_t>(M.x), b0, b1);   // M.x: the root's byte offset
     if (COUNT && ((mask >> lane) & 1ull)) cnt.c[kSlab]++;
-    const unsigned long long m = slab_mask<FAST>(b0, b1, r) & mask;
+    const unsigned long long m =
+        (OCT ? slab_mask<kSlabOct>(b0, b1, q) : slab_mask<FAST ? kSlabFast : kSlabExact>(b0, b1, r)) & mask;
     if (m == 0) return;
     if (RTX_LEAN_WALK && !COUNT && !RTX_STAMPS)
-        bvh_walk_lean<ANY, FAST>(S, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask, lane,
-                                 stk, sc_t, sc_tri, live, nullptr, 0u);
+        bvh_walk_lean<ANY, OCT ? kSlabOct : (FAST ? kSlabFast : kSlabExact)>(
+            S, nb, cull_sign(M.z, ANY), r, q, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask, lane, stk, sc_t,
+            sc_tri, live, nullptr, 0u);
     else
         bvh_walk<ANY, FAST, COUNT>(S, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask,
                                    lane, stk, sT, sc_t, sc_tri, live, cnt);
@@ -481,7 +568,7 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, uns
     const int4 M = ldcb16i(S.meshes, static_cast<uint32_t>(E.x) * 16u);
     float4 b0, b1;
     ldcb32(S.nodes, static_cast<uint32_t>(M.x), b0, b1);   // M.x: the root's byte offset
-    unsigned long long m = slab_mask<FAST>(b0, b1, r) & mask;
+    unsigned long long m = slab_mask<FAST ? kSlabFast : kSlabExact>(b0, b1, r) & mask;
     uint32_t link = __float_as_uint(b1.z), ntri = __float_as_uint(b1.w);
     const uint32_t path = static_cast<uint32_t>(E.z);
     for (int d = 0; d < E.w && m; ++d) {
@@ -489,14 +576,14 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, uns
         ldcb64(S.nodes, link, P.l0, P.l1, P.r0, P.r1);
         const bool right = (path >> d) & 1u;
         const float4 c0 = right ? P.r0 : P.l0, c1 = right ? P.r1 : P.l1;
-        m &= slab_mask<FAST>(c0, c1, r);
+        m &= slab_mask<FAST ? kSlabFast : kSlabExact>(c0, c1, r);
         link = __float_as_uint(c1.z);
         ntri = __float_as_uint(c1.w);
     }
     if (m == 0) return;
     if (RTX_LEAN_WALK && !RTX_STAMPS)
-        bvh_walk_lean<ANY, FAST>(S, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, sc_t, sc_tri, live,
-                                 occ_word, occ_bit);
+        bvh_walk_lean<ANY, FAST ? kSlabFast : kSlabExact>(S, S.nodes, cull_sign(M.z, ANY), r, r, link, ntri, m, mask,
+                                                          lane, stk, sc_t, sc_tri, live, occ_word, occ_bit);
     else
         bvh_walk<ANY, FAST, false>(S, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, nullptr, sc_t, sc_tri,
                                    live, cnt, occ_word, occ_bit);
@@ -663,6 +750,8 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     const Ray vr = make_ray(V.origin[0], V.origin[1], V.origin[2], dx, dy, dz, 0.0001f, FLT_MAX);
     const unsigned long long active = ballot(valid);
     const bool fast = (active & ~finite_inv_mask(vr)) == 0 && S.tri_fast;
+    // octant of the wave's primary rays (-1: mixed signs, or no octant copies)
+    const int poct = (RTX_OCTANT && fast && S.oct_bytes && PHASE == 0) ? batch_octant(vr, active) : -1;
 
     // ---- Scene::GetClosestHit (Scene.cpp:29-66)
     float best_t = FLT_MAX, sc_t = FLT_MAX;
@@ -701,10 +790,12 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
             const int4 M = ldcb16i(S.meshes, opaque(mi * 16u));
             uint32_t sc_tri = 0;
             unsigned long long unused = 0;
-            if (fast)
-                mesh_traverse<false, true, COUNT>(S, M, vr, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
+            if (poct >= 0)
+                mesh_traverse<false, kSlabOct, COUNT>(S, M, vr, poct, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
+            else if (fast)
+                mesh_traverse<false, kSlabFast, COUNT>(S, M, vr, 0, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
             else
-                mesh_traverse<false, false, COUNT>(S, M, vr, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
+                mesh_traverse<false, kSlabExact, COUNT>(S, M, vr, 0, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
             if (sc_t < best_t) { best_t = sc_t; best_kind = 3; best_idx = sc_tri; }
         }
     } else if (PHASE == 1) {
@@ -778,6 +869,8 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                 const Ray sr = make_ray(oox, ooy, ooz, lx, ly, lz, 0.0001f, mag);
                 unsigned long long live = hitmask;
                 const bool sfast = (hitmask & ~finite_inv_mask(sr)) == 0 && S.tri_fast;
+                const int soct =
+                    (RTX_OCTANT && sfast && S.oct_bytes && PHASE == 0 && S.n_meshes) ? batch_octant(sr, hitmask) : -1;
                 if (COUNT && did) cnt.c[kShadow]++;
                 // (single-condition loops with a separate exit test: a `&& live` loop
                 // condition is carried as a VGPR boolean by the compiler)
@@ -805,11 +898,13 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                     if (!live) break;
                     float st = 0.f;
                     uint32_t stri = 0;
-                    if (sfast)
-                        mesh_traverse<true, true, COUNT>(S, ldcb16i(S.meshes, opaque(mi * 16u)), sr, live, lane, stk, sT, st, stri, live, cnt);
+                    const int4 M = ldcb16i(S.meshes, opaque(mi * 16u));
+                    if (soct >= 0)
+                        mesh_traverse<true, kSlabOct, COUNT>(S, M, sr, soct, live, lane, stk, sT, st, stri, live, cnt);
+                    else if (sfast)
+                        mesh_traverse<true, kSlabFast, COUNT>(S, M, sr, 0, live, lane, stk, sT, st, stri, live, cnt);
                     else
-                        mesh_traverse<true, false, COUNT>(S, ldcb16i(S.meshes, opaque(mi * 16u)), sr, live, lane, stk, sT, st, stri, live,
-                                                          cnt);
+                        mesh_traverse<true, kSlabExact, COUNT>(S, M, sr, 0, live, lane, stk, sT, st, stri, live, cnt);
                 }
                 if (PHASE == 2) {
                     const int4 E = ldc(S.parts, part);
@@ -1350,6 +1445,28 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
         std::memcpy(&cnt, &nodes[n + 1].w, 4);
         nodes[n + 1].z = bits(cnt ? link * 64u : link * 32u);
     }
+    // Octant copies of the node array (DevScene::oct_bytes, slab_mask<kSlabOct>): possible
+    // when every box is ordered lo <= hi per axis (no NaN).  The reference's quirky bounds
+    // (max initialised with FLT_MIN) stay ordered; an empty box would not.
+    const size_t node_bytes = align256(nodes.size() * 16);
+    bool oct_ok = !nodes.empty() && 8 * node_bytes < (1ull << 32);
+    for (size_t n = 0; oct_ok && n < nodes.size(); n += 2)
+        oct_ok = nodes[n].x <= nodes[n].y && nodes[n].z <= nodes[n].w && nodes[n + 1].x <= nodes[n + 1].y;
+    std::vector<float4> node_img;
+    if (oct_ok) {
+        node_img.assign(8 * node_bytes / 16, f4(0, 0, 0, 0));
+        for (int k = 0; k < 8; ++k) {
+            float4* dst = node_img.data() + k * (node_bytes / 16);
+            const bool mx = k & 1, my = k & 2, mz = k & 4;
+            for (size_t n = 0; n < nodes.size(); n += 2) {
+                const float4 a = nodes[n], b = nodes[n + 1];
+                dst[n] = f4(mx ? -a.y : a.x, mx ? -a.x : a.y, my ? -a.w : a.z, my ? -a.z : a.w);
+                dst[n + 1] = f4(mz ? -b.y : b.x, mz ? -b.x : b.y, b.z, b.w);
+            }
+        }
+    } else {
+        node_img = nodes;
+    }
     for (uint32_t i = 0; i < s->n_lights; ++i) {
         const rtx_light& l = s->lights[i];
         lights.push_back(f4(l.origin[0], l.origin[1], l.origin[2], bitsi(l.type)));
@@ -1367,7 +1484,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     struct Sec { const void* p; size_t n; size_t off; };
     Sec secs[] = {{sph.data(), sph.size() * 16, 0},       {sph_mat.data(), sph_mat.size() * 4, 0},
                   {pl.data(), pl.size() * 16, 0},         {tri.data(), tri.size() * 16, 0},
-                  {nodes.data(), nodes.size() * 16, 0},
+                  {node_img.data(), node_img.size() * 16, 0},
                   {meshes.data(), meshes.size() * 16, 0}, {lights.data(), lights.size() * 16, 0},
                   {mats.data(), mats.size() * 16, 0},     {parts.data(), parts.size() * 16, 0}};
     size_t total = 0;
@@ -1415,6 +1532,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     d.n_spheres = s->n_spheres; d.n_planes = s->n_planes; d.n_meshes = s->n_meshes;
     d.n_lights = s->n_lights; d.n_materials = nm;
     d.tri_fast = max_ee <= 0x1p56 ? 1u : 0u;
+    d.oct_bytes = (RTX_OCTANT && oct_ok && !std::getenv("RTX_NO_OCTANT")) ? static_cast<uint32_t>(node_bytes) : 0u;
     d.n_tris = static_cast<uint32_t>(tri.size() / 4); d.n_nodes = static_cast<uint32_t>(nodes.size() / 2);
     c->dev = d;
     c->split_ok = split_ok && !parts.empty();

@@ -191,3 +191,26 @@ def test_scene_file_parity(gpu_ctx, path, t, mode, shadows):
     gpx, grgb = gpu_ctx.render(cam, p)
     rpx, rrgb = oracle_bind.render(s, cam, p)
     _compare(f"{path.stem}/m{mode}s{shadows}", gpx, grgb, rpx, rrgb, exact=mode in (0, 1) or path.stem == "w4_bunny")
+
+
+@pytest.mark.parametrize("name", ["W4_Bunny", "W4_Reference", "W4_Optional", "Bunny8Lights", "Synthetic100k"])
+@pytest.mark.parametrize("shadows", [0, 1])
+def test_octant_slab_path_bit_identical(gpu_ctx, name, shadows, monkeypatch):
+    """Wave batches with one direction octant test the mirrored node copy (slab_mask<kSlabOct>):
+    the frame must equal the one rendered with the general slab form only (RTX_NO_OCTANT
+    uploads no octant copies), bit for bit, and the oracle's."""
+    hs = HostScene(name)
+    if name.startswith("W4"):
+        hs.update(1.3)
+    s, cam = hs.view()
+    p = abi.make_params(320, 180, 3, shadows)
+    gpu_ctx.upload(s)
+    opx, orgb = gpu_ctx.render(cam, p)
+    monkeypatch.setenv("RTX_NO_OCTANT", "1")
+    gpu_ctx.upload(s)
+    gpx, grgb = gpu_ctx.render(cam, p)
+    monkeypatch.delenv("RTX_NO_OCTANT")
+    gpu_ctx.upload(s)
+    assert np.array_equal(opx, gpx) and np.array_equal(orgb.view(np.uint32), grgb.view(np.uint32))
+    rpx, rrgb = oracle_bind.render(s, cam, p)
+    _compare(name, opx, orgb, rpx, rrgb, exact=name in POW_FREE)

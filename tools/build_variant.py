@@ -20,6 +20,7 @@ def main() -> int:
     flags = {"-DRTX_MIN_WAVES_PER_EU=6"}
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-O3", "-ffp-contract=off",
            "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize",
+           "-mllvm", "-structurizecfg-skip-uniform-regions=true",
            *([f for f in flags if not any(a.startswith(f.split("=")[0]) for a in args)]), "-fPIC", "-shared",
            "-Wall", f"-I{ROOT / 'include'}", f"-I{PKG / 'csrc'}", *args, str(src), "-o", str(out)]
     print(" ".join(cmd[-4:]), flush=True)
