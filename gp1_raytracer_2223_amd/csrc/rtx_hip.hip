@@ -692,22 +692,22 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     uint4* stk = stkE[wave];
     unsigned long long* sT = stkT[COUNT ? wave : 0];
 
-    // Work unit = one 8x8 wave tile of one view; the 4 waves of a workgroup are independent
-    // (no barrier) and take 4 consecutive entries of the dispatch order.  The order is a
-    // permutation (F.order, null = identity) that rtx_reorder_kernel derives from the
-    // previous frame's measured per-tile cost: heavy tiles start first and do not form a
-    // tail, and the 4 waves of a workgroup have similar cost, so a finished wave seldom
-    // waits for its siblings to release the workgroup's slot.  Which wave renders a tile
-    // never changes a pixel's value.
+    // Work unit = one 8x8 wave tile of one view; the waves of a workgroup (one by default,
+    // RTX_BLOCK_THREADS) are independent (no barrier) and take consecutive entries of the
+    // dispatch order.  The order is a permutation (F.order, null = identity) that
+    // rtx_reorder_kernel derives from the previous frame's measured per-tile cost: heavy
+    // tiles start first and do not form a tail.  One-wave workgroups free their slot the
+    // moment the wave ends (4-wave ones held it until the slowest sibling ended: Bunny
+    // -3 %, Synthetic100k -9 %).  Which wave renders a tile never changes a pixel's value.
     const uint32_t b = blockIdx.x;
-    const uint32_t widx = b * (kBlockThreads / 64) + wave;   // wave index in the launch
+    const uint32_t widx = b * kWavesPerBlock + wave;   // wave index in the launch
     uint32_t tile, part = 0, light = 0;
     if (PHASE == 0) {
         if (widx >= F.n_tiles) return;
         tile = F.order ? ldc(F.order, widx) : widx;
         if (F.heavy_flag && ldc(F.heavy_flag, tile)) return;   // rendered by the split launches
     } else {
-        // grid (heavy tiles / 4, parts, lights), tile fastest: every heavy tile's part 0 is
+        // grid (heavy tiles / waves per block, parts, lights), tile fastest: every heavy tile's part 0 is
         // dispatched first, the big top-of-tree parts before the small ones.  (Pinning a
         // part to one XCD for L2 locality was measured slower: the heavy parts then load a
         // few XCDs only.)
@@ -1606,7 +1606,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     F.counters = c->d_counters;
     const uint32_t ntiles = F.tiles_x * gy * static_cast<uint32_t>(n_views);
     F.n_tiles = ntiles;
-    grid = dim3((ntiles + 3) / 4, 1, 1);
+    grid = dim3((ntiles + kWavesPerBlock - 1) / kWavesPerBlock, 1, 1);
     // Cost-ordered dispatch (see the kernel): keep one order/cost pair per launch shape.
     if (ntiles > c->sched_cap) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1674,7 +1674,7 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         // The heavy tiles, one BVH frontier part per workgroup (see the kernel), on a
         // high-priority stream forked from the frame stream: they share no pixels with the
         // main kernel, so the two run side by side and the join closes the frame.
-        const uint32_t nh = (c->heavy_n + 3) / 4, np = c->dev.n_parts;   // 4 heavy wave tiles per workgroup
+        const uint32_t nh = (c->heavy_n + kWavesPerBlock - 1) / kWavesPerBlock, np = c->dev.n_parts;   // heavy wave tiles per workgroup
         hipStream_t s2 = c->split_stream;
         HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fork, 0));

@@ -8,7 +8,11 @@ namespace rtxd {
 // Per-wave DFS stack entries in LDS (node index + 64-bit lane mask).  The host checks
 // every uploaded BVH's depth against this before accepting the scene.
 constexpr int kStackDepth = 64;
-constexpr int kBlockThreads = 256;     // 4 independent waves, each an 8 x 8 pixel "wave tile"
+#ifndef RTX_BLOCK_THREADS
+#define RTX_BLOCK_THREADS 64
+#endif
+constexpr int kBlockThreads = RTX_BLOCK_THREADS;   // independent waves, each an 8 x 8 pixel "wave tile"
+constexpr int kWavesPerBlock = kBlockThreads / 64;
 constexpr int kWaveTile = 8;
 constexpr int kReorderThreads = 256;
 constexpr int kCostBuckets = 32;

@@ -8,7 +8,7 @@ rc=$?
 echo "pytest exit $rc"
 tail -25 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "abnormal pytest exit $rc: stopping"; exit $rc; fi
-timeout -k 10 400 python bench.py --steps 100 --warmup 10 > gpurun_out/bench.json 2> gpurun_out/bench.err
+timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?
 echo "bench exit $rc"
 cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err

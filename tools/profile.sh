@@ -7,7 +7,7 @@ cd "$PWD" && export TMPDIR=/tmp
 TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BENCH="python3 bench.py --steps ${TRACE_STEPS:-100} --warmup 10 --no-cpu-baseline ${BENCH_ARGS:-}"
+BENCH="python3 bench.py --steps ${TRACE_STEPS:-100} --warmup 10 --no-cpu-baseline --inflight 1 ${BENCH_ARGS:-}"
 set -o pipefail
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $BENCH > $OUT/trace.log 2>&1 || { echo "trace pass failed"; tail -20 $OUT/trace.log; exit 1; }
 echo "trace ok"
@@ -17,7 +17,7 @@ IFS='|' read -ra GRPS <<< "$PMCLIST"
 for grp in "${GRPS[@]}"; do
   i=$((i+1))
   # one counter group per pass, hard-killed if the profiler stalls; stop at the first failure
-  timeout -s KILL 90 rocprofv3 --pmc $grp -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py --steps ${PMC_STEPS:-20} --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i ($grp) failed: stopping"; tail -5 $OUT/pmc$i.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $grp -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py --steps ${PMC_STEPS:-20} --warmup 2 --no-cpu-baseline --inflight 1 ${BENCH_ARGS:-} > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i ($grp) failed: stopping"; tail -5 $OUT/pmc$i.log; exit 1; }
 done
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 find $OUT -name "*.csv" | head -50
