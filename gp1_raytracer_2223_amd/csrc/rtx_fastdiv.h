@@ -51,16 +51,21 @@ __device__ __forceinline__ float rcp_exact(float b) {
     return y;
 }
 
-// RN(1/x), RN(1/y), RN(1/z) with ONE domain test for the three (v_min3/v_max3 of the
-// magnitudes): the IEEE fallback runs only in lanes where some component is outside.
-__device__ __forceinline__ void rcp3_exact(float x, float y, float z, float& rx, float& ry, float& rz) {
+// RN(1/x), RN(1/y), RN(1/z) with ONE domain test for the three: the IEEE fallback runs
+// only in lanes where some component is outside.  Returns the ballot of those lanes.  In
+// the domain every reciprocal is finite and non-zero, which is what the FAST slab path
+// needs, so the ballot doubles as its (conservative) exclusion mask.  The magnitude sum
+// carries a NaN or inf component into the test (v_min3 would drop a NaN).
+__device__ __forceinline__ unsigned long long rcp3_exact(float x, float y, float z, float& rx, float& ry, float& rz) {
     rx = rcp_rn(x); ry = rcp_rn(y); rz = rcp_rn(z);
     const float lo = fminf(fminf(fabsf(x), fabsf(y)), fabsf(z));
-    const float hi = fmaxf(fmaxf(fabsf(x), fabsf(y)), fabsf(z));
-    // a NaN component (dropped by v_min/v_max) gives NaN on both paths
-    if (__builtin_expect(!(lo >= 0x1p-60f && hi <= 0x1p60f), 0)) {
+    const float sum = (fabsf(x) + fabsf(y)) + fabsf(z);
+    const bool in = lo >= 0x1p-60f && sum <= 0x1p60f;
+    const unsigned long long out = __builtin_amdgcn_ballot_w64(!in);
+    if (__builtin_expect(!in, 0)) {
         rx = 1.f / x; ry = 1.f / y; rz = 1.f / z;
     }
+    return out;
 }
 
 // (x, y, z) / m, each correctly rounded, for m = |(x, y, z)| as computed by the caller.

@@ -123,12 +123,14 @@ struct Ray {
     float ox, oy, oz, dx, dy, dz, ix, iy, iz, tmin, tmax;
 };
 
-// dae::Ray constructor (DataTypes.h:549-564): inversedDir = 1 / dir
+// dae::Ray constructor (DataTypes.h:549-564): inversedDir = 1 / dir.  `slow` = lanes whose
+// direction is outside the fast reciprocal domain (rcp3_exact); every other lane has a
+// finite, non-zero inverse direction — the FAST slab condition.
 __device__ __forceinline__ Ray make_ray(float ox, float oy, float oz, float dx, float dy, float dz, float tmin,
-                                        float tmax) {
+                                        float tmax, unsigned long long& slow) {
     Ray r;
     r.ox = ox; r.oy = oy; r.oz = oz; r.dx = dx; r.dy = dy; r.dz = dz;
-    rcp3_exact(dx, dy, dz, r.ix, r.iy, r.iz);
+    slow = rcp3_exact(dx, dy, dz, r.ix, r.iy, r.iz);
     r.tmin = tmin; r.tmax = tmax;
     return r;
 }
@@ -290,16 +292,6 @@ __device__ __forceinline__ Ray octant_ray(const Ray& r, int oct) {
     q.oz = (oct & 4) ? -r.oz : r.oz;
     q.ix = fabsf(r.ix); q.iy = fabsf(r.iy); q.iz = fabsf(r.iz);
     return q;
-}
-
-// FAST-path condition for one ray: every inverse direction component finite AND non-zero
-// (so the direction itself is finite too).  v_cmp_class: +-normal, +-denormal.
-// As a lane mask: one ballot per v_cmp_class (a ballot of the combined bool would be
-// materialised in a VGPR and compared again).
-__device__ __forceinline__ unsigned long long finite_inv_mask(const Ray& r) {
-    constexpr int kFiniteNonZero = 0x198;
-    return ballot(__builtin_amdgcn_classf(r.ix, kFiniteNonZero)) & ballot(__builtin_amdgcn_classf(r.iy, kFiniteNonZero)) &
-           ballot(__builtin_amdgcn_classf(r.iz, kFiniteNonZero));
 }
 
 // The mesh record carries its cull sign as float bits (set at upload: -1 FrontFaceCulling,
@@ -747,9 +739,11 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     float dz = V.right[2] * cx + V.up[2] * cy + V.forward[2] * 1.f;
     const float dm = sqrtf(dx * dx + dy * dy + dz * dz);
     div3_exact(dx, dy, dz, dm);   // dx /= dm; ... (Vector3::Normalize)
-    const Ray vr = make_ray(V.origin[0], V.origin[1], V.origin[2], dx, dy, dz, 0.0001f, FLT_MAX);
+    unsigned long long vslow;
+    const Ray vr = make_ray(V.origin[0], V.origin[1], V.origin[2], dx, dy, dz, 0.0001f, FLT_MAX, vslow);
     const unsigned long long active = ballot(valid);
-    const bool fast = (active & ~finite_inv_mask(vr)) == 0 && S.tri_fast;
+    // FAST: every active lane's inverse direction finite and non-zero (make_ray's domain)
+    const bool fast = (active & vslow) == 0 && S.tri_fast;
     // octant of the wave's primary rays (-1: mixed signs, or no octant copies)
     const int poct = (RTX_OCTANT && fast && S.oct_bytes && PHASE == 0) ? batch_octant(vr, active) : -1;
 
@@ -866,9 +860,10 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
             if (F.shadows) {
                 // Scene::DoesHit (Scene.cpp:68-96) on Ray{originOffset, l, 1e-4, |l|}; `live` =
                 // lanes still without an occluder (first hit wins, order irrelevant for a bool)
-                const Ray sr = make_ray(oox, ooy, ooz, lx, ly, lz, 0.0001f, mag);
+                unsigned long long sslow;
+                const Ray sr = make_ray(oox, ooy, ooz, lx, ly, lz, 0.0001f, mag, sslow);
                 unsigned long long live = hitmask;
-                const bool sfast = (hitmask & ~finite_inv_mask(sr)) == 0 && S.tri_fast;
+                const bool sfast = (hitmask & sslow) == 0 && S.tri_fast;
                 const int soct =
                     (RTX_OCTANT && sfast && S.oct_bytes && PHASE == 0 && S.n_meshes) ? batch_octant(sr, hitmask) : -1;
                 if (COUNT && did) cnt.c[kShadow]++;
