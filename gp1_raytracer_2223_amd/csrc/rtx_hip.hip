@@ -428,6 +428,12 @@ __device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t lin
 #ifndef RTX_OCTANT
 #define RTX_OCTANT 1
 #endif
+// primary-ray plane loop: skip the division when no lane can hit (1) or always divide (0:
+// camera rays nearly always have candidates, and the skip test costs a ballot, an s_and
+// and a branch per plane)
+#ifndef RTX_PPLANE_SKIP
+#define RTX_PPLANE_SKIP 0
+#endif
 // bvh_walk without counters, shaped for the scalar unit: one inner loop descends through
 // inner nodes with scalar selects (no i1 value crosses a block, so nothing is carried as a
 // VGPR boolean or a lane-mask flow variable), a dead end leaves it as an empty "leaf", and
@@ -731,9 +737,13 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
     if (COUNT && valid) cnt.c[kPixels] = 1;
 
     // ---- primary ray (Renderer.cpp:104-114; Matrix::TransformVector Matrix.cpp:35-42)
+    // (px + 0.5f) / W and (2 * (py + 0.5f)) / H as Markstein quotients with the exact
+    // reciprocals RN(1/W), RN(1/H) (wave-uniform): numerators in [0.5, 2^17], divisors in
+    // [1, 2^16] lie inside div_rn's domain (rtx_fastdiv.h), so each is the IEEE quotient.
     const int W = static_cast<int>(F.width), H = static_cast<int>(F.height);
-    const float cx = (2.f * ((px + 0.5f) / W) - 1) * F.aspect * V.fov;
-    const float cy = (1.f - (2.f * (py + 0.5f) / H)) * V.fov;
+    const float fW = static_cast<float>(W), fH = static_cast<float>(H);
+    const float cx = (2.f * div_rn(px + 0.5f, fW, rcp_rn(fW)) - 1) * F.aspect * V.fov;
+    const float cy = (1.f - div_rn(2.f * (py + 0.5f), fH, rcp_rn(fH))) * V.fov;
     float dx = V.right[0] * cx + V.up[0] * cy + V.forward[0] * 1.f;
     float dy = V.right[1] * cx + V.up[1] * cy + V.forward[1] * 1.f;
     float dz = V.right[2] * cx + V.up[2] * cy + V.forward[2] * 1.f;
@@ -770,7 +780,9 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
         ldcb32(S.planes, opaque(i), p0, p1);
         if (COUNT && valid) cnt.c[kPlane]++;
         const float num = plane_num(p0, p1, vr), den = plane_den(p1, vr);
+#if RTX_PPLANE_SKIP
         if (!(plane_same_sign(num, den) & active)) continue;   // no lane can have t >= tmin > 0
+#endif
         const float t = num / den;
         const bool h = valid & (t >= vr.tmin) & (t < vr.tmax);
         sc_t = h ? t : sc_t;
