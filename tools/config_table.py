@@ -3,7 +3,8 @@ reference CPU Renderer built in place (oracle/_ref/ref_harness) on the same box'
 
 GPU: kernel-only ms/frame (HIP events, min of 3 x `iters` launches), algorithmic FLOP of one
 frame (instrumented kernel, SURVEY §8(d) model), end-to-end ms incl. the D2H copy of the
-frame into pageable host memory.  CPU: median Renderer::Render seconds over `frames` frames.
+frame into pageable host memory; frames-in-flight throughput (2 render contexts, frames issued
+round robin, as bench.py).  CPU: median Renderer::Render seconds over `frames` frames.
 Usage (GPU box):  python tools/config_table.py [out.json]
 """
 import ctypes as C
@@ -64,6 +65,7 @@ def main():
     except OSError:
         pass
     ctx = DeviceContext(0)
+    ctx2 = DeviceContext(0)   # second frame in flight
     rows = []
     for scene, W, H, frames in CONFIGS:
         hs = HostScene(scene)
@@ -83,12 +85,25 @@ def main():
                                          None), "rtx_render", ctx.h)
             ts.append(time.perf_counter() - t0)
         e2e_ms = float(np.median(ts)) * 1e3
+        # frames in flight: two contexts, frames issued round robin, wall time per frame
+        ctx2.upload(s)
+        pair = (ctx, ctx2)
+        nfl = 10 if scene == "Synthetic100k" else 200
+        for i in range(20):
+            abi.check(ctx.lib.rtx_render_async(pair[i % 2].h, C.byref(cam), C.byref(p), 0), "render", ctx.h)
+        ctx.synchronize(); ctx2.synchronize()
+        t0 = time.perf_counter()
+        for i in range(nfl):
+            abi.check(ctx.lib.rtx_render_async(pair[i % 2].h, C.byref(cam), C.byref(p), 0), "render", ctx.h)
+        ctx.synchronize(); ctx2.synchronize()
+        fl_ms = (time.perf_counter() - t0) / nfl * 1e3
         row = {"scene": scene, "width": W, "height": H, "mode": "combined", "shadows": True,
                "kernel_ms": round(ms, 5), "mpix_s": round(W * H / (ms * 1e-3) / 1e6, 1),
                "flop_per_px": round(flop / (W * H), 1),
                "tflops": round(flop / (ms * 1e-3) / 1e12, 3),
                "frac_fp32": round(flop / (ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
-               "e2e_ms": round(e2e_ms, 4), "e2e_mpix_s": round(W * H / (e2e_ms * 1e-3) / 1e6, 1)}
+               "e2e_ms": round(e2e_ms, 4), "e2e_mpix_s": round(W * H / (e2e_ms * 1e-3) / 1e6, 1),
+               "inflight2_ms": round(fl_ms, 5), "inflight2_mpix_s": round(W * H / (fl_ms * 1e-3) / 1e6, 1)}
         if harness.exists():
             r = cpu_ref(harness, scene, W, H, threads, frames)
             row.update({"cpu_mpix_s": round(r["mpix_s"], 3), "cpu_threads": threads, "cpu_frames": frames,
@@ -99,6 +114,7 @@ def main():
     if out_path:
         out_path.write_text(json.dumps(meta, indent=1))
     ctx.close()
+    ctx2.close()
 
 
 if __name__ == "__main__":
