@@ -193,16 +193,19 @@ def main() -> int:
     ap.add_argument("--inflight", type=int, default=2, help="frames in flight (render contexts per GPU)")
     args = ap.parse_args()
 
+    # The render contexts come up BEFORE the gloo process group: torch's gloo barrier
+    # initialises torch's own bundled HIP runtime, after which this process's ROCm runtime
+    # (librtx_hip) no longer detects the device ("no ROCm-capable device", seen at N = 2).
+    # RTX_BENCH_DEVICE pins every rank to one device: rehearsing the N-rank path on a
+    # one-GPU machine (the driver's multi-GPU runs leave it unset: rank r -> device LOCAL_RANK)
+    dev = int(os.environ.get("RTX_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    ctxs = [DeviceContext(dev) for _ in range(max(1, args.inflight))]
     d = Dist()
     N = d.world
     if args.gpus != N and d.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={N}; using {N}", file=sys.stderr)
     hs = HostScene(args.scene)
     scene, cam = hs.view()
-    # RTX_BENCH_DEVICE pins every rank to one device: rehearsing the N-rank path on a
-    # one-GPU machine (the driver's multi-GPU runs leave it unset: rank r -> device LOCAL_RANK)
-    dev = int(os.environ.get("RTX_BENCH_DEVICE", d.local))
-    ctxs = [DeviceContext(dev) for _ in range(max(1, args.inflight))]
     for c in ctxs:
         c.upload(scene)
     ctx = ctxs[0]

@@ -1255,14 +1255,29 @@ bool build_parts(const std::vector<float4>& nodes, uint32_t root, uint32_t mesh,
 
 extern "C" int rtx_abi_version(void) { return RTX_ABI_VERSION; }
 
+namespace {
+// Reason for the last failed rtx_create on this thread (rtx_last_error(NULL)).
+thread_local std::string g_create_err;
+}  // namespace
+
 extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     if (!out) return RTX_E_INVALID;
     *out = nullptr;
+    g_create_err.clear();
     rtx_ctx* c = new (std::nothrow) rtx_ctx;
     if (!c) return RTX_E_NOMEM;
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) { delete c; return RTX_E_DEVICE; }
-    if (device_id < 0 || device_id >= n) { delete c; return RTX_E_INVALID; }
+    const hipError_t ce = hipGetDeviceCount(&n);
+    if (ce != hipSuccess || n == 0) {
+        g_create_err = std::string("hipGetDeviceCount: ") + (ce != hipSuccess ? hipGetErrorString(ce) : "no device");
+        delete c;
+        return RTX_E_DEVICE;
+    }
+    if (device_id < 0 || device_id >= n) {
+        g_create_err = "device id out of range";
+        delete c;
+        return RTX_E_INVALID;
+    }
     c->device = device_id;
     // RTX_TILE_ORDER=0 disables cost-ordered tile dispatch (identity order every frame)
     if (const char* e = std::getenv("RTX_TILE_ORDER")) c->sched_enabled = std::strcmp(e, "0") != 0;
@@ -1278,26 +1293,37 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     }
     const size_t heavy_px = static_cast<size_t>(kMaxHeavyTiles) * 64;   // pixels of the heavy wave tiles
     int cus = 0, lo_prio = 0, hi_prio = 0;
-    if (hipSetDevice(device_id) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_heavy, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->sb[0].done, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->sb[1].done, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-        hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess ||
-        hipStreamCreateWithPriority(&c->split_stream, hipStreamNonBlocking, hi_prio) != hipSuccess ||
-        hipMalloc(&c->d_counters, sizeof(unsigned long long) * kNumCounters) != hipSuccess ||
-        hipMalloc(&c->d_heavy_n, 4) != hipSuccess || hipHostMalloc(&c->h_heavy_n, 4) != hipSuccess ||
-        hipMalloc(&c->d_heavy_list[0], 4 * kMaxHeavyTiles) != hipSuccess ||
-        hipMalloc(&c->d_heavy_list[1], 4 * kMaxHeavyTiles) != hipSuccess ||
-        hipMalloc(&c->d_hit_key, 8 * heavy_px) != hipSuccess || hipMalloc(&c->d_occ, 4 * heavy_px) != hipSuccess ||
-        hipMemset(c->d_hit_key, 0xff, 8 * heavy_px) != hipSuccess || hipMemset(c->d_occ, 0, 4 * heavy_px) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id) != hipSuccess) {
-        rtx_destroy(c);
-        return RTX_E_DEVICE;
-    }
+#define RTX_CREATE_TRY(call)                                                             \
+    do {                                                                                 \
+        const hipError_t e_ = (call);                                                    \
+        if (e_ != hipSuccess) {                                                          \
+            g_create_err = std::string(#call) + ": " + hipGetErrorString(e_);            \
+            rtx_destroy(c);                                                              \
+            return RTX_E_DEVICE;                                                         \
+        }                                                                                \
+    } while (0)
+    RTX_CREATE_TRY(hipSetDevice(device_id));
+    RTX_CREATE_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    RTX_CREATE_TRY(hipEventCreate(&c->ev0));
+    RTX_CREATE_TRY(hipEventCreate(&c->ev1));
+    RTX_CREATE_TRY(hipEventCreateWithFlags(&c->ev_heavy, hipEventDisableTiming));
+    RTX_CREATE_TRY(hipEventCreateWithFlags(&c->sb[0].done, hipEventDisableTiming));
+    RTX_CREATE_TRY(hipEventCreateWithFlags(&c->sb[1].done, hipEventDisableTiming));
+    RTX_CREATE_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    RTX_CREATE_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    RTX_CREATE_TRY(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+    RTX_CREATE_TRY(hipStreamCreateWithPriority(&c->split_stream, hipStreamNonBlocking, hi_prio));
+    RTX_CREATE_TRY(hipMalloc(&c->d_counters, sizeof(unsigned long long) * kNumCounters));
+    RTX_CREATE_TRY(hipMalloc(&c->d_heavy_n, 4));
+    RTX_CREATE_TRY(hipHostMalloc(&c->h_heavy_n, 4));
+    RTX_CREATE_TRY(hipMalloc(&c->d_heavy_list[0], 4 * kMaxHeavyTiles));
+    RTX_CREATE_TRY(hipMalloc(&c->d_heavy_list[1], 4 * kMaxHeavyTiles));
+    RTX_CREATE_TRY(hipMalloc(&c->d_hit_key, 8 * heavy_px));
+    RTX_CREATE_TRY(hipMalloc(&c->d_occ, 4 * heavy_px));
+    RTX_CREATE_TRY(hipMemset(c->d_hit_key, 0xff, 8 * heavy_px));
+    RTX_CREATE_TRY(hipMemset(c->d_occ, 0, 4 * heavy_px));
+    RTX_CREATE_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id));
+#undef RTX_CREATE_TRY
     // waves resident at once: 7 per SIMD, 4 SIMDs per CU at the render kernel's occupancy
     c->split_slots = static_cast<uint32_t>(cus > 0 ? cus : 1) * 28u;
     *out = c;
@@ -1337,7 +1363,8 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     delete c;
 }
 
-extern "C" const char* rtx_last_error(const rtx_ctx* c) { return c ? c->err.c_str() : "null context"; }
+// NULL: why the last rtx_create on this thread failed (empty if it did not).
+extern "C" const char* rtx_last_error(const rtx_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
 
 extern "C" int rtx_scene_bytes(const rtx_ctx* c, uint64_t* bytes) {
     if (!c || !bytes) return RTX_E_INVALID;

@@ -33,7 +33,8 @@ class DeviceContext:
         h = C.c_void_p()
         rc = self.lib.rtx_create(C.byref(h), int(device))
         if rc != abi.RTX_OK:
-            raise RuntimeError(f"rtx_create(device={device}) failed with code {rc} (no usable HIP device?)")
+            why = (self.lib.rtx_last_error(None) or b"").decode(errors="replace")
+            raise RuntimeError(f"rtx_create(device={device}) failed with code {rc}: {why or 'no usable HIP device?'}")
         self.h = h
         self.device = device
         self._uploaded = None

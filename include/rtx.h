@@ -175,6 +175,8 @@ int rtx_abi_version(void);
  * is the supported multi-GPU model).  Creates its own non-blocking stream. */
 int rtx_create(rtx_ctx** out, int device_id);
 void rtx_destroy(rtx_ctx* ctx);
+/* Reason for the last error on `ctx`; with ctx == NULL, why the calling thread's last
+ * rtx_create failed. */
 const char* rtx_last_error(const rtx_ctx* ctx);
 /* Copy the caller-owned scene into HBM (device layout of DESIGN.md §3).  The caller
  * may free its arrays afterwards.  Re-call after an animated Scene::Update. */

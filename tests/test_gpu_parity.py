@@ -214,3 +214,27 @@ def test_octant_slab_path_bit_identical(gpu_ctx, name, shadows, monkeypatch):
     assert np.array_equal(opx, gpx) and np.array_equal(orgb.view(np.uint32), grgb.view(np.uint32))
     rpx, rrgb = oracle_bind.render(s, cam, p)
     _compare(name, opx, orgb, rpx, rrgb, exact=name in POW_FREE)
+
+
+def test_frames_in_flight_bit_identical(gpu_ctx):
+    """Two contexts on one device rendering alternate frames (bench.py --inflight 2) while each
+    other's launches are still running: every frame equals the single-context frame."""
+    import ctypes as C
+    from gp1_raytracer_2223_amd.renderer import DeviceContext
+    hs = HostScene("W4_Bunny")
+    s, cam = hs.view()
+    p = abi.make_params(640, 360)
+    gpu_ctx.upload(s)
+    ref, _ = gpu_ctx.render(cam, p, want_rgb=False)
+    other = DeviceContext(0)
+    try:
+        other.upload(s)
+        pair = (gpu_ctx, other)
+        for i in range(40):   # enqueue without waiting: launches of the two contexts overlap
+            c = pair[i % 2]
+            abi.check(c.lib.rtx_render_async(c.h, C.byref(cam), C.byref(p), 0), "render", c.h)
+        for c in pair:
+            px, _ = c.render(cam, p, want_rgb=False)
+            assert np.array_equal(px, ref)
+    finally:
+        other.close()
