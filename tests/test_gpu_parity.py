@@ -216,14 +216,16 @@ def test_octant_slab_path_bit_identical(gpu_ctx, name, shadows, monkeypatch):
     _compare(name, opx, orgb, rpx, rrgb, exact=name in POW_FREE)
 
 
-def test_frames_in_flight_bit_identical(gpu_ctx):
+@pytest.mark.parametrize("name,W,H", [("W4_Bunny", 640, 360), ("W4_Optional", 480, 270), ("Synthetic100k", 320, 180)])
+def test_frames_in_flight_bit_identical(gpu_ctx, name, W, H):
     """Two contexts on one device rendering alternate frames (bench.py --inflight 2) while each
-    other's launches are still running: every frame equals the single-context frame."""
+    other's launches are still running — split rendering of heavy tiles included (own split
+    stream and buffers per context): every frame equals the single-context frame."""
     import ctypes as C
     from gp1_raytracer_2223_amd.renderer import DeviceContext
-    hs = HostScene("W4_Bunny")
+    hs = HostScene(name)
     s, cam = hs.view()
-    p = abi.make_params(640, 360)
+    p = abi.make_params(W, H)
     gpu_ctx.upload(s)
     ref, _ = gpu_ctx.render(cam, p, want_rgb=False)
     other = DeviceContext(0)
