@@ -303,6 +303,9 @@ def main() -> int:
                      "frac": round(achieved / FP32_PEAK_TFLOPS, 5), "traffic": traffic,
                      "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                      "hbm_gbs": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic and kernel_ms > 0 else None,
+                     # north star: the HBM roofline fraction, reported beside the VALU one
+                     "hbm_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                     if traffic and kernel_ms > 0 else None,
                      "kernel": "rtx_render_kernel<false, 0> (+ split phases 1-3 when tiles are heavy)", "kernel_ms": round(kernel_ms, 5),
                      "flop_per_launch": flop, "pixels_per_launch": pixels_per_rank,
                      "flop_per_pixel": round(flop / max(pixels_per_rank, 1), 2),
