@@ -212,6 +212,37 @@ __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const flo
     return fmaxf(rej, r.tmin - t);
 }
 
+// tri_t with two wave-uniform early exits for the lanes in `act` (the ones whose result is
+// used): after the cull test (Utils.h:114-127) and after the u range test (:160-163), the
+// rest is skipped when no lane in `act` can still be accepted — the same early returns as
+// the reference's, taken per wave.  A skipped triangle reports reject (1) for every lane.
+template <bool FAST>
+__device__ __forceinline__ float tri_t_wave(const float4 A, const float4 B, const float4 C, float cs, const Ray& r,
+                                            unsigned long long act, float& t) {
+    const float cullDot = A.w * r.dx + B.w * r.dy + C.w * r.dz;
+    float rej = fmaxf(FLT_EPSILON - fabsf(cullDot), cs * cullDot);
+    t = 0.f;
+    if ((ballot(!(rej > 0.f)) & act) == 0) return 1.f;
+    const float hx = r.dy * C.z - r.dz * C.y;
+    const float hy = -(r.dx * C.z - r.dz * C.x);
+    const float hz = r.dx * C.y - r.dy * C.x;
+    const float a = B.x * hx + B.y * hy + B.z * hz;
+    rej = fmaxf(rej, FLT_EPSILON - fabsf(a));
+    float ai = rcp_rn(a);
+    if (!(FAST && RTX_TRI_NOFIX) && __builtin_expect(fabsf(a) > 0x1p60f, 0)) ai = 1.f / a;
+    const float sx = r.ox - A.x, sy = r.oy - A.y, sz = r.oz - A.z;
+    const float u = ai * (sx * hx + sy * hy + sz * hz);
+    rej = fmaxf(rej, fmaxf(-u, u - 1.f));
+    if ((ballot(!(rej > 0.f)) & act) == 0) return 1.f;
+    const float qx = sy * B.z - sz * B.y;
+    const float qy = -(sx * B.z - sz * B.x);
+    const float qz = sx * B.y - sy * B.x;
+    const float v = ai * (r.dx * qx + r.dy * qy + r.dz * qz);
+    rej = fmaxf(rej, fmaxf(-v, (u + v) - 1.f));
+    t = ai * (C.x * qx + C.y * qy + C.z * qz);
+    return fmaxf(rej, r.tmin - t);
+}
+
 // SlabTest_BVH (Utils.h:221-243).  FAST uses v_min/v_max_f32, which differ from std::min/
 // std::max only when an operand is NaN; a NaN slab value needs (box - origin) * inv with
 // an infinite inv component, so FAST is taken only when every live lane's inverse
@@ -431,6 +462,9 @@ __device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t lin
 // primary-ray plane loop: skip the division when no lane can hit (1) or always divide (0:
 // camera rays nearly always have candidates, and the skip test costs a ballot, an s_and
 // and a branch per plane)
+#ifndef RTX_TRI_EARLY
+#define RTX_TRI_EARLY 1
+#endif
 #ifndef RTX_PPLANE_SKIP
 #define RTX_PPLANE_SKIP 0
 #endif
@@ -497,7 +531,11 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                 Tri T;
                 ldcb64(S.tris, ti, T.a, T.b, T.c, T.d);
                 float t;
+#if RTX_TRI_EARLY
+                const float rej = tri_t_wave<FAST>(T.a, T.b, T.c, cs, r, ANY ? (m & live) : m, t);
+#else
                 const float rej = tri_t<FAST>(T.a, T.b, T.c, cs, r, t);
+#endif
                 if (ANY) {
                     live &= ~(ballot(!(rej > 0.f)) & ballot(!(t >= r.tmax)) & m);
                 } else {
