@@ -215,14 +215,16 @@ __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const flo
 // tri_t with two wave-uniform early exits for the lanes in `act` (the ones whose result is
 // used): after the cull test (Utils.h:114-127) and after the u range test (:160-163), the
 // rest is skipped when no lane in `act` can still be accepted — the same early returns as
-// the reference's, taken per wave.  A skipped triangle reports reject (1) for every lane.
+// the reference's, taken per wave.  Returns false (wave-uniform) when the triangle was
+// skipped — no lane hits it — else true with the reject score in `rej_out` and t in `t`.
+// (A uniform flag rather than a reject value: a phi of the reject compare is carried as a
+// lane mask and rebuilt with v_cndmask + v_cmp per triangle.)
 template <bool FAST>
-__device__ __forceinline__ float tri_t_wave(const float4 A, const float4 B, const float4 C, float cs, const Ray& r,
-                                            unsigned long long act, float& t) {
+__device__ __forceinline__ bool tri_t_wave(const float4 A, const float4 B, const float4 C, float cs, const Ray& r,
+                                           unsigned long long act, float& rej_out, float& t) {
     const float cullDot = A.w * r.dx + B.w * r.dy + C.w * r.dz;
     float rej = fmaxf(FLT_EPSILON - fabsf(cullDot), cs * cullDot);
-    t = 0.f;
-    if ((ballot(!(rej > 0.f)) & act) == 0) return 1.f;
+    if ((ballot(!(rej > 0.f)) & act) == 0) return false;
     const float hx = r.dy * C.z - r.dz * C.y;
     const float hy = -(r.dx * C.z - r.dz * C.x);
     const float hz = r.dx * C.y - r.dy * C.x;
@@ -233,14 +235,15 @@ __device__ __forceinline__ float tri_t_wave(const float4 A, const float4 B, cons
     const float sx = r.ox - A.x, sy = r.oy - A.y, sz = r.oz - A.z;
     const float u = ai * (sx * hx + sy * hy + sz * hz);
     rej = fmaxf(rej, fmaxf(-u, u - 1.f));
-    if ((ballot(!(rej > 0.f)) & act) == 0) return 1.f;
+    if ((ballot(!(rej > 0.f)) & act) == 0) return false;
     const float qx = sy * B.z - sz * B.y;
     const float qy = -(sx * B.z - sz * B.x);
     const float qz = sx * B.y - sy * B.x;
     const float v = ai * (r.dx * qx + r.dy * qy + r.dz * qz);
     rej = fmaxf(rej, fmaxf(-v, (u + v) - 1.f));
     t = ai * (C.x * qx + C.y * qy + C.z * qz);
-    return fmaxf(rej, r.tmin - t);
+    rej_out = fmaxf(rej, r.tmin - t);
+    return true;
 }
 
 // SlabTest_BVH (Utils.h:221-243).  FAST uses v_min/v_max_f32, which differ from std::min/
@@ -532,7 +535,8 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                 ldcb64(S.tris, ti, T.a, T.b, T.c, T.d);
                 float t;
 #if RTX_TRI_EARLY
-                const float rej = tri_t_wave<FAST>(T.a, T.b, T.c, cs, r, ANY ? (m & live) : m, t);
+                float rej;
+                if (!tri_t_wave<FAST>(T.a, T.b, T.c, cs, r, ANY ? (m & live) : m, rej, t)) continue;
 #else
                 const float rej = tri_t<FAST>(T.a, T.b, T.c, cs, r, t);
 #endif
