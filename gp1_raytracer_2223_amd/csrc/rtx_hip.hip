@@ -468,6 +468,11 @@ __device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t lin
 #ifndef RTX_TRI_EARLY
 #define RTX_TRI_EARLY 1
 #endif
+// shadow sphere loop: leave once no lane is live (1), or run to the end with a single loop
+// exit (0: a second exit is merged into the loop test as SGPR lane-mask logic)
+#ifndef RTX_SPHERE_BREAK
+#define RTX_SPHERE_BREAK 0
+#endif
 #ifndef RTX_PPLANE_SKIP
 #define RTX_PPLANE_SKIP 0
 #endif
@@ -924,7 +929,9 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                 // (single-condition loops with a separate exit test: a `&& live` loop
                 // condition is carried as a VGPR boolean by the compiler)
                 for (uint32_t i = 0; i < (PHASE == 2 ? 0u : S.n_spheres * 16u); i += 16u) {
+#if RTX_SPHERE_BREAK
                     if (!live) break;
+#endif
                     const float4 s = ldcb16(S.spheres, opaque(i));
                     if (COUNT && ((live >> lane) & 1ull)) cnt.c[kSphere]++;
                     const SphereProj q = sphere_perp(s, sr);
