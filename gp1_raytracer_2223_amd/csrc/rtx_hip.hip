@@ -1204,7 +1204,7 @@ struct rtx_ctx {
     bool heavy_pending = false;
     uint32_t split_mode = 1;         // 0 off, 1 auto, 2 force (RTX_SPLIT=0 / unset / force)
     uint32_t split_slots = 0;        // concurrent render waves on this device
-    uint32_t split_permille = kSplitFactor * 1000;   // RTX_SPLIT_FACTOR (tuning)
+    uint32_t split_permille = kSplitPermille;   // RTX_SPLIT_FACTOR (tuning)
     uint32_t split_parts = kPartsPerMesh;            // RTX_SPLIT_PARTS (tuning)
     bool split_ok = false;           // the uploaded scene admits split rendering
     unsigned long long* d_hit_key = nullptr;

@@ -19,12 +19,14 @@ constexpr int kCostBuckets = 32;
 constexpr int kSchedPeriod = 64;      // frames between tile-cost measurements
 
 // Split rendering of heavy tiles: a wave tile whose measured cost exceeds
-// kSplitFactor x (frame cost / concurrent wave slots) is rendered by three extra
+// kSplitPermille/1000 x (frame cost / concurrent wave slots) is rendered by three extra
 // launches in which its BVH traversals are cut into subtree parts run by separate workgroups.
 constexpr int kPartsPerMesh = 64;      // target frontier size per mesh BVH
 constexpr int kMaxParts = 1024;        // all meshes together
 constexpr int kMaxHeavyTiles = 8192;   // heavy wave tiles per frame (hit-key buffer: 64 px each)
-constexpr int kSplitFactor = 2;
+// 1.5 (v14 sweep, tools/split_sweep.sh): Synthetic100k 4.38 -> 3.51 ms, W4_Optional within
+// noise of 2.0; below 1.25 the split overhead outgrows the tail it removes
+constexpr int kSplitPermille = 1500;
 constexpr int kMaxSplitLights = 32;    // occlusion bits per pixel
 
 // Work counters (SURVEY §8(d) cost model; same order as the oracle's).
