@@ -1,6 +1,7 @@
 // rtx_kernels.h — device layout of the uploaded scene and the per-frame launch record.
 // Shared by the kernels and the host-side upload code in rtx_hip.hip.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace rtxd {
@@ -76,6 +77,7 @@ struct DevScene {
     uint32_t oct_bytes;
 };
 
+constexpr size_t kOctantMaxNodeBytes = size_t(1) << 20;   // octant node copies only below this (per copy)
 constexpr int kMaxViews = 8;   // views (camera positions) rendered by one launch
 
 struct ViewCam {
