@@ -473,6 +473,10 @@ __device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t lin
 #ifndef RTX_SPHERE_BREAK
 #define RTX_SPHERE_BREAK 0
 #endif
+#ifndef RTX_PNUM_CACHE
+#define RTX_PNUM_CACHE 1
+#endif
+constexpr int kPlaneCache = 8;   // planes whose shadow-ray numerators are kept in LDS
 #ifndef RTX_PPLANE_SKIP
 #define RTX_PPLANE_SKIP 0
 #endif
@@ -729,6 +733,8 @@ template <bool COUNT, int PHASE>
 __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_render_kernel(const DevScene S, const FrameArgs F) {
     __shared__ uint4 stkE[kBlockThreads / 64][kStackDepth];
     __shared__ unsigned long long stkT[COUNT ? kBlockThreads / 64 : 1][kStackDepth];
+    // per-lane shadow-ray plane numerators, shared by every light (see the light loop)
+    __shared__ float pnumS[RTX_PNUM_CACHE ? kBlockThreads / 64 : 1][RTX_PNUM_CACHE ? kPlaneCache : 1][64];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
 #if RTX_STAMPS
     // diagnostic build only: per-wave {start, end, hw_id} in the counters buffer
@@ -940,15 +946,35 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                     const float t = sphere_t(s, q);
                     live &= ~(near & ballot(!(t < sr.tmin)) & ballot(!(t > sr.tmax)));
                 }
-                for (uint32_t i = 0; i < ((RTX_ABL_SPLANE || PHASE == 2) ? 0u : S.n_planes * 32u); i += 32u) {
-                    float4 p0, p1;
-                    ldcb32(S.planes, opaque(i), p0, p1);
-                    if (COUNT && ((live >> lane) & 1ull)) cnt.c[kPlane]++;
-                    const float num = plane_num(p0, p1, sr), den = plane_den(p1, sr);
-                    const unsigned long long cand = plane_same_sign(num, den) & live;
-                    if (!cand) continue;   // also taken once no lane is live
-                    const float t = num / den;
-                    live &= ~(ballot(t >= sr.tmin) & ballot(t < sr.tmax) & cand);
+                // HitTest_Plane's numerator (p0 - o) . n depends only on the shadow ray's origin,
+                // the same originOffset for every light: the first light computes it and keeps it
+                // in LDS, the others read it back (same value, bit for bit).  One loop version
+                // per case, so no per-plane select.
+                const uint32_t np = (RTX_ABL_SPLANE || PHASE == 2) ? 0u : S.n_planes * 32u;
+                const bool cache_ok = RTX_PNUM_CACHE && !COUNT && np <= static_cast<uint32_t>(kPlaneCache) * 32u;
+                if (cache_ok && li != l_first) {
+                    for (uint32_t i = 0; i < np; i += 32u) {
+                        float4 p0, p1;
+                        ldcb32(S.planes, opaque(i), p0, p1);
+                        const float num = pnumS[RTX_PNUM_CACHE ? wave : 0][RTX_PNUM_CACHE ? (i >> 5) : 0][lane];
+                        const float den = plane_den(p1, sr);
+                        const unsigned long long cand = plane_same_sign(num, den) & live;
+                        if (!cand) continue;
+                        const float t = num / den;
+                        live &= ~(ballot(t >= sr.tmin) & ballot(t < sr.tmax) & cand);
+                    }
+                } else {
+                    for (uint32_t i = 0; i < np; i += 32u) {
+                        float4 p0, p1;
+                        ldcb32(S.planes, opaque(i), p0, p1);
+                        if (COUNT && ((live >> lane) & 1ull)) cnt.c[kPlane]++;
+                        const float num = plane_num(p0, p1, sr), den = plane_den(p1, sr);
+                        if (cache_ok) pnumS[RTX_PNUM_CACHE ? wave : 0][RTX_PNUM_CACHE ? (i >> 5) : 0][lane] = num;
+                        const unsigned long long cand = plane_same_sign(num, den) & live;
+                        if (!cand) continue;   // also taken once no lane is live
+                        const float t = num / den;
+                        live &= ~(ballot(t >= sr.tmin) & ballot(t < sr.tmax) & cand);
+                    }
                 }
                 for (uint32_t mi = 0; mi < ((RTX_ABL_SMESH || PHASE != 0) ? 0u : S.n_meshes); ++mi) {
                     if (!live) break;
