@@ -90,3 +90,16 @@ def test_product_does_not_link_oracle():
 
 def test_abi_version():
     assert abi.load_hip().rtx_abi_version() == 1
+
+
+def test_create_reports_why_it_failed():
+    """Bad arguments come back as codes, never as a crash; a failed rtx_create leaves its
+    reason for rtx_last_error(NULL).  (No GPU here: the device query itself fails or the
+    device id is out of range — either way a reason is recorded.)"""
+    lib = abi.load_hip()
+    assert lib.rtx_create(None, 0) == abi.RTX_E_INVALID
+    h = C.c_void_p()
+    rc = lib.rtx_create(C.byref(h), 1 << 20)   # no machine has that many devices
+    assert rc in (abi.RTX_E_DEVICE, abi.RTX_E_INVALID)
+    assert not h.value
+    assert lib.rtx_last_error(None)   # non-empty reason
