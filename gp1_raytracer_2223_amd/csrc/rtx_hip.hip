@@ -268,9 +268,8 @@ __device__ __forceinline__ bool tri_t_wave(const float4 A, const float4 B, const
 //               component, so it is taken only when every live lane's inverse direction is
 //               finite (decided once per ray batch with a ballot);
 //   kSlabOct    kSlabFast for a ray batch whose inverse directions have ONE sign per axis
-//               (an octant), against the node copy mirrored for that octant (see
-//               octant_ray): the near and far planes are known, so min/max of each pair
-//               disappears (below).
+//               (an octant), against the node copy ordered (near, far) for that octant:
+//               the near and far planes are known, so min/max of each pair disappears.
 // Returned as a wave lane mask: one v_cmp per condition straight into SGPRs (a ballot
 // of the && would materialise the bool in a VGPR and compare it again).
 enum { kSlabExact = 0, kSlabFast = 1, kSlabOct = 2 };
@@ -281,10 +280,9 @@ __device__ __forceinline__ unsigned long long slab_mask(const float4 a, const fl
     const float tz1 = (b.x - r.oz) * r.iz, tz2 = (b.y - r.oz) * r.iz;
     float tMin, tMax;
     if (SLAB == kSlabOct) {
-        // Octant copy: per axis the record holds (near, far) with near <= far in the
-        // mirrored frame, r.o is the mirrored origin and r.i = |inv| > 0, so rounding
-        // monotonicity gives t_near <= t_far per axis (the pair's min and max), and each
-        // value equals the reference's up to the sign of a zero (negation is exact).
+        // Octant copy: per axis the record holds (near, far) = (lo, hi) where inv > 0 and
+        // (hi, lo) where inv < 0, so rounding monotonicity gives t_near <= t_far per axis
+        // (the pair's min and max); each value is the reference's own (same operands).
         tMin = fmaxf(fmaxf(fmaxf(tx1, ty1), tz1), 0x1p-149f);
         tMax = fminf(fminf(tx2, ty2), tz2);
         return ballot(tMax >= tMin);
@@ -316,18 +314,6 @@ __device__ __forceinline__ int batch_octant(const Ray& r, unsigned long long mas
     const uint32_t c0 = __builtin_amdgcn_readlane(code, first);
     return (ballot(code == c0) & mask) == mask ? static_cast<int>(c0) : -1;
 }
-// The slab view of a ray in octant `oct`'s mirrored frame: a mirrored axis negates the
-// origin (the node copy stores (-hi, -lo) there), every inverse direction becomes |inv|.
-// (-hi - (-o)) * |inv| == (hi - o) * inv exactly: negation commutes with RN.
-__device__ __forceinline__ Ray octant_ray(const Ray& r, int oct) {
-    Ray q = r;
-    q.ox = (oct & 1) ? -r.ox : r.ox;
-    q.oy = (oct & 2) ? -r.oy : r.oy;
-    q.oz = (oct & 4) ? -r.oz : r.oz;
-    q.ix = fabsf(r.ix); q.iy = fabsf(r.iy); q.iz = fabsf(r.iz);
-    return q;
-}
-
 // The mesh record carries its cull sign as float bits (set at upload: -1 FrontFaceCulling,
 // +1 BackFaceCulling, 0 NoCulling); shadow rays use the negation, the reference's swap.
 __device__ __forceinline__ float cull_sign(int cs_bits, bool shadow) {
@@ -484,10 +470,9 @@ constexpr int kPlaneCache = 8;   // planes whose shadow-ray numerators are kept 
 // inner nodes with scalar selects (no i1 value crosses a block, so nothing is carried as a
 // VGPR boolean or a lane-mask flow variable), a dead end leaves it as an empty "leaf", and
 // the pop loop is the only other path.  Same visits, tests and order as bvh_walk.
-// `nb` is the node copy the slab form reads (the octant's mirrored copy for kSlabOct) and
-// `q` the ray as the slab test sees it (octant_ray), `r` the ray of the triangle tests.
+// `nb` is the node copy the slab form reads (the octant's (near, far) copy for kSlabOct).
 template <bool ANY, int SLAB>
-__device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, const Ray& r, const Ray& q, uint32_t link,
+__device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, const Ray& r, uint32_t link,
                               uint32_t ntri, unsigned long long m, unsigned long long mask, uint32_t lane, uint4* stk,
                               float& sc_t, uint32_t& sc_tri, unsigned long long& live, const uint32_t* occ_word,
                               uint32_t occ_bit) {
@@ -497,8 +482,8 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
         while (ntri == 0) {
             NodePair P;
             ldcb64(nb, link, P.l0, P.l1, P.r0, P.r1);
-            const unsigned long long ml = slab_mask<SLAB>(P.l0, P.l1, q) & m;
-            const unsigned long long mr = slab_mask<SLAB>(P.r0, P.r1, q) & m;
+            const unsigned long long ml = slab_mask<SLAB>(P.l0, P.l1, r) & m;
+            const unsigned long long mr = slab_mask<SLAB>(P.r0, P.r1, r) & m;
 #if RTX_ASM_SELECT
             // next (link, ntri): left, else right, else a dead end taken as an empty leaf
             // (ntri = 1 with m = 0); `both` = mr if the left child is taken too (the right
@@ -587,17 +572,16 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
     const float4* nb = OCT ? reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.nodes) +
                                                              static_cast<uint32_t>(oct) * S.oct_bytes)
                            : S.nodes;
-    const Ray q = OCT ? octant_ray(r, oct) : r;
     // root (odd global index; every child pair starts at an even one, 64-B aligned)
     float4 b0, b1;
     ldcb32(nb, static_cast<uint32_t>(M.x), b0, b1);   // M.x: the root's byte offset
     if (COUNT && ((mask >> lane) & 1ull)) cnt.c[kSlab]++;
     const unsigned long long m =
-        (OCT ? slab_mask<kSlabOct>(b0, b1, q) : slab_mask<FAST ? kSlabFast : kSlabExact>(b0, b1, r)) & mask;
+        (OCT ? slab_mask<kSlabOct>(b0, b1, r) : slab_mask<FAST ? kSlabFast : kSlabExact>(b0, b1, r)) & mask;
     if (m == 0) return;
     if (RTX_LEAN_WALK && !COUNT && !RTX_STAMPS)
         bvh_walk_lean<ANY, OCT ? kSlabOct : (FAST ? kSlabFast : kSlabExact)>(
-            S, nb, cull_sign(M.z, ANY), r, q, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask, lane, stk, sc_t,
+            S, nb, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask, lane, stk, sc_t,
             sc_tri, live, nullptr, 0u);
     else
         bvh_walk<ANY, FAST, COUNT>(S, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask,
@@ -631,7 +615,7 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, uns
     }
     if (m == 0) return;
     if (RTX_LEAN_WALK && !RTX_STAMPS)
-        bvh_walk_lean<ANY, FAST ? kSlabFast : kSlabExact>(S, S.nodes, cull_sign(M.z, ANY), r, r, link, ntri, m, mask,
+        bvh_walk_lean<ANY, FAST ? kSlabFast : kSlabExact>(S, S.nodes, cull_sign(M.z, ANY), r, link, ntri, m, mask,
                                                           lane, stk, sc_t, sc_tri, live, occ_word, occ_bit);
     else
         bvh_walk<ANY, FAST, false>(S, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, nullptr, sc_t, sc_tri,
@@ -1571,8 +1555,8 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
             const bool mx = k & 1, my = k & 2, mz = k & 4;
             for (size_t n = 0; n < nodes.size(); n += 2) {
                 const float4 a = nodes[n], b = nodes[n + 1];
-                dst[n] = f4(mx ? -a.y : a.x, mx ? -a.x : a.y, my ? -a.w : a.z, my ? -a.z : a.w);
-                dst[n + 1] = f4(mz ? -b.y : b.x, mz ? -b.x : b.y, b.z, b.w);
+                dst[n] = f4(mx ? a.y : a.x, mx ? a.x : a.y, my ? a.w : a.z, my ? a.z : a.w);
+                dst[n + 1] = f4(mz ? b.y : b.x, mz ? b.x : b.y, b.z, b.w);
             }
         }
     } else {

@@ -70,8 +70,9 @@ struct DevScene {
     // stays inside the exact fast-reciprocal domain (rtx_fastdiv.h)
     uint32_t tri_fast;
     // Byte stride between the 8 octant copies of the node array (0: no copies, the octant
-    // slab path is off).  Copy k mirrors the axes whose bit is set in k: per axis it
-    // stores (-hi, -lo) instead of (lo, hi), every (lo, hi) ordered lo <= hi (checked at
+    // slab path is off).  Copy k swaps the axes whose bit is set in k (the axes a ray of
+    // octant k crosses from hi to lo): per axis it stores (hi, lo) instead of (lo, hi),
+    // every (lo, hi) ordered lo <= hi (checked at
     // upload); links, counts and slots are the same in every copy.  Copy 0 is the array
     // the other slab forms read.
     uint32_t oct_bytes;
