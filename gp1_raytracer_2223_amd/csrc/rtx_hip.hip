@@ -165,6 +165,18 @@ __device__ __forceinline__ float plane_den(const float4 p1, const Ray& r) {
 __device__ __forceinline__ unsigned long long plane_same_sign(float num, float den) {
     return ballot((__float_as_int(num) ^ __float_as_int(den)) >= 0);
 }
+#ifndef RTX_PLANE_BEYOND
+#define RTX_PLANE_BEYOND 1
+#endif
+// Shadow rays (finite tmax): a lane whose exact |num| / |den| exceeds tmax cannot hit either —
+// RN(num/den) >= tmax by monotonicity — and one fma tells it exactly: the sign of
+// RN(|den| * tmax - |num|) is the sign of the exact value (an underflow to -0 reads as "not
+// beyond", and a NaN or inf operand as well; the division then decides).  Walls behind the
+// light are the common case, so most waves skip the division.
+__device__ __forceinline__ unsigned long long plane_cand(float num, float den, float tmax) {
+    if (!RTX_PLANE_BEYOND) return plane_same_sign(num, den);
+    return ballot(((__float_as_int(num) ^ __float_as_int(den)) >= 0) & !(fmaf(fabsf(den), tmax, -fabsf(num)) < 0.f));
+}
 
 // HitTest_Triangle (Utils.h:109-184), Möller–Trumbore with the reference's cull rules
 // (shadow rays swap front/back culling, :114-127).
@@ -942,7 +954,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                         ldcb32(S.planes, opaque(i), p0, p1);
                         const float num = pnumS[RTX_PNUM_CACHE ? wave : 0][RTX_PNUM_CACHE ? (i >> 5) : 0][lane];
                         const float den = plane_den(p1, sr);
-                        const unsigned long long cand = plane_same_sign(num, den) & live;
+                        const unsigned long long cand = plane_cand(num, den, sr.tmax) & live;
                         if (!cand) continue;
                         const float t = num / den;
                         live &= ~(ballot(t >= sr.tmin) & ballot(t < sr.tmax) & cand);
@@ -954,7 +966,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
                         if (COUNT && ((live >> lane) & 1ull)) cnt.c[kPlane]++;
                         const float num = plane_num(p0, p1, sr), den = plane_den(p1, sr);
                         if (cache_ok) pnumS[RTX_PNUM_CACHE ? wave : 0][RTX_PNUM_CACHE ? (i >> 5) : 0][lane] = num;
-                        const unsigned long long cand = plane_same_sign(num, den) & live;
+                        const unsigned long long cand = plane_cand(num, den, sr.tmax) & live;
                         if (!cand) continue;   // also taken once no lane is live
                         const float t = num / den;
                         live &= ~(ballot(t >= sr.tmin) & ballot(t < sr.tmax) & cand);
