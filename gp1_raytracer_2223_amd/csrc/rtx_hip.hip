@@ -787,12 +787,12 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
 
     // ---- primary ray (Renderer.cpp:104-114; Matrix::TransformVector Matrix.cpp:35-42)
     // (px + 0.5f) / W and (2 * (py + 0.5f)) / H as Markstein quotients with the exact
-    // reciprocals RN(1/W), RN(1/H) (wave-uniform): numerators in [0.5, 2^17], divisors in
+    // reciprocals RN(1/W), RN(1/H) (divided on the host, FrameArgs): numerators in [0.5, 2^17], divisors in
     // [1, 2^16] lie inside div_rn's domain (rtx_fastdiv.h), so each is the IEEE quotient.
     const int W = static_cast<int>(F.width), H = static_cast<int>(F.height);
     const float fW = static_cast<float>(W), fH = static_cast<float>(H);
-    const float cx = (2.f * div_rn(px + 0.5f, fW, rcp_rn(fW)) - 1) * F.aspect * V.fov;
-    const float cy = (1.f - div_rn(2.f * (py + 0.5f), fH, rcp_rn(fH))) * V.fov;
+    const float cx = (2.f * div_rn(px + 0.5f, fW, F.inv_width) - 1) * F.aspect * V.fov;
+    const float cy = (1.f - div_rn(2.f * (py + 0.5f), fH, F.inv_height)) * V.fov;
     float dx = V.right[0] * cx + V.up[0] * cy + V.forward[0] * 1.f;
     float dy = V.right[1] * cx + V.up[1] * cy + V.forward[1] * 1.f;
     float dz = V.right[2] * cx + V.up[2] * cy + V.forward[2] * 1.f;
@@ -885,7 +885,7 @@ __global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_rende
             const float4 s = ldcb16(S.spheres, best_idx);
             nx = hx - s.x; ny = hy - s.y; nz = hz - s.z;
             const float m = sqrtf(nx * nx + ny * ny + nz * nz);   // closestHit.normal.Normalize()
-            nx /= m; ny /= m; nz /= m;
+            div3_exact(nx, ny, nz, m);   // nx /= m; ny /= m; nz /= m
             mat = ldc(S.sphere_mat, best_idx >> 4);
         } else if (best_kind == 2) {
             float4 p0, p1;
@@ -1692,6 +1692,8 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         F.cam[v].fov = cams[v].fov;
     }
     F.aspect = static_cast<int>(p->width) / static_cast<float>(static_cast<int>(p->height));  // Renderer.cpp:30
+    F.inv_width = 1.f / static_cast<float>(static_cast<int>(p->width));
+    F.inv_height = 1.f / static_cast<float>(static_cast<int>(p->height));
     F.width = p->width; F.height = p->height;
     F.mode = p->lighting_mode; F.shadows = p->shadows_enabled ? 1 : 0;
     F.rshift = p->format.rshift; F.gshift = p->format.gshift; F.bshift = p->format.bshift; F.amask = p->format.amask;

@@ -93,6 +93,7 @@ struct ViewCam {
 struct FrameArgs {
     ViewCam cam[kMaxViews];       // blockIdx.z selects the view
     float aspect;                 // (float)W / (float)H  (Renderer.cpp:30)
+    float inv_width, inv_height;  // RN(1/W), RN(1/H): IEEE divisions on the host
     uint32_t width, height;
     int32_t mode, shadows;
     uint32_t rshift, gshift, bshift, amask;
