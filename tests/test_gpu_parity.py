@@ -240,3 +240,42 @@ def test_frames_in_flight_bit_identical(gpu_ctx, name, W, H):
             assert np.array_equal(px, ref)
     finally:
         other.close()
+
+
+LIGHTS_ON_PLANES = {
+    # a point light exactly on a wall: shadow rays from the other walls reach it at t == tmax
+    # on that wall's plane (the near-tie of the shadow-ray plane skip, plane_cand), and rays
+    # from the wall itself run parallel to it (den = 0)
+    "floor": "light point 0.5 0 3  30 1 1 1",
+    "back": "light point 1 2 10  30 1 0.8 0.6",
+    "side": "light point -5 3 2  30 0.6 0.8 1",
+    # just in front of / just behind the floor (one ulp of 1e-7-ish), and a corner
+    "near_floor": "light point 0.5 1e-7 3  30 1 1 1\nlight point 0.5 -1e-7 3.5  30 1 1 1",
+    "corner": "light point -5 0 10  40 1 1 1",
+}
+
+
+@pytest.mark.parametrize("case", sorted(LIGHTS_ON_PLANES))
+@pytest.mark.parametrize("mode", [3, 1])
+def test_lights_on_planes(gpu_ctx, tmp_path, case, mode):
+    """Adversarial shadow-ray cases (lights on or one ulp off a plane) render bit-exact like
+    the oracle: Lambert-only scene, so no powf anywhere."""
+    path = tmp_path / f"{case}.rtxscene"
+    path.write_text("\n".join([
+        "camera 0 2.5 -8 50",
+        "material lambert 0.49 0.57 0.57 1",
+        "material lambert 1 1 1 1",
+        "plane 0 0 10   0 0 -1  1",
+        "plane 0 0 0    0 1 0   1",
+        "plane -5 0 0   1 0 0   1",
+        "sphere 2 1 2 0.9 2",
+        "mesh lowpoly_bunny2 2 back scale 1.5 1.5 1.5 translate 0 0 0.5",
+        LIGHTS_ON_PLANES[case],
+    ]) + "\n")
+    hs = HostScene(f"file:{path}")
+    s, cam = hs.view()
+    p = abi.make_params(256, 144, mode, 1)
+    gpu_ctx.upload(s)
+    gpx, grgb = gpu_ctx.render(cam, p)
+    rpx, rrgb = oracle_bind.render(s, cam, p)
+    _compare(f"{case}/m{mode}", gpx, grgb, rpx, rrgb, exact=True)
