@@ -175,7 +175,9 @@ __device__ __forceinline__ unsigned long long plane_same_sign(float num, float d
 // light are the common case, so most waves skip the division.
 __device__ __forceinline__ unsigned long long plane_cand(float num, float den, float tmax) {
     if (!RTX_PLANE_BEYOND) return plane_same_sign(num, den);
-    return ballot(((__float_as_int(num) ^ __float_as_int(den)) >= 0) & !(fmaf(fabsf(den), tmax, -fabsf(num)) < 0.f));
+    const int same = (__float_as_int(num) ^ __float_as_int(den)) >= 0;
+    const int beyond = fmaf(fabsf(den), tmax, -fabsf(num)) < 0.f;
+    return ballot(same & !beyond);
 }
 
 // HitTest_Triangle (Utils.h:109-184), Möller–Trumbore with the reference's cull rules
