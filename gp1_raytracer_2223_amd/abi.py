@@ -136,7 +136,10 @@ def load_host() -> C.CDLL:
 HIP_SYMBOLS = ["rtx_abi_version", "rtx_create", "rtx_destroy", "rtx_last_error", "rtx_upload_scene",
                "rtx_render", "rtx_render_async", "rtx_synchronize", "rtx_download", "rtx_device_buffers",
                "rtx_time_frames", "rtx_scene_bytes", "rtx_count_work",
-               "rtx_render_views_async", "rtx_time_views", "rtx_count_work_ex", "rtx_split_info"]
+               "rtx_render_views_async", "rtx_time_views", "rtx_count_work_ex", "rtx_split_info",
+               "rtx_gather_async", "rtx_host_register", "rtx_host_unregister",
+               "rtx_group_create", "rtx_group_destroy", "rtx_group_last_error", "rtx_group_size",
+               "rtx_group_context", "rtx_group_upload_scene", "rtx_group_render"]
 
 
 def load_hip() -> C.CDLL:
@@ -189,6 +192,28 @@ def load_hip() -> C.CDLL:
         if hasattr(lib, "rtx_split_info"):   # absent only in older experiment builds (RTX_HIP_LIB)
             lib.rtx_split_info.argtypes = [VP, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
             lib.rtx_split_info.restype = C.c_int
+        if hasattr(lib, "rtx_group_create"):   # absent only in older experiment builds
+            lib.rtx_gather_async.argtypes = [VP, C.POINTER(C.c_uint32), C.POINTER(C.c_float)]
+            lib.rtx_gather_async.restype = C.c_int
+            lib.rtx_host_register.argtypes = [VP, VP, C.c_size_t]
+            lib.rtx_host_register.restype = C.c_int
+            lib.rtx_host_unregister.argtypes = [VP, VP]
+            lib.rtx_host_unregister.restype = C.c_int
+            lib.rtx_group_create.argtypes = [C.POINTER(VP), C.POINTER(C.c_int), C.c_int]
+            lib.rtx_group_create.restype = C.c_int
+            lib.rtx_group_destroy.argtypes = [VP]
+            lib.rtx_group_destroy.restype = None
+            lib.rtx_group_last_error.argtypes = [VP]
+            lib.rtx_group_last_error.restype = C.c_char_p
+            lib.rtx_group_size.argtypes = [VP]
+            lib.rtx_group_size.restype = C.c_int
+            lib.rtx_group_context.argtypes = [VP, C.c_int]
+            lib.rtx_group_context.restype = VP
+            lib.rtx_group_upload_scene.argtypes = [VP, C.POINTER(Scene)]
+            lib.rtx_group_upload_scene.restype = C.c_int
+            lib.rtx_group_render.argtypes = [VP, C.POINTER(Camera), C.POINTER(RenderParams), C.POINTER(C.c_uint32),
+                                             C.POINTER(C.c_float)]
+            lib.rtx_group_render.restype = C.c_int
         _hip = lib
     return _hip
 

@@ -56,7 +56,7 @@ def build_host(force: bool = False) -> Path:
 def build_hip(force: bool = False) -> Path:
     LIB.mkdir(exist_ok=True)
     out = LIB / "librtx_hip.so"
-    srcs = [CSRC / "rtx_hip.hip"]
+    srcs = [CSRC / "rtx_hip.hip", CSRC / "rtx_group.cpp"]
     deps = srcs + list(CSRC.glob("*.h")) + [INC / "rtx.h", Path(__file__)]   # flags live here
     if force or _stale(out, deps):
         # -fno-slp-vectorize: the SLP packer turns independent f32 ops into v_pk_* plus
@@ -67,7 +67,7 @@ def build_hip(force: bool = False) -> Path:
         _run([HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-O3", "-ffp-contract=off",
               "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize",
               "-mllvm", "-structurizecfg-skip-uniform-regions=true",
-              "-DRTX_MIN_WAVES_PER_EU=6", "-fPIC", "-shared",
+              "-DRTX_MIN_WAVES_PER_EU=6", "-fPIC", "-shared", "-pthread",
               "-Wall", f"-I{INC}", f"-I{CSRC}", *srcs, "-o", out])
     return out
 

@@ -1851,7 +1851,13 @@ extern "C" int rtx_synchronize(rtx_ctx* c) {
     return RTX_OK;
 }
 
-extern "C" int rtx_download(rtx_ctx* c, uint32_t* out_px, float* out_rgb) {
+namespace {
+
+// Queue the D2H copy of the rows the last render owns (every view) into the caller's
+// full-frame host buffers, on the context stream.  A striped frame is one
+// hipMemcpy2DAsync per view and plane: `stripe_rows` rows every `stripe_step` stripes
+// (row pitch of the 2-D copy = stripe_step stripes), plus the trailing partial stripe.
+int queue_owned_copy(rtx_ctx* c, uint32_t* out_px, float* out_rgb) {
     if (!c || !out_px) return RTX_E_INVALID;
     if (!c->last_valid) return fail(c, RTX_E_STATE, "nothing rendered yet");
     if (out_rgb && !c->last_rgb) return fail(c, RTX_E_STATE, "last render did not produce colours");
@@ -1859,21 +1865,64 @@ extern "C" int rtx_download(rtx_ctx* c, uint32_t* out_px, float* out_rgb) {
     HIP_TRY(c, hipSetDevice(c->device));
     const size_t W = p.width, H = p.height;
     const bool striped = p.stripe_rows != 0 && p.stripe_step > 1;
-    const uint32_t rows_per = striped ? p.stripe_rows : static_cast<uint32_t>(H);
-    const uint32_t step = striped ? p.stripe_step : 1;
     for (int v = 0; v < c->last_views; ++v) {
-        const uint32_t first = striped ? (p.stripe_first + step - static_cast<uint32_t>(v) % step) % step : 0;
         const size_t base = static_cast<size_t>(v) * W * H;
-        for (size_t s = first; s * rows_per < H; s += step) {
-            const size_t r0 = s * rows_per, r1 = (r0 + rows_per < H) ? r0 + rows_per : H;
-            HIP_TRY(c, hipMemcpyAsync(out_px + base + r0 * W, c->d_px + base + r0 * W, (r1 - r0) * W * 4,
-                                      hipMemcpyDeviceToHost, c->stream));
+        if (!striped) {
+            HIP_TRY(c, hipMemcpyAsync(out_px + base, c->d_px + base, W * H * 4, hipMemcpyDeviceToHost, c->stream));
             if (out_rgb)
-                HIP_TRY(c, hipMemcpyAsync(out_rgb + 3 * (base + r0 * W), c->d_rgb + 3 * (base + r0 * W),
-                                          (r1 - r0) * W * 12, hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(c, hipMemcpyAsync(out_rgb + 3 * base, c->d_rgb + 3 * base, W * H * 12, hipMemcpyDeviceToHost,
+                                          c->stream));
+            continue;
+        }
+        const size_t rows = p.stripe_rows, step = p.stripe_step;
+        const size_t first = (p.stripe_first + step - static_cast<uint32_t>(v) % step) % step;
+        // owned stripes s = first + k*step; the full ones end at or before row H
+        size_t n_full = 0;
+        if ((first + 1) * rows <= H) n_full = ((H / rows) - 1 - first) / step + 1;
+        const size_t last = first + n_full * step;   // next owned stripe (maybe partial or past H)
+        struct Plane { char* dst; const char* src; size_t elem; };
+        const Plane planes[2] = {{reinterpret_cast<char*>(out_px), reinterpret_cast<const char*>(c->d_px), 4},
+                                 {reinterpret_cast<char*>(out_rgb), reinterpret_cast<const char*>(c->d_rgb), 12}};
+        for (const Plane& pl : planes) {
+            if (!pl.dst) continue;
+            const size_t row_b = W * pl.elem, off = (base + first * rows * W) * pl.elem;
+            if (n_full)
+                HIP_TRY(c, hipMemcpy2DAsync(pl.dst + off, step * rows * row_b, pl.src + off, step * rows * row_b,
+                                            rows * row_b, n_full, hipMemcpyDeviceToHost, c->stream));
+            if (last * rows < H) {
+                const size_t o2 = (base + last * rows * W) * pl.elem;
+                HIP_TRY(c, hipMemcpyAsync(pl.dst + o2, pl.src + o2, (H - last * rows) * row_b, hipMemcpyDeviceToHost,
+                                          c->stream));
+            }
         }
     }
+    return RTX_OK;
+}
+
+}  // namespace
+
+extern "C" int rtx_download(rtx_ctx* c, uint32_t* out_px, float* out_rgb) {
+    const int rc = queue_owned_copy(c, out_px, out_rgb);
+    if (rc != RTX_OK) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return RTX_OK;
+}
+
+extern "C" int rtx_gather_async(rtx_ctx* c, uint32_t* out_px, float* out_rgb) {
+    return queue_owned_copy(c, out_px, out_rgb);
+}
+
+extern "C" int rtx_host_register(rtx_ctx* c, void* p, size_t bytes) {
+    if (!c || !p || !bytes) return RTX_E_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipHostRegister(p, bytes, hipHostRegisterPortable));
+    return RTX_OK;
+}
+
+extern "C" int rtx_host_unregister(rtx_ctx* c, void* p) {
+    if (!c || !p) return RTX_E_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipHostUnregister(p));
     return RTX_OK;
 }
 

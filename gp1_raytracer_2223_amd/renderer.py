@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes as C
 import struct
+import weakref
 
 import numpy as np
 
@@ -70,6 +71,17 @@ class DeviceContext:
     def synchronize(self):
         abi.check(self.lib.rtx_synchronize(self.h), "rtx_synchronize", self.h)
 
+    def gather_async(self, out_px: np.ndarray, out_rgb: np.ndarray | None = None) -> None:
+        """Queue the D2H copy of the rows the last render owns into full-frame host arrays
+        (rtx_gather_async); complete after synchronize()."""
+        assert out_px.dtype == np.uint32 and out_px.flags.c_contiguous
+        rgbp = None
+        if out_rgb is not None:
+            assert out_rgb.dtype == np.float32 and out_rgb.flags.c_contiguous
+            rgbp = out_rgb.ctypes.data_as(C.POINTER(C.c_float))
+        abi.check(self.lib.rtx_gather_async(self.h, out_px.ctypes.data_as(C.POINTER(C.c_uint32)), rgbp),
+                  "rtx_gather_async", self.h)
+
     def time_frames(self, cam, params, iters: int) -> float:
         ms = C.c_float()
         abi.check(self.lib.rtx_time_frames(self.h, C.byref(cam), C.byref(params), int(iters), C.byref(ms)),
@@ -88,6 +100,52 @@ class DeviceContext:
         return np.array(list(out), dtype=np.uint64)
 
 
+class DeviceGroup:
+    """Owns one rtx_group: one frame tiled over several contexts (GPUs) by this process,
+    each member with its own host thread and stream gathering its 16-row stripes into
+    one host frame (include/rtx.h)."""
+
+    def __init__(self, devices):
+        self.lib = abi.load_hip()
+        ids = (C.c_int * len(devices))(*[int(d) for d in devices])
+        h = C.c_void_p()
+        rc = self.lib.rtx_group_create(C.byref(h), ids, len(devices))
+        if rc != abi.RTX_OK:
+            why = (self.lib.rtx_group_last_error(None) or b"").decode(errors="replace")
+            raise RuntimeError(f"rtx_group_create({list(devices)}) failed with code {rc}: {why}")
+        self.h = h
+        self.devices = list(devices)
+
+    def _check(self, rc, what):
+        if rc != abi.RTX_OK:
+            why = (self.lib.rtx_group_last_error(self.h) or b"").decode(errors="replace")
+            raise RuntimeError(f"{what} failed with code {rc}: {why}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.rtx_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, scene: abi.Scene) -> None:
+        self._check(self.lib.rtx_group_upload_scene(self.h, C.byref(scene)), "rtx_group_upload_scene")
+
+    def render(self, cam: abi.Camera, params: abi.RenderParams, want_rgb: bool = True, out_px=None):
+        n = params.width * params.height
+        px = np.zeros(n, np.uint32) if out_px is None else out_px
+        rgb = np.zeros(3 * n, np.float32) if want_rgb else None
+        rc = self.lib.rtx_group_render(self.h, C.byref(cam), C.byref(params),
+                                       px.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                       rgb.ctypes.data_as(C.POINTER(C.c_float)) if want_rgb else None)
+        self._check(rc, "rtx_group_render")
+        return px, rgb
+
+
 class Renderer:
     def __init__(self, width: int, height: int, device: int = 0, stripe: tuple[int, int, int] | None = None,
                  pixel_format=abi.XRGB8888):
@@ -98,7 +156,8 @@ class Renderer:
         self.stripe = stripe
         self.format = pixel_format
         self.ctx = DeviceContext(device)
-        self._scene_key = None
+        self._scene_ref = None    # weakref to the uploaded HostScene
+        self._scene_gen = -1      # its generation at upload
         self.buffer = np.zeros(self.m_Width * self.m_Height, np.uint32)
         self.rgb = None
 
@@ -110,9 +169,11 @@ class Renderer:
     def Render(self, scene: HostScene, upload: bool = True, want_rgb: bool = False) -> np.ndarray:
         """Renderer::Render (Renderer.cpp:34-98): blocking; fills self.buffer."""
         s, cam = scene.view()
-        if upload or self._scene_key is not id(scene):
+        same = self._scene_ref is not None and self._scene_ref() is scene and self._scene_gen == scene.generation
+        if upload or not same:
             self.ctx.upload(s)
-            self._scene_key = id(scene)
+            self._scene_ref = weakref.ref(scene)
+            self._scene_gen = scene.generation
         n = self.m_Width * self.m_Height
         rgb = np.zeros(3 * n, np.float32) if want_rgb else None
         rc = self.ctx.lib.rtx_render(self.ctx.h, C.byref(cam), C.byref(self.params()),

@@ -30,6 +30,9 @@ class HostScene:
         if rc != abi.RTX_OK:
             raise RuntimeError(f"scene {name!r}: {err.value.decode()} (code {rc})")
         self._h = h
+        # bumped by every update(): a Renderer re-uploads when the generation it uploaded
+        # differs (value comparison, so a recycled id() can never alias another scene)
+        self.generation = 0
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -44,6 +47,7 @@ class HostScene:
 
     def update(self, total_time: float) -> None:
         abi.check(self._lib.rtx_host_scene_update(self._h, float(total_time)), "rtx_host_scene_update")
+        self.generation += 1
 
     @property
     def animated(self) -> bool:

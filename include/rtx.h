@@ -201,6 +201,18 @@ int rtx_render_views_async(rtx_ctx* ctx, const rtx_camera* cams, int n_views,
 int rtx_synchronize(rtx_ctx* ctx);
 /* Copy the context's frame buffer (rows owned by the last render) to host memory. */
 int rtx_download(rtx_ctx* ctx, uint32_t* out_pixels, float* out_rgb);
+/* Host gather of one partition: queue, on the context stream, the D2H copy
+ * of the rows the last render owns into the caller's FULL-FRAME host buffers (row-major,
+ * pitch = width; one hipMemcpy2DAsync per view and plane for a striped render) and
+ * return.  Rows the context does not own are never written, so several contexts (GPUs,
+ * or processes sharing one mapping) can gather disjoint stripes into one frame.  Truly
+ * asynchronous only for page-locked memory (rtx_host_register); complete after
+ * rtx_synchronize. */
+int rtx_gather_async(rtx_ctx* ctx, uint32_t* out_pixels, float* out_rgb);
+/* Page-lock caller memory (e.g. a frame shared between the ranks' processes) for every
+ * device of the process (hipHostRegister, portable), and undo it. */
+int rtx_host_register(rtx_ctx* ctx, void* ptr, size_t bytes);
+int rtx_host_unregister(rtx_ctx* ctx, void* ptr);
 /* Device pointers of the HBM frame buffer (width*height uint32 / 3*width*height f32). */
 int rtx_device_buffers(rtx_ctx* ctx, void** d_pixels, void** d_rgb);
 /* Time `iters` back-to-back launches of the render kernel(s) with HIP events recorded
@@ -227,6 +239,29 @@ int rtx_count_work_ex(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_para
  * and the frontier size of the uploaded scene (0 = the scene is rendered unsplit).
  * Environment: RTX_SPLIT=0 disables, RTX_SPLIT=force splits every tile (tests). */
 int rtx_split_info(rtx_ctx* ctx, uint32_t* heavy_tiles, uint32_t* parts);
+
+/* ---- one frame over several GPUs from one process ------------------
+ * The reference's Renderer::Render covers the frame with parallel_for
+ * (source/Renderer.cpp:79-85); a group covers it with G render contexts instead.  Rows are
+ * dealt in `stripe_rows`-row stripes round robin (member i owns stripe s iff s % G == i);
+ * each member has its own host thread and stream, renders its stripes and gathers them
+ * straight into the caller's host frame (rtx_gather_async).  rtx_group_render blocks until
+ * the whole frame is in out_pixels / out_rgb; the result is bit-identical to one
+ * context's rtx_render.  Device ids may repeat (several contexts on one GPU). */
+#define RTX_GROUP_MAX 64
+typedef struct rtx_group rtx_group;
+int rtx_group_create(rtx_group** out, const int* device_ids, int n);
+void rtx_group_destroy(rtx_group* group);
+/* Reason for the group's last error; with NULL, why this thread's last create failed. */
+const char* rtx_group_last_error(const rtx_group* group);
+int rtx_group_size(const rtx_group* group);
+/* Member i's context (owned by the group), e.g. for rtx_time_frames on its stripes. */
+rtx_ctx* rtx_group_context(rtx_group* group, int i);
+int rtx_group_upload_scene(rtx_group* group, const rtx_scene* scene);
+/* params: stripe_rows = stripe height (multiple of 16; 0 = 16); stripe_step must be 0/1
+ * (the group assigns the stripes).  out_pixels: width*height uint32; out_rgb may be NULL. */
+int rtx_group_render(rtx_group* group, const rtx_camera* cam, const rtx_render_params* params,
+                     uint32_t* out_pixels, float* out_rgb);
 
 #ifdef __cplusplus
 }

@@ -63,7 +63,7 @@ def test_reference_record_sizes():
 
 def _declared(header: Path) -> list[str]:
     txt = header.read_text()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(rtx_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*|rtx_ctx\*)\s+(rtx_\w+)\s*\(", txt, re.M)))
 
 
 def test_hip_library_exports_every_declared_symbol():

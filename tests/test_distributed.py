@@ -75,3 +75,31 @@ def test_stripe_partition_gloo(world):
     assert all(stitched), stitched
     assert sum(counts) == world * W * H          # every pixel of every view exactly once
     assert len(set(counts)) == 1                 # weak scaling: equal share per rank
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2])
+def test_bench_strong_mode_hip_gloo(world, tmp_path):
+    """The real multi-rank path on the HIP renderer: bench.py under torch.distributed.run
+    with `world` gloo ranks pinned to device 0 (RTX_BENCH_DEVICE; the driver's N-GPU runs
+    map rank r to device r).  Each rank renders its 16-row stripes of one Bunny 1080p frame
+    and gathers them into the shared page-locked host frame; rank 0 checks the gathered
+    frame against the reference's SHA-256 (bench.py `parity`)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, RTX_BENCH_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    port = 29700 + os.getpid() % 200
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(root / "bench.py"), "--gpus", str(world),
+           "--steps", "20", "--warmup", "5", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-4000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+    r = json.loads(line)
+    assert r["n_gpus"] == world and r["scaling"] == "strong"
+    assert r["parity"]["bit_exact"] is True, r["parity"]
+    assert r["roofline"]["frame_pixels_counted"] == 1920 * 1080   # every pixel exactly once over the ranks
+    assert r["host_gather"]["mpix_s"] > 0
