@@ -139,7 +139,7 @@ HIP_SYMBOLS = ["rtx_abi_version", "rtx_create", "rtx_destroy", "rtx_last_error",
                "rtx_render_views_async", "rtx_time_views", "rtx_count_work_ex", "rtx_split_info",
                "rtx_gather_async", "rtx_host_register", "rtx_host_unregister",
                "rtx_group_create", "rtx_group_destroy", "rtx_group_last_error", "rtx_group_size",
-               "rtx_group_context", "rtx_group_upload_scene", "rtx_group_render"]
+               "rtx_group_context", "rtx_group_upload_scene", "rtx_group_render", "rtx_schedule_state"]
 
 
 def load_hip() -> C.CDLL:
@@ -192,6 +192,10 @@ def load_hip() -> C.CDLL:
         if hasattr(lib, "rtx_split_info"):   # absent only in older experiment builds (RTX_HIP_LIB)
             lib.rtx_split_info.argtypes = [VP, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
             lib.rtx_split_info.restype = C.c_int
+        if hasattr(lib, "rtx_schedule_state"):
+            lib.rtx_schedule_state.argtypes = [VP, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_uint32,
+                                               C.POINTER(C.c_uint32)]
+            lib.rtx_schedule_state.restype = C.c_int
         if hasattr(lib, "rtx_group_create"):   # absent only in older experiment builds
             lib.rtx_gather_async.argtypes = [VP, C.POINTER(C.c_uint32), C.POINTER(C.c_float)]
             lib.rtx_gather_async.restype = C.c_int

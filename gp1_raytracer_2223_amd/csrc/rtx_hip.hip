@@ -1093,86 +1093,167 @@ template __global__ void rtx_render_kernel<false, 3>(const DevScene, const Frame
 
 // Next frames' dispatch order from this frame's per-tile cost: heaviest first, STABLE
 // within a cost class so that tiles rendered together stay spatial neighbours (they walk
-// the same BVH nodes: scalar-cache locality).  One workgroup: each thread owns a
-// contiguous run of tiles; counts[class][thread] + an exclusive scan in (class, thread)
-// order give every tile its slot.  Clears the costs it read.
-//
+// the same BVH nodes: scalar-cache locality).  The order is (class, tile index): the same
+// permutation a serial counting sort would give, computed by three launches over chunks of
+// kSchedChunk tiles (one 256-thread workgroup each):
+//   rtx_sched_count    per chunk: class histogram + cost sum (and the saved-cost fix-up)
+//   rtx_sched_scan     one workgroup: exclusive prefix of the histograms in (class, chunk)
+//                      order, the heavy threshold
+//   rtx_sched_scatter  per chunk: every tile's slot = its (class, chunk) base + its rank
+//                      among the chunk's tiles of that class; heavy flags / list; clears costs
 // It also picks the heavy tiles for split rendering: cost > split_permille/1000 x (total cost /
 // min(tiles, concurrent workgroup slots)), i.e. a tile that alone would outlast its share of
 // the frame.  `split_slots` = 0 disables splitting, UINT32_MAX forces every tile heavy
 // (tests).  Flags and list go to the staging set the host adopts at its next frame.
-__global__ void __launch_bounds__(kReorderThreads) rtx_reorder_kernel(uint32_t* __restrict__ cost,
-                                                                      uint32_t* __restrict__ order, uint32_t n,
-                                                                      uint32_t split_slots, uint32_t split_permille,
-                                                                      const uint32_t* __restrict__ was_heavy,
-                                                                      uint32_t* __restrict__ saved,
-                                                                      uint32_t* __restrict__ heavy_flag,
-                                                                      uint32_t* __restrict__ heavy_list,
-                                                                      uint32_t* __restrict__ heavy_n) {
-    __shared__ uint32_t cnt[kCostBuckets][kReorderThreads];
-    __shared__ uint32_t tot[kCostBuckets];
-    __shared__ unsigned long long csum[kReorderThreads];
-    __shared__ uint32_t nheavy;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t per = (n + kReorderThreads - 1) / kReorderThreads;
-    const uint32_t lo = tid * per, hi = (lo + per < n) ? lo + per : n;
-    auto bucket = [](uint32_t cst) -> uint32_t {   // heavier -> smaller class
-        const uint32_t lg = cst ? 32u - static_cast<uint32_t>(__builtin_clz(cst)) : 0u;   // 0..32
-        const uint32_t half = (cst && lg >= 2) ? ((cst >> (lg - 2)) & 1u) : 0u;
-        uint32_t k = 2u * lg + half;                                                     // 0..65
-        k = k > 2u * 6u ? k - 2u * 6u : 0u;        // costs below 2^6 (x16 cycles) share a class
-        return (kCostBuckets - 1) - (k < kCostBuckets ? k : kCostBuckets - 1);
-    };
-    // A tile rendered split this frame has no fresh one-piece cost: it keeps the one it had
-    // when it was last rendered whole (kept in `saved`).
-    for (uint32_t t = lo; t < hi; ++t) {
-        if (was_heavy && was_heavy[t])
-            cost[t] = saved[t];
-        else
-            saved[t] = cost[t];
-    }
-    for (int k = 0; k < kCostBuckets; ++k) cnt[k][tid] = 0;
-    for (uint32_t t = lo; t < hi; ++t) cnt[bucket(cost[t])][tid]++;
+__device__ __forceinline__ uint32_t cost_class(uint32_t cst) {   // heavier -> smaller class
+    const uint32_t lg = cst ? 32u - static_cast<uint32_t>(__builtin_clz(cst)) : 0u;   // 0..32
+    const uint32_t half = (cst && lg >= 2) ? ((cst >> (lg - 2)) & 1u) : 0u;
+    uint32_t k = 2u * lg + half;                                                     // 0..65
+    k = k > 2u * 6u ? k - 2u * 6u : 0u;        // costs below 2^6 (x16 cycles) share a class
+    return (kCostBuckets - 1) - (k < kCostBuckets ? k : kCostBuckets - 1);
+}
+
+// A tile rendered split this frame has no fresh one-piece cost: it keeps the one it had
+// when it was last rendered whole (kept in `saved`).
+__global__ void __launch_bounds__(kReorderThreads) rtx_sched_count(uint32_t* __restrict__ cost, uint32_t n,
+                                                                   const uint32_t* __restrict__ was_heavy,
+                                                                   uint32_t* __restrict__ saved,
+                                                                   uint32_t* __restrict__ hist,
+                                                                   unsigned long long* __restrict__ csum,
+                                                                   uint32_t nchunks) {
+    __shared__ uint32_t h[kCostBuckets];
+    __shared__ unsigned long long tot;
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * kSchedChunk;
+    if (tid < kCostBuckets) h[tid] = 0;
+    if (tid == 0) tot = 0;
     __syncthreads();
-    if (tid < kCostBuckets) {   // exclusive scan of one class row
-        uint32_t acc = 0;
-        for (int j = 0; j < kReorderThreads; ++j) { const uint32_t v = cnt[tid][j]; cnt[tid][j] = acc; acc += v; }
-        tot[tid] = acc;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t acc = 0;
-        for (int k = 0; k < kCostBuckets; ++k) { const uint32_t v = tot[k]; tot[k] = acc; acc += v; }
-    }
-    __syncthreads();
-    for (uint32_t t = lo; t < hi; ++t) {
-        const uint32_t k = bucket(cost[t]);
-        order[tot[k] + cnt[k][tid]++] = t;
-    }
-    // heavy tiles
     unsigned long long my = 0;
-    for (uint32_t t = lo; t < hi; ++t) my += cost[t];
-    csum[tid] = my;
-    if (tid == 0) nheavy = 0;
+    for (uint32_t k = 0; k < kSchedChunk / kReorderThreads; ++k) {
+        const uint32_t t = base + k * kReorderThreads + tid;   // coalesced; counting ignores order
+        if (t >= n) break;
+        uint32_t c = cost[t];
+        if (was_heavy && was_heavy[t]) {
+            c = saved[t];
+            cost[t] = c;
+        } else {
+            saved[t] = c;
+        }
+        atomicAdd(&h[cost_class(c)], 1u);
+        my += c;
+    }
+    atomicAdd(&tot, my);
     __syncthreads();
-    for (uint32_t w = kReorderThreads / 2; w > 0; w >>= 1) {
-        if (tid < w) csum[tid] += csum[tid + w];
+    if (tid < kCostBuckets) hist[tid * nchunks + blockIdx.x] = h[tid];
+    if (tid == 0) csum[blockIdx.x] = tot;
+}
+
+// Exclusive prefix of hist[class][chunk] in class-major order (in place), the total cost and
+// the heavy threshold; zeroes the heavy counter the scatter appends to.
+__global__ void __launch_bounds__(kScanThreads) rtx_sched_scan(uint32_t* __restrict__ hist, uint32_t nchunks,
+                                                               const unsigned long long* __restrict__ csum, uint32_t n,
+                                                               uint32_t split_slots, uint32_t split_permille,
+                                                               unsigned long long* __restrict__ thr_out,
+                                                               uint32_t* __restrict__ heavy_n) {
+    __shared__ uint32_t part[kScanThreads];
+    __shared__ unsigned long long cpart[kScanThreads];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t len = kCostBuckets * nchunks;
+    const uint32_t per = (len + kScanThreads - 1) / kScanThreads;
+    const uint32_t lo = tid * per, hi = (lo + per < len) ? lo + per : len;
+    uint32_t s = 0;
+    for (uint32_t i = lo; i < hi; ++i) s += hist[i];
+    unsigned long long cs = 0;
+    for (uint32_t i = tid; i < nchunks; i += kScanThreads) cs += csum[i];
+    part[tid] = s;
+    cpart[tid] = cs;
+    __syncthreads();
+    for (uint32_t off = 1; off < kScanThreads; off <<= 1) {   // inclusive Hillis-Steele scan
+        const uint32_t v = tid >= off ? part[tid - off] : 0u;
+        const unsigned long long w = tid >= off ? cpart[tid - off] : 0ull;
+        __syncthreads();
+        part[tid] += v;
+        cpart[tid] += w;
         __syncthreads();
     }
-    const bool force = split_slots == 0xffffffffu;
-    const unsigned long long thr =
-        (split_slots && !force) ? csum[0] * split_permille / (1000ull * (n < split_slots ? n : split_slots)) : ~0ull;
-    for (uint32_t t = lo; t < hi; ++t) {
-        uint32_t f = 0;
-        if (force || cost[t] > thr) {
-            const uint32_t k = atomicAdd(&nheavy, 1u);
-            if (k < static_cast<uint32_t>(kMaxHeavyTiles)) { heavy_list[k] = t; f = 1; }
-        }
-        heavy_flag[t] = f;
+    uint32_t acc = part[tid] - s;   // exclusive
+    for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t v = hist[i];
+        hist[i] = acc;
+        acc += v;
+    }
+    if (tid == 0) {
+        const unsigned long long total = cpart[kScanThreads - 1];
+        const bool force = split_slots == 0xffffffffu;
+        *thr_out = force ? 0ull
+                         : (split_slots ? total * split_permille / (1000ull * (n < split_slots ? n : split_slots))
+                                        : ~0ull);
+        *heavy_n = 0;
+    }
+}
+
+__global__ void __launch_bounds__(kReorderThreads) rtx_sched_scatter(uint32_t* __restrict__ cost,
+                                                                     uint32_t* __restrict__ order, uint32_t n,
+                                                                     const uint32_t* __restrict__ hist,
+                                                                     uint32_t nchunks,
+                                                                     const unsigned long long* __restrict__ thr_in,
+                                                                     uint32_t force, uint32_t* __restrict__ heavy_flag,
+                                                                     uint32_t* __restrict__ heavy_list,
+                                                                     uint32_t* __restrict__ heavy_n) {
+    constexpr uint32_t kPer = kSchedChunk / kReorderThreads;   // consecutive tiles per thread
+    constexpr uint32_t kSeg = kCostBuckets;   // (class, thread) entries scanned per thread: 32 x 256 / 256
+    __shared__ uint32_t cnt[kCostBuckets][kReorderThreads];
+    __shared__ uint32_t tsum[kReorderThreads];
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * kSchedChunk + tid * kPer;
+    uint32_t cls[kPer], cst[kPer];
+    for (uint32_t k = 0; k < kCostBuckets; ++k) cnt[k][tid] = 0;
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t t = base + k;
+        cst[k] = t < n ? cost[t] : 0u;
+        cls[k] = cost_class(cst[k]);
+        if (t < n) cnt[cls[k]][tid]++;
     }
     __syncthreads();
-    if (tid == 0) *heavy_n = nheavy < static_cast<uint32_t>(kMaxHeavyTiles) ? nheavy : kMaxHeavyTiles;
-    for (uint32_t t = lo; t < hi; ++t) cost[t] = 0;
+    // exclusive scan of cnt flattened in (class, thread) order: thread j scans kSeg
+    // consecutive entries, then the per-thread sums are scanned
+    uint32_t* flat = &cnt[0][0];
+    uint32_t s = 0;
+    for (uint32_t i = 0; i < kSeg; ++i) s += flat[tid * kSeg + i];
+    tsum[tid] = s;
+    __syncthreads();
+    for (uint32_t off = 1; off < kReorderThreads; off <<= 1) {
+        const uint32_t v = tid >= off ? tsum[tid - off] : 0u;
+        __syncthreads();
+        tsum[tid] += v;
+        __syncthreads();
+    }
+    uint32_t acc = tsum[tid] - s;
+    for (uint32_t i = 0; i < kSeg; ++i) {
+        const uint32_t v = flat[tid * kSeg + i];
+        flat[tid * kSeg + i] = acc;
+        acc += v;
+    }
+    __syncthreads();
+    // slot = global (class, chunk) base + rank within the chunk's class (= flattened prefix
+    // minus the prefix at the class's first thread) + rank within the thread
+    const unsigned long long thr = *thr_in;
+    uint32_t seen[kPer];
+    for (uint32_t k = 0; k < kPer; ++k) {
+        seen[k] = 0;
+        for (uint32_t j = 0; j < k; ++j) seen[k] += cls[j] == cls[k];
+    }
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t t = base + k;
+        if (t >= n) break;
+        const uint32_t c = cls[k];
+        order[hist[c * nchunks + blockIdx.x] + (cnt[c][tid] - cnt[c][0]) + seen[k]] = t;
+        uint32_t f = 0;
+        if (force || cst[k] > thr) {
+            const uint32_t h = atomicAdd(heavy_n, 1u);
+            if (h < static_cast<uint32_t>(kMaxHeavyTiles)) { heavy_list[h] = t; f = 1; }
+        }
+        heavy_flag[t] = f;
+        cost[t] = 0;
+    }
 }
 
 // ====================================================================== host side
@@ -1208,6 +1289,9 @@ struct rtx_ctx {
     uint32_t* d_order = nullptr;
     uint32_t* d_cost = nullptr;
     uint32_t* d_saved_cost = nullptr;   // last one-piece cost per tile
+    uint32_t* d_hist = nullptr;         // per (class, chunk) tile counts -> slot bases (rtx_sched_*)
+    unsigned long long* d_csum = nullptr;   // per chunk cost sums
+    unsigned long long* d_thr = nullptr;    // heavy threshold of the measured frame
     uint32_t sched_cap = 0;
     std::string sched_key;
     bool sched_ready = false;
@@ -1388,6 +1472,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     RTX_CREATE_TRY(hipStreamCreateWithPriority(&c->split_stream, hipStreamNonBlocking, hi_prio));
     RTX_CREATE_TRY(hipMalloc(&c->d_counters, sizeof(unsigned long long) * kNumCounters));
     RTX_CREATE_TRY(hipMalloc(&c->d_heavy_n, 4));
+    RTX_CREATE_TRY(hipMalloc(&c->d_thr, 8));
     RTX_CREATE_TRY(hipHostMalloc(&c->h_heavy_n, 4));
     RTX_CREATE_TRY(hipMalloc(&c->d_heavy_list[0], 4 * kMaxHeavyTiles));
     RTX_CREATE_TRY(hipMalloc(&c->d_heavy_list[1], 4 * kMaxHeavyTiles));
@@ -1418,6 +1503,9 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     (void)hipFree(c->d_order);
     (void)hipFree(c->d_cost);
     (void)hipFree(c->d_saved_cost);
+    (void)hipFree(c->d_hist);
+    (void)hipFree(c->d_csum);
+    (void)hipFree(c->d_thr);
     for (int k = 0; k < 2; ++k) { (void)hipFree(c->d_heavy_flag[k]); (void)hipFree(c->d_heavy_list[k]); }
     (void)hipFree(c->d_heavy_n);
     if (c->h_heavy_n) (void)hipHostFree(c->h_heavy_n);
@@ -1726,6 +1814,10 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         for (int k = 0; k < 2; ++k) { (void)hipFree(c->d_heavy_flag[k]); c->d_heavy_flag[k] = nullptr; }
         (void)hipFree(c->d_saved_cost);
         c->d_saved_cost = nullptr;
+        (void)hipFree(c->d_hist);
+        (void)hipFree(c->d_csum);
+        c->d_hist = nullptr;
+        c->d_csum = nullptr;
         c->d_order = nullptr;
         c->d_cost = nullptr;
         c->sched_cap = 0;
@@ -1733,6 +1825,9 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         HIP_TRY(c, hipMalloc(&c->d_cost, ntiles * 4));
         for (int k = 0; k < 2; ++k) HIP_TRY(c, hipMalloc(&c->d_heavy_flag[k], ntiles * 4));
         HIP_TRY(c, hipMalloc(&c->d_saved_cost, ntiles * 4));
+        const size_t nch = (ntiles + kSchedChunk - 1) / kSchedChunk;
+        HIP_TRY(c, hipMalloc(&c->d_hist, nch * kCostBuckets * 4));
+        HIP_TRY(c, hipMalloc(&c->d_csum, nch * 8));
         c->sched_cap = ntiles;
         c->sched_key.clear();
     }
@@ -1752,7 +1847,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         // adopt the heavy set the last measured frame selected (one sync per measurement)
         HIP_TRY(c, hipEventSynchronize(c->ev_heavy));
         c->heavy_pending = false;
-        c->heavy_n = *c->h_heavy_n;
+        c->heavy_n = std::min<uint32_t>(*c->h_heavy_n, kMaxHeavyTiles);
         c->heavy_cur ^= 1;
     }
     const bool split = c->split_mode != 0 && c->split_ok && c->sched_enabled && c->heavy_n > 0;
@@ -1807,9 +1902,16 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         const uint32_t slots = (c->split_mode == 0 || !c->split_ok) ? 0u
                                : (c->split_mode == 2 ? 0xffffffffu : c->split_slots);
         const int stage = c->heavy_cur ^ 1;
-        hipLaunchKernelGGL(rtx_reorder_kernel, dim3(1), dim3(kReorderThreads), 0, c->stream, F.cost, c->d_order,
-                           F.n_tiles, slots, c->split_permille, F.heavy_flag, c->d_saved_cost, c->d_heavy_flag[stage],
-                           c->d_heavy_list[stage], c->d_heavy_n);
+        const uint32_t nch = (F.n_tiles + kSchedChunk - 1) / kSchedChunk;
+        hipLaunchKernelGGL(rtx_sched_count, dim3(nch), dim3(kReorderThreads), 0, c->stream, F.cost, F.n_tiles,
+                           F.heavy_flag, c->d_saved_cost, c->d_hist, c->d_csum, nch);
+        HIP_TRY(c, hipGetLastError());
+        hipLaunchKernelGGL(rtx_sched_scan, dim3(1), dim3(kScanThreads), 0, c->stream, c->d_hist, nch, c->d_csum,
+                           F.n_tiles, slots, c->split_permille, c->d_thr, c->d_heavy_n);
+        HIP_TRY(c, hipGetLastError());
+        hipLaunchKernelGGL(rtx_sched_scatter, dim3(nch), dim3(kReorderThreads), 0, c->stream, F.cost, c->d_order,
+                           F.n_tiles, c->d_hist, nch, c->d_thr, slots == 0xffffffffu ? 1u : 0u,
+                           c->d_heavy_flag[stage], c->d_heavy_list[stage], c->d_heavy_n);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipMemcpyAsync(c->h_heavy_n, c->d_heavy_n, 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_heavy, c->stream));
@@ -1996,13 +2098,25 @@ extern "C" int rtx_count_work_ex(rtx_ctx* c, const rtx_camera* cam, const rtx_re
     return RTX_OK;
 }
 
+extern "C" int rtx_schedule_state(rtx_ctx* c, uint32_t* order, uint32_t* cost, uint32_t n, uint32_t* n_tiles) {
+    if (!c) return RTX_E_INVALID;
+    if (n_tiles) *n_tiles = c->sched_ready ? c->sched_cap : 0u;
+    if (!c->sched_ready || !order || !cost) return RTX_OK;
+    if (n > c->sched_cap) return fail(c, RTX_E_INVALID, "n exceeds the schedule size");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpy(order, c->d_order, n * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(cost, c->d_saved_cost, n * 4, hipMemcpyDeviceToHost));
+    return RTX_OK;
+}
+
 extern "C" int rtx_split_info(rtx_ctx* c, uint32_t* heavy_tiles, uint32_t* parts) {
     if (!c) return RTX_E_INVALID;
     if (c->heavy_pending) {   // a measured frame is in flight: report the set it selects
         HIP_TRY(c, hipSetDevice(c->device));
         HIP_TRY(c, hipEventSynchronize(c->ev_heavy));
     }
-    const uint32_t n = c->heavy_pending ? *c->h_heavy_n : c->heavy_n;
+    const uint32_t n = c->heavy_pending ? std::min<uint32_t>(*c->h_heavy_n, kMaxHeavyTiles) : c->heavy_n;
     const bool on = c->split_mode != 0 && c->split_ok && c->sched_enabled;
     if (heavy_tiles) *heavy_tiles = on ? n : 0u;
     if (parts) *parts = c->split_ok ? c->dev.n_parts : 0u;

@@ -15,7 +15,9 @@ constexpr int kStackDepth = 64;
 constexpr int kBlockThreads = RTX_BLOCK_THREADS;   // independent waves, each an 8 x 8 pixel "wave tile"
 constexpr int kWavesPerBlock = kBlockThreads / 64;
 constexpr int kWaveTile = 8;
-constexpr int kReorderThreads = 256;
+constexpr int kReorderThreads = 256;   // rtx_sched_count / rtx_sched_scatter workgroup
+constexpr int kSchedChunk = 1024;      // tiles per scheduling workgroup (4 per thread)
+constexpr int kScanThreads = 1024;     // rtx_sched_scan (one workgroup)
 constexpr int kCostBuckets = 32;
 constexpr int kSchedPeriod = 64;      // frames between tile-cost measurements
 

@@ -239,6 +239,11 @@ int rtx_count_work_ex(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_para
  * and the frontier size of the uploaded scene (0 = the scene is rendered unsplit).
  * Environment: RTX_SPLIT=0 disables, RTX_SPLIT=force splits every tile (tests). */
 int rtx_split_info(rtx_ctx* ctx, uint32_t* heavy_tiles, uint32_t* parts);
+/* Diagnostics of the cost-ordered dispatch (tests): after a measured frame, the dispatch
+ * permutation of the first n tiles' slots (`order`) and the one-piece tile costs it was
+ * sorted by (`cost`).  *n_tiles = tiles of the current schedule (0 = none measured yet;
+ * then nothing is copied). */
+int rtx_schedule_state(rtx_ctx* ctx, uint32_t* order, uint32_t* cost, uint32_t n, uint32_t* n_tiles);
 
 /* ---- one frame over several GPUs from one process ------------------
  * The reference's Renderer::Render covers the frame with parallel_for
