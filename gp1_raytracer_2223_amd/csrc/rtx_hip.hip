@@ -727,10 +727,13 @@ __device__ __forceinline__ uint32_t q8(float c) {
 #ifndef RTX_MIN_WAVES_PER_EU
 #define RTX_MIN_WAVES_PER_EU 1
 #endif
-template <bool COUNT, int PHASE>
-__global__ void __launch_bounds__(kBlockThreads, RTX_MIN_WAVES_PER_EU) rtx_render_kernel(const DevScene S, const FrameArgs F) {
-    __shared__ uint4 stkE[kBlockThreads / 64][kStackDepth];
-    __shared__ unsigned long long stkT[COUNT ? kBlockThreads / 64 : 1][kStackDepth];
+// DEEP: the variant for scenes whose BVH is kStackDepth or more levels deep (a DFS stack of
+// kStackDepthDeep entries per wave in LDS; fewer waves fit a CU, so it is used only then).
+template <bool COUNT, int PHASE, bool DEEP = false>
+__global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : RTX_MIN_WAVES_PER_EU) rtx_render_kernel(const DevScene S, const FrameArgs F) {
+    constexpr int kDepth = DEEP ? kStackDepthDeep : kStackDepth;
+    __shared__ uint4 stkE[kBlockThreads / 64][kDepth];
+    __shared__ unsigned long long stkT[COUNT ? kBlockThreads / 64 : 1][COUNT ? kDepth : 1];
     // per-lane shadow-ray plane numerators, shared by every light (see the light loop)
     __shared__ float pnumS[RTX_PNUM_CACHE ? kBlockThreads / 64 : 1][RTX_PNUM_CACHE ? kPlaneCache : 1][64];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -1090,6 +1093,8 @@ template __global__ void rtx_render_kernel<true, 0>(const DevScene, const FrameA
 template __global__ void rtx_render_kernel<false, 1>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 2>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 3>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 0, true>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<true, 0, true>(const DevScene, const FrameArgs);
 
 // Next frames' dispatch order from this frame's per-tile cost: heaviest first, STABLE
 // within a cost class so that tiles rendered together stay spatial neighbours (they walk
@@ -1315,6 +1320,7 @@ struct rtx_ctx {
     uint32_t split_permille = kSplitPermille;   // RTX_SPLIT_FACTOR (tuning)
     uint32_t split_parts = kPartsPerMesh;            // RTX_SPLIT_PARTS (tuning)
     bool split_ok = false;           // the uploaded scene admits split rendering
+    bool deep_stack = false;         // the uploaded scene needs rtx_render_kernel<..., DEEP = true>
     unsigned long long* d_hit_key = nullptr;
     uint32_t* d_occ = nullptr;
     rtx_render_params last{};
@@ -1342,25 +1348,32 @@ inline float bitsi(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
 inline int32_t bitsi_f(float f) { int32_t i; std::memcpy(&i, &f, 4); return i; }
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Deepest DFS stack a wave can need for this BVH (pending right siblings on a path).
-bool bvh_depth_ok(const rtx_mesh& m, std::string& why) {
+// Deepest DFS stack a wave can need for this BVH (pending right siblings on a path): at
+// most the depth of the deepest node, returned in `depth`.  RTX_E_INVALID for a malformed
+// tree, RTX_E_UNSUPPORTED for one deeper than the deep-stack variant handles.
+int bvh_depth_check(const rtx_mesh& m, std::string& why, int& depth) {
     std::vector<std::pair<uint32_t, int>> st{{0u, 0}};
     int maxd = 0;
     size_t visited = 0;
     while (!st.empty()) {
         auto [n, d] = st.back();
         st.pop_back();
-        if (++visited > 4ull * m.n_nodes + 4) { why = "BVH has a cycle"; return false; }
+        if (++visited > 4ull * m.n_nodes + 4) { why = "BVH has a cycle"; return RTX_E_INVALID; }
         maxd = d > maxd ? d : maxd;
         const rtx_bvh_node& nd = m.nodes[n];
         if (nd.idx_count == 0) {
-            if (nd.left_node + 1 >= m.n_nodes || nd.left_node == 0) { why = "BVH child index out of range"; return false; }
+            if (nd.left_node + 1 >= m.n_nodes || nd.left_node == 0) { why = "BVH child index out of range"; return RTX_E_INVALID; }
             st.push_back({nd.left_node + 1, d + 1});
             st.push_back({nd.left_node, d + 1});
         }
     }
-    if (maxd >= kStackDepth) { why = "BVH deeper than the device stack (" + std::to_string(maxd) + ")"; return false; }
-    return true;
+    depth = maxd;
+    if (maxd >= kStackDepthDeep) {
+        why = "BVH deeper than the deep-variant device stack (" + std::to_string(maxd) + " >= " +
+              std::to_string(kStackDepthDeep) + " levels)";
+        return RTX_E_UNSUPPORTED;
+    }
+    return RTX_OK;
 }
 
 // Frontier of one re-laid-out mesh BVH for split rendering: start from the root and split
@@ -1545,6 +1558,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     std::vector<int4> meshes, parts;
     bool split_ok = s->n_lights <= static_cast<uint32_t>(kMaxSplitLights);
     double max_ee = 0.0;   // max |e1| * |e2| over the triangles (DevScene::tri_fast)
+    int max_depth = 0;     // deepest BVH node over the meshes (stack variant)
     for (uint32_t i = 0; i < s->n_spheres; ++i) {
         const rtx_sphere& p = s->spheres[i];
         if (p.material >= nm) return fail(c, RTX_E_INVALID, "sphere material out of range");
@@ -1589,7 +1603,10 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
         if (m.n_nodes) {
             if (!m.nodes) return fail(c, RTX_E_INVALID, "mesh nodes missing");
             std::string why;
-            if (!bvh_depth_ok(m, why)) return fail(c, RTX_E_INVALID, why);
+            int depth = 0;
+            const int drc = bvh_depth_check(m, why, depth);
+            if (drc != RTX_OK) return fail(c, drc, why);
+            max_depth = std::max(max_depth, depth);
             // Re-lay the tree out for the device: the root at an odd slot, every child pair
             // (left, left + 1) at an even slot so one 64-B scalar load fetches both boxes.
             // Only the numbering changes; the tree and the left-then-right order do not.
@@ -1732,7 +1749,9 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     d.oct_bytes = (RTX_OCTANT && oct_ok && !std::getenv("RTX_NO_OCTANT")) ? static_cast<uint32_t>(node_bytes) : 0u;
     d.n_tris = static_cast<uint32_t>(tri.size() / 4); d.n_nodes = static_cast<uint32_t>(nodes.size() / 2);
     c->dev = d;
-    c->split_ok = split_ok && !parts.empty();
+    // a BVH kStackDepth or more levels deep renders with the deep-stack variant, unsplit
+    c->deep_stack = max_depth >= kStackDepth;
+    c->split_ok = split_ok && !parts.empty() && !c->deep_stack;
     c->has_scene = true;
     ++c->scene_gen;
     c->scene_sig = std::to_string(d.n_spheres) + "/" + std::to_string(d.n_planes) + "/" + std::to_string(d.n_meshes) +
@@ -1872,7 +1891,10 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         G.order = nullptr;
         G.cost = nullptr;
         G.heavy_flag = nullptr;
-        hipLaunchKernelGGL((rtx_render_kernel<true, 0>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, G);
+        if (c->deep_stack)
+            hipLaunchKernelGGL((rtx_render_kernel<true, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, G);
+        else
+            hipLaunchKernelGGL((rtx_render_kernel<true, 0>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, G);
         HIP_TRY(c, hipGetLastError());
         return RTX_OK;
     }
@@ -1895,7 +1917,10 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(c->ev_join, s2));
     }
-    hipLaunchKernelGGL((rtx_render_kernel<false, 0>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
+    if (c->deep_stack)
+        hipLaunchKernelGGL((rtx_render_kernel<false, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
+    else
+        hipLaunchKernelGGL((rtx_render_kernel<false, 0>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
     HIP_TRY(c, hipGetLastError());
     if (F.heavy_flag) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     if (F.cost) {

@@ -9,6 +9,9 @@ namespace rtxd {
 // Per-wave DFS stack entries in LDS (node index + 64-bit lane mask).  The host checks
 // every uploaded BVH's depth against this before accepting the scene.
 constexpr int kStackDepth = 64;
+// Deep-stack variant (BVH kStackDepth..kStackDepthDeep-1 levels deep): 16 KB of LDS per
+// wave for the stack; deeper trees are refused at upload with RTX_E_UNSUPPORTED.
+constexpr int kStackDepthDeep = 1024;
 #ifndef RTX_BLOCK_THREADS
 #define RTX_BLOCK_THREADS 64
 #endif

@@ -2,7 +2,8 @@
 rejected by rtx_upload_scene with RTX_E_INVALID and a reason in rtx_last_error, the context
 stays usable (the previous scene keeps rendering), and calls out of order are state errors.
 The BVH checks guard the kernel: an out-of-range child or a cycle would walk off the node
-array, a tree deeper than the LDS stack would overflow it (rtx_hip.hip bvh_depth_ok)."""
+array, a tree deeper than the deep-variant LDS stack would overflow it (rtx_hip.hip
+bvh_depth_check: RTX_E_UNSUPPORTED)."""
 import ctypes as C
 
 import numpy as np
@@ -86,22 +87,28 @@ def test_bad_bvh_links_are_rejected(ctx, nodes, why):
     assert why in _reason(ctx)
 
 
-def test_bvh_deeper_than_the_device_stack_is_rejected(ctx):
+def _chain(depth):
     # a chain: inner node 2k has children 2k+1 (a leaf) and 2k+2 (the next inner node, a leaf
-    # at the bottom), so the pending-sibling depth grows by one per level: 70 > the 64-entry
-    # LDS stack
-    depth = 70
+    # at the bottom), so the pending-sibling depth grows by one per level
     nodes = []
     for _ in range(depth):
         nodes.append((0, 0, len(nodes) + 1))   # inner at 2k: children 2k+1, 2k+2
         nodes.append((0, 3, 0))                # leaf at 2k+1
     nodes.append((0, 3, 0))                    # bottom leaf
-    assert _upload_rc(ctx, _scene(nodes)) == abi.RTX_E_INVALID
-    assert "deeper than the device stack" in _reason(ctx)
-    # a 60-level chain (inside the limit) uploads
-    nodes = nodes[2 * (depth - 60):]
-    nodes = [(f, c, (l - 2 * (depth - 60)) if c == 0 else 0) for f, c, l in nodes]
-    assert _upload_rc(ctx, _scene(nodes)) == abi.RTX_OK, _reason(ctx)
+    return nodes
+
+
+def test_bvh_deeper_than_the_default_stack_uses_the_deep_variant(ctx):
+    # 70 levels > the 64-entry LDS stack: accepted (deep-stack kernel; rendering parity in
+    # tests/test_gpu_deep_bvh.py)
+    assert _upload_rc(ctx, _scene(_chain(70))) == abi.RTX_OK
+
+
+def test_bvh_deeper_than_the_deep_stack_is_refused(ctx):
+    assert _upload_rc(ctx, _scene(_chain(1030))) == abi.RTX_E_UNSUPPORTED
+    assert "deeper than the deep-variant device stack" in _reason(ctx)
+    # a 60-level chain (the default stack) uploads
+    assert _upload_rc(ctx, _scene(_chain(60))) == abi.RTX_OK, _reason(ctx)
 
 
 @pytest.mark.parametrize("kw,why", [

@@ -14,7 +14,9 @@ import subprocess
 import pytest
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-KERNEL = "_Z17rtx_render_kernelILb0ELi0EEvN4rtxd8DevSceneENS0_9FrameArgsE"
+# product variants of the PHASE-0 render kernel (COUNT = false, default-depth stack)
+PRODUCT = "_Z17rtx_render_kernelILb0ELi0ELb0E"
+DEEP = "_Z17rtx_render_kernelILb0ELi0ELb1E"
 
 
 def _code_object(tmp_path, lib):
@@ -39,31 +41,41 @@ def isa(tmp_path_factory):
                          capture_output=True, text=True).stdout
     notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", str(co)], check=True, capture_output=True,
                            text=True).stdout
-    start = dis.index(f"<{KERNEL}>:")
-    body = dis[start:dis.index("s_endpgm", start)]
-    meta = {}
-    for block in notes.split("  - .")[1:]:
-        if re.search(rf"\.name:\s+{KERNEL}\b", block):
-            for key in ("vgpr_count", "sgpr_count", "private_segment_fixed_size"):
-                m = re.search(rf"\.{key}:\s+(\d+)", block)
-                if m:
-                    meta[key] = int(m.group(1))
-    return body, meta
+    out = {}
+    for m in re.finditer(r"^[0-9a-f]+ <(_Z17rtx_render_kernel\w+)>:", dis, re.M):
+        name = m.group(1)
+        body = dis[m.end():dis.index("s_endpgm", m.end())]
+        meta = {}
+        for block in notes.split("  - .")[1:]:
+            if re.search(rf"\.name:\s+{name}\b", block):
+                for key in ("vgpr_count", "sgpr_count", "private_segment_fixed_size"):
+                    mm = re.search(rf"\.{key}:\s+(\d+)", block)
+                    if mm:
+                        meta[key] = int(mm.group(1))
+        out[name] = (body, meta)
+    assert any(n.startswith(PRODUCT) for n in out), sorted(out)
+    return out
+
+
+def _product(isa):
+    return [(n, b, m) for n, (b, m) in isa.items() if n.startswith(PRODUCT)]
 
 
 def test_uniform_records_are_scalar_loads(isa):
-    body, _ = isa
-    # node pairs + triangles, closest-hit and any-hit, fast and exact slab variants
-    assert body.count("s_load_dwordx16") >= 8, "64-byte BVH/triangle records are no longer scalar loads"
+    for name, body, _ in _product(isa):
+        # node pairs + triangles, closest-hit and any-hit, fast and exact slab variants
+        assert body.count("s_load_dwordx16") >= 8, f"{name}: 64-byte BVH/triangle records are no longer scalar loads"
 
 
 def test_vector_loads_only_for_per_lane_gathers(isa):
-    body, _ = isa
-    n = len(re.findall(r"\bglobal_load_", body))
-    assert n <= 20, f"{n} vector loads in the render kernel: scene reads fell back to per-lane loads"
+    for name, body, _ in _product(isa):
+        n = len(re.findall(r"\bglobal_load_", body))
+        assert n <= 20, f"{name}: {n} vector loads in the render kernel: scene reads fell back to per-lane loads"
 
 
 def test_registers_and_scratch(isa):
-    _, meta = isa
-    assert meta.get("private_segment_fixed_size") == 0, meta
-    assert meta.get("vgpr_count", 999) <= 72, meta
+    for name, _, meta in _product(isa):
+        assert meta.get("private_segment_fixed_size") == 0, (name, meta)
+        assert meta.get("vgpr_count", 999) <= 72, (name, meta)
+    deep = [(n, m) for n, (_, m) in isa.items() if n.startswith(DEEP)]
+    assert deep and all(m.get("private_segment_fixed_size") == 0 for _, m in deep), deep
