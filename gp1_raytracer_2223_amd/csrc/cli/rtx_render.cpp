@@ -3,13 +3,14 @@
 // C-ABI of librtx_hip.so and writes RayTracing_Buffer.bmp like the reference's X key.
 //
 //   rtx_render <scene> [width height] [--time T] [--mode 0..3] [--no-shadows]
-//              [--frames N] [--out file.bmp] [--assets dir] [--benchmark [windows]]
+//              [--frames N] [--out file.bmp] [--assets dir] [--benchmark [windows]] [--inflight F]
 //
 // --benchmark runs the reference's frame loop (main.cpp:86-100: Scene::Update with the
 // timer's total time, Render into the host pixel buffer, Timer::Update) under its F6
 // benchmark (Timer.cpp:44-131): `windows` one-second dFPS windows (default 10), then
 // ">> HIGH/LOW/AVG" on stdout and benchmark.txt in the reference's format.  Animated
 // scenes are re-uploaded after every Update; the per-stage means are printed as well.
+// --inflight F (default 2) overlaps F frames (run_benchmark); 1 = the serial loop.
 #include <algorithm>
 #include <cfloat>
 #include <chrono>
@@ -56,45 +57,102 @@ struct Benchmark {
     }
 };
 
-int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows) {
+// The reference's frame loop is serial: Update, Render (into the window surface), present.
+// Here `inflight` frames overlap: frame k is updated, uploaded and queued (render + D2H into
+// its own page-locked host frame) on context k % inflight while frame k - 1 still runs on
+// another context's stream, so the host's Update / BVH rebuild of the next frame hides
+// behind the current frame's GPU work.  Every frame is still fully rendered and in host
+// memory before it counts: the benchmark ticks when frame k's context has finished.
+// inflight = 1 is the reference's serial loop.
+// With `seq` (--sequence t1,t2,...): no timer; frame k is Update(seq[k]) and is written to
+// `<stem>_<k>.bmp` when it completes (the pipelined loop's frames, checked by the tests).
+int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int inflight,
+                  const std::vector<float>* seq = nullptr, const std::string& stem = "") {
     const bool animated = rtx_host_scene_animated(hs) == 1;
+    const size_t npx = static_cast<size_t>(r.Width()) * r.Height();
+    std::vector<rtx_ctx*> ctx{r.Context()};
+    for (int f = 1; f < inflight; ++f) {
+        rtx_ctx* c = nullptr;
+        if (rtx_create(&c, 0) != RTX_OK) {
+            std::fprintf(stderr, "rtx_create: %s\n", rtx_last_error(nullptr));
+            for (size_t i = 1; i < ctx.size(); ++i) rtx_destroy(ctx[i]);
+            return 1;
+        }
+        ctx.push_back(c);
+    }
+    std::vector<std::vector<uint32_t>> buf(inflight, std::vector<uint32_t>(npx));
+    for (int f = 0; f < inflight; ++f) rtx_host_register(ctx[f], buf[f].data(), npx * 4);   // async D2H
+    const rtx_render_params p = r.Params();
     Benchmark b(windows);
-    std::cout << "**BENCHMARK STARTED**\n";
-    double t_update = 0, t_upload = 0, t_render = 0;
-    long frames = 0;
+    if (!seq) std::cout << "**BENCHMARK STARTED**\n";
+    double t_update = 0, t_upload = 0, t_queue = 0, t_wait = 0;
+    long frames = 0, queued = 0;
+    int rc = 0, last = -1;
     const Clock::time_point start = Clock::now();
     Clock::time_point prev = start;
     rtx_scene s;
     rtx_camera cam;
+    auto ok = [&](int code, const char* what, rtx_ctx* c) {
+        if (code == RTX_OK) return true;
+        std::fprintf(stderr, "%s: %s\n", what, rtx_last_error(c));
+        rc = 1;
+        return false;
+    };
     for (;;) {
+        const int f = static_cast<int>(queued % inflight);
+        if (queued >= inflight) {   // frame queued - inflight (this context's) completes
+            const Clock::time_point w0 = Clock::now();
+            if (!ok(rtx_synchronize(ctx[f]), "rtx_synchronize", ctx[f])) break;
+            const Clock::time_point w1 = Clock::now();
+            t_wait += secs(w0, w1);
+            ++frames;
+            last = f;
+            const float elapsed = static_cast<float>(secs(prev, w1));                  // Timer::Update
+            prev = w1;
+            if (seq) {
+                r.Pixels() = buf[f];
+                if (!r.SaveBufferToImage(stem + "_" + std::to_string(frames - 1) + ".bmp")) { rc = 1; break; }
+                if (frames == static_cast<long>(seq->size())) break;
+            } else if (b.Tick(elapsed)) {
+                break;
+            }
+        }
+        if (seq && queued >= static_cast<long>(seq->size())) {   // drain: nothing left to queue
+            ++queued;
+            continue;
+        }
         const Clock::time_point f0 = Clock::now();
-        if (animated) rtx_host_scene_update(hs, static_cast<float>(secs(start, f0)));   // Scene::Update(pTimer)
+        if (animated) rtx_host_scene_update(hs, seq ? (*seq)[queued] : static_cast<float>(secs(start, f0)));  // Scene::Update
         const Clock::time_point f1 = Clock::now();
-        if (rtx_host_scene_view(hs, &s, &cam) != RTX_OK) return 1;
-        if (animated || frames == 0) r.Upload(s);
+        if (!ok(rtx_host_scene_view(hs, &s, &cam), "rtx_host_scene_view", nullptr)) break;
+        if ((animated || queued < inflight) && !ok(rtx_upload_scene(ctx[f], &s), "rtx_upload_scene", ctx[f])) break;
         const Clock::time_point f2 = Clock::now();
-        r.Render(cam);                                                                  // Renderer::Render
+        if (!ok(rtx_render_async(ctx[f], &cam, &p, 0), "rtx_render_async", ctx[f])) break;  // Renderer::Render
+        if (!ok(rtx_gather_async(ctx[f], buf[f].data(), nullptr), "rtx_gather_async", ctx[f])) break;
         const Clock::time_point f3 = Clock::now();
         t_update += secs(f0, f1);
         t_upload += secs(f1, f2);
-        t_render += secs(f2, f3);
-        ++frames;
-        const float elapsed = static_cast<float>(secs(prev, f3));                      // Timer::Update
-        prev = f3;
-        if (b.Tick(elapsed)) break;
+        t_queue += secs(f2, f3);
+        ++queued;
     }
+    for (int f = 0; f < inflight; ++f) rtx_synchronize(ctx[f]);
+    if (last >= 0) r.Pixels() = buf[last];   // the last completed frame (SaveBufferToImage)
+    for (int f = 0; f < inflight; ++f) rtx_host_unregister(ctx[f], buf[f].data());
+    for (size_t i = 1; i < ctx.size(); ++i) rtx_destroy(ctx[i]);
+    if (rc || seq) return rc;
     std::cout << "**BENCHMARK FINISHED**\n";
     std::cout << ">> HIGH = " << b.high << std::endl;
     std::cout << ">> LOW = " << b.low << std::endl;
     std::cout << ">> AVG = " << b.avg << std::endl;
-    std::ofstream f("benchmark.txt");
-    f << "FRAMES = " << b.dfps.size() << std::endl;
-    f << "HIGH = " << b.high << std::endl;
-    f << "LOW = " << b.low << std::endl;
-    f << "AVG = " << b.avg << std::endl;
-    std::printf("frames %ld%s: update %.3f ms, upload %.3f ms, render+D2H %.3f ms per frame\n", frames,
-                animated ? " (animated)" : "", t_update / frames * 1e3, t_upload / frames * 1e3,
-                t_render / frames * 1e3);
+    std::ofstream out("benchmark.txt");
+    out << "FRAMES = " << b.dfps.size() << std::endl;
+    out << "HIGH = " << b.high << std::endl;
+    out << "LOW = " << b.low << std::endl;
+    out << "AVG = " << b.avg << std::endl;
+    const double n = static_cast<double>(queued);
+    std::printf("frames %ld%s, %d in flight: per frame update %.3f ms, upload %.3f ms, queue %.3f ms, "
+                "wait for GPU %.3f ms\n", frames, animated ? " (animated)" : "", inflight, t_update / n * 1e3,
+                t_upload / n * 1e3, t_queue / n * 1e3, t_wait / std::max(1.0, double(frames)) * 1e3);
     return 0;
 }
 
@@ -103,11 +161,12 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows) {
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s <scene> [width height] [--time T] [--mode M] [--no-shadows] [--frames N] "
-                             "[--out f.bmp] [--assets dir] [--benchmark [windows]]\n", argv[0]);
+                             "[--out f.bmp] [--assets dir] [--benchmark [windows]] [--inflight F]\n", argv[0]);
         return 2;
     }
     std::string scene = argv[1], out = "RayTracing_Buffer.bmp", assets;
-    int W = 640, H = 480, mode = 3, frames = 1, bench = 0;
+    int W = 640, H = 480, mode = 3, frames = 1, bench = 0, inflight = 2;
+    std::vector<float> seq;
     float t = -1.f;
     bool shadows = true;
     int pos = 0;
@@ -117,6 +176,15 @@ int main(int argc, char** argv) {
         else if (a == "--mode" && i + 1 < argc) mode = std::atoi(argv[++i]);
         else if (a == "--no-shadows") shadows = false;
         else if (a == "--frames" && i + 1 < argc) frames = std::atoi(argv[++i]);
+        else if (a == "--sequence" && i + 1 < argc) {
+            for (const char* q = argv[++i]; *q;) {
+                char* e = nullptr;
+                seq.push_back(std::strtof(q, &e));
+                q = (*e == ',') ? e + 1 : e;
+                if (e == q && *q) break;
+            }
+        }
+        else if (a == "--inflight" && i + 1 < argc) inflight = std::max(1, std::min(8, std::atoi(argv[++i])));
         else if (a == "--out" && i + 1 < argc) out = argv[++i];
         else if (a == "--assets" && i + 1 < argc) assets = argv[++i];
         else if (a == "--benchmark") bench = (i + 1 < argc && std::atoi(argv[i + 1]) > 0) ? std::atoi(argv[++i]) : 10;
@@ -135,8 +203,16 @@ int main(int argc, char** argv) {
         rtx::Renderer r(W, H);
         r.m_CurrentLightingMode = static_cast<rtx::Renderer::LightingMode>(mode);
         r.m_ShadowsEnabled = shadows;
+        if (!seq.empty()) {
+            // --sequence t1,...: the pipelined frame loop over fixed Update times, frame k
+            // written to <out stem>_<k>.bmp
+            const std::string stem = out.size() > 4 && out.substr(out.size() - 4) == ".bmp" ? out.substr(0, out.size() - 4) : out;
+            rc = run_benchmark(r, hs, 0, inflight, &seq, stem);
+            rtx_host_scene_destroy(hs);
+            return rc;
+        }
         if (bench) {
-            rc = run_benchmark(r, hs, bench);
+            rc = run_benchmark(r, hs, bench, inflight);
         } else {
             r.Render(hs, true);
             auto t0 = Clock::now();

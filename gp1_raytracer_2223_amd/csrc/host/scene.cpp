@@ -7,8 +7,15 @@
 #include <cstring>
 #include <fstream>
 #include <random>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <utility>
+
+#include <emmintrin.h>
 
 namespace rtx {
 
@@ -51,8 +58,318 @@ void TriangleMesh::UpdateTransforms() {
     BuildBVH();
 }
 
+namespace {
+
+// RTX_HOST_BVH=direct: the direct restatement (BuildBVHDirect) instead of the fast builder.
+bool UseDirectBuilder() {
+    static const bool direct = [] {
+        const char* e = std::getenv("RTX_HOST_BVH");
+        return e && std::strcmp(e, "direct") == 0;
+    }();
+    return direct;
+}
+
+// Subtree tasks of the fast builder.  A small process-wide pool (at most 8 workers, or
+// RTX_HOST_THREADS) that sleeps between builds; a thread waiting for its task helps by
+// running queued tasks, so nesting cannot deadlock.
+class BuildPool {
+public:
+    struct Task {
+        std::function<void()> fn;
+        std::atomic<bool> done{false};
+    };
+    static BuildPool& Get() {
+        static BuildPool* pool = new BuildPool();   // never destroyed: workers may outlive main's statics
+        return *pool;
+    }
+    int Workers() const { return static_cast<int>(threads_.size()); }
+    void Submit(Task* t) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(t);
+            queued_.fetch_add(1, std::memory_order_release);
+        }
+        if (sleeping_.load(std::memory_order_acquire)) cv_.notify_one();
+    }
+    void Wait(Task* t) {
+        while (!t->done.load(std::memory_order_acquire))
+            if (!RunOne()) std::this_thread::yield();
+    }
+
+private:
+    BuildPool() {
+        unsigned n = std::thread::hardware_concurrency();
+        if (const char* e = std::getenv("RTX_HOST_THREADS")) n = static_cast<unsigned>(std::atoi(e));
+        n = n > 8 ? 8 : n;
+        for (unsigned k = 1; k < n; ++k) threads_.emplace_back([this] { Loop(); });
+        for (auto& th : threads_) th.detach();
+    }
+    bool RunOne() {
+        Task* t = nullptr;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            if (q_.empty()) return false;
+            t = q_.front();
+            q_.pop_front();
+            queued_.fetch_sub(1, std::memory_order_relaxed);
+        }
+        t->fn();
+        t->done.store(true, std::memory_order_release);
+        return true;
+    }
+    // Workers spin a while on the queue counter before sleeping: during a build the next
+    // subtree task is picked up within a microsecond instead of a futex wake-up.
+    void Loop() {
+        for (;;) {
+            for (int spin = 0; spin < kSpin; ++spin) {
+                if (queued_.load(std::memory_order_acquire) > 0 && RunOne()) spin = 0;
+                else _mm_pause();
+            }
+            std::unique_lock<std::mutex> g(mu_);
+            sleeping_.fetch_add(1, std::memory_order_acq_rel);
+            cv_.wait(g, [this] { return !q_.empty(); });
+            sleeping_.fetch_sub(1, std::memory_order_acq_rel);
+        }
+    }
+    static constexpr int kSpin = 1 << 16;   // ~1-2 ms of _mm_pause
+    std::atomic<int> queued_{0}, sleeping_{0};
+    std::vector<std::thread> threads_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Task*> q_;
+};
+
+// std::min(a, b) = (b < a) ? b : a = minps(b, a) per lane; std::max(a, b) = maxps(b, a).
+inline __m128 MinRef(__m128 a, __m128 b) { return _mm_min_ps(b, a); }
+inline __m128 MaxRef(__m128 a, __m128 b) { return _mm_max_ps(b, a); }
+// AABB::Area (e.x * e.y + e.y * e.z + e.z * e.x, summed left to right), e = hi - lo
+inline float Area(__m128 lo, __m128 hi) {
+    const __m128 e = _mm_sub_ps(hi, lo);
+    const __m128 p = _mm_mul_ps(e, _mm_shuffle_ps(e, e, _MM_SHUFFLE(3, 0, 2, 1)));   // (xy, yz, zx, ww)
+    const float xy = _mm_cvtss_f32(p), yz = _mm_cvtss_f32(_mm_shuffle_ps(p, p, 1)),
+                zx = _mm_cvtss_f32(_mm_shuffle_ps(p, p, 2));
+    return xy + yz + zx;
+}
+inline Vec3 ToVec3(__m128 v) {
+    alignas(16) float f[4];
+    _mm_store_ps(f, v);
+    return {f[0], f[1], f[2]};
+}
+
+}  // namespace
+
 void TriangleMesh::BuildBVH() {
     if (nodes.empty() || indices.empty()) return;   // reference: UB / crash (see Scene_W4_TestScene)
+    if (!UseDirectBuilder() && BuildBVHFast()) return;
+    BuildBVHDirect();
+}
+
+// The fast builder takes the same decisions as BuildBVHDirect:
+//  * min/max keep the reference's std::min/std::max semantics lane by lane (MinRef/MaxRef),
+//    and a triangle's box min(min(v0, v1), v2) grows a node or bin exactly as its three
+//    vertices in order would (first-occurrence ties) — as long as no coordinate is NaN,
+//    so a mesh with a NaN position takes the direct path;
+//  * bin indices, costs and split positions are the same binary32 expressions;
+//  * the partition is the reference's swap loop on triangle units (i += 3 / j -= 3 become
+//    +-1), applied to (centroid, id) records; the id sequence IS the composed permutation.
+bool TriangleMesh::BuildBVHFast() {
+    const size_t ntri = indices.size() / 3;
+    pt_.resize(ntri);
+    box_.resize(ntri);
+    for (size_t k = 0; k < ntri; ++k) {
+        const Vec3& v0 = transformedPositions[indices[3 * k]];
+        const Vec3& v1 = transformedPositions[indices[3 * k + 1]];
+        const Vec3& v2 = transformedPositions[indices[3 * k + 2]];
+        if (v0.x != v0.x || v0.y != v0.y || v0.z != v0.z || v1.x != v1.x || v1.y != v1.y || v1.z != v1.z ||
+            v2.x != v2.x || v2.y != v2.y || v2.z != v2.z)
+            return false;
+        const Vec3 c = (v0 + v1 + v2) * 0.3333f;
+        pt_[k] = {{c.x, c.y, c.z}, static_cast<uint32_t>(k)};
+        const Vec3 lo = Vec3::Min(Vec3::Min(v0, v1), v2), hi = Vec3::Max(Vec3::Max(v0, v1), v2);
+        box_[k] = {{lo.x, lo.y, lo.z, 0.f}, {hi.x, hi.y, hi.z, 0.f}};
+    }
+    BVHNode& root = nodes[0];
+    root.leftNode = 0;
+    root.firstIdx = 0;
+    root.idxCount = static_cast<uint32_t>(indices.size());
+    nodesUsed = 1;
+    tmp_.resize(2 * ntri + 1);
+    tmpUsed_ = 1;
+    tmp_[0] = {0u, root.idxCount, {}, {}, -1, -1};
+    BoundsFast(tmp_[0]);
+    SubdivideFast(0);
+    root.minAABB = tmp_[0].mn;
+    root.maxAABB = tmp_[0].mx;
+    Emit(0, 0);
+    // apply the composed permutation: slot k now holds the triangle that was at pt_[k].id
+    scratchI_.assign(indices.begin(), indices.end());
+    scratchN_.assign(normals.begin(), normals.end());
+    scratchTN_.assign(transformedNormals.begin(), transformedNormals.end());
+    const bool hasN = normals.size() >= ntri, hasTN = transformedNormals.size() >= ntri;
+    for (size_t k = 0; k < ntri; ++k) {
+        const uint32_t id = pt_[k].id;
+        indices[3 * k] = scratchI_[3 * id];
+        indices[3 * k + 1] = scratchI_[3 * id + 1];
+        indices[3 * k + 2] = scratchI_[3 * id + 2];
+        if (hasN) normals[k] = scratchN_[id];
+        if (hasTN) transformedNormals[k] = scratchTN_[id];
+    }
+    return true;
+}
+
+void TriangleMesh::BoundsFast(TmpNode& n) const {
+    __m128 mn = _mm_set1_ps(FLT_MAX), mx = _mm_set1_ps(FLT_MIN);
+    for (uint32_t k = n.first / 3; k < (n.first + n.count) / 3; ++k) {
+        const TriBox& b = box_[pt_[k].id];
+        mn = MinRef(mn, _mm_load_ps(b.lo));
+        mx = MaxRef(mx, _mm_load_ps(b.hi));
+    }
+    n.mn = ToVec3(mn);
+    n.mx = ToVec3(mx);
+}
+
+void TriangleMesh::SubdivideFast(uint32_t t) {
+    TmpNode& n = tmp_[t];
+    if (n.count <= 8) return;
+    BVHNode view;
+    view.firstIdx = n.first;
+    view.idxCount = n.count;
+    view.minAABB = n.mn;
+    view.maxAABB = n.mx;
+    int axis = 0;
+    float splitPos = 0.f;
+    const float splitCost = FindBestSplitFast(view, axis, splitPos);
+    const float noSplitCost = CalculateNodeCost(view);
+    if (splitCost >= noSplitCost) return;
+
+    // the reference's partition (DataTypes.h:335-363) in triangle units
+    int i = static_cast<int>(n.first / 3);
+    int j = static_cast<int>((n.first + n.count) / 3) - 1;
+    while (i <= j) {
+        if (pt_[i].c[axis] < splitPos) {
+            ++i;
+        } else {
+            std::swap(pt_[i], pt_[j]);
+            --j;
+        }
+    }
+    const int leftCount = 3 * i - static_cast<int>(n.first);
+    if (leftCount == 0 || static_cast<uint32_t>(leftCount) == n.count) return;
+
+    const uint32_t L = __atomic_fetch_add(&tmpUsed_, 2u, __ATOMIC_RELAXED), R = L + 1;
+    tmp_[L] = {n.first, static_cast<uint32_t>(leftCount), {}, {}, -1, -1};
+    tmp_[R] = {static_cast<uint32_t>(3 * i), n.count - static_cast<uint32_t>(leftCount), {}, {}, -1, -1};
+    BoundsFast(tmp_[L]);
+    BoundsFast(tmp_[R]);
+    n.l = static_cast<int32_t>(L);
+    n.r = static_cast<int32_t>(R);
+    BuildPool& pool = BuildPool::Get();
+    if (pool.Workers() > 0 && tmp_[L].count >= 3 * 2048 && tmp_[R].count >= 3 * 2048) {
+        BuildPool::Task task;
+        task.fn = [this, L] { SubdivideFast(L); };
+        pool.Submit(&task);
+        SubdivideFast(R);
+        pool.Wait(&task);
+    } else {
+        SubdivideFast(L);
+        SubdivideFast(R);
+    }
+}
+
+// FindBestSplitPlane (DataTypes.h:378-456) over the (centroid, id) records: one SSE pass
+// for the three axes' centroid bounds, one for the three axes' bins.
+float TriangleMesh::FindBestSplitFast(const BVHNode& node, int& axis, float& splitPos) const {
+    float bestCost = FLT_MAX;
+    const uint32_t k0 = node.firstIdx / 3, k1 = (node.firstIdx + node.idxCount) / 3;
+    __m128 cmn = _mm_set1_ps(FLT_MAX), cmx = _mm_set1_ps(FLT_MIN);
+    for (uint32_t k = k0; k < k1; ++k) {
+        const __m128 c = _mm_load_ps(pt_[k].c);   // lane 3 (the id) is never read back
+        cmn = MinRef(cmn, c);
+        cmx = MaxRef(cmx, c);
+    }
+    alignas(16) float minB[4], maxB[4], scales[4];
+    _mm_store_ps(minB, cmn);
+    _mm_store_ps(maxB, cmx);
+    constexpr int kBins = 8, kPlanes = kBins - 1;
+    bool live[3];
+    for (int a = 0; a < 3; ++a) {
+        const float d = maxB[a] - minB[a];
+        live[a] = !(fabsf(d) < FLT_EPSILON);
+        scales[a] = live[a] ? kBins / d : 0.f;
+    }
+    scales[3] = 0.f;
+    __m128 blo[3][kBins], bhi[3][kBins];
+    uint32_t counts[3][kBins] = {};
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < kBins; ++b) { blo[a][b] = _mm_set1_ps(FLT_MAX); bhi[a][b] = _mm_set1_ps(FLT_MIN); }
+    const __m128 vmin = _mm_load_ps(minB), vscale = _mm_load_ps(scales);
+    const bool all_live = live[0] && live[1] && live[2];
+    for (uint32_t k = k0; k < k1; ++k) {
+        // (centroid[axis] - minBounds) * scale, truncated like static_cast<int>
+        alignas(16) int32_t bi[4];
+        _mm_store_si128(reinterpret_cast<__m128i*>(bi),
+                        _mm_cvttps_epi32(_mm_mul_ps(_mm_sub_ps(_mm_load_ps(pt_[k].c), vmin), vscale)));
+        const TriBox& tb = box_[pt_[k].id];
+        const __m128 lo = _mm_load_ps(tb.lo), hi = _mm_load_ps(tb.hi);
+        for (int a = 0; a < 3; ++a) {
+            if (!all_live && !live[a]) continue;
+            int b = bi[a];
+            if (kPlanes < b) b = kPlanes;   // std::min(amountOfPlaneBins, b)
+            if (b < 0) b = 0;               // NaN / out of int range: undefined in the reference
+            counts[a][b] += 3;
+            blo[a][b] = MinRef(blo[a][b], lo);
+            bhi[a][b] = MaxRef(bhi[a][b], hi);
+        }
+    }
+    for (int axisIdx = 0; axisIdx < 3; ++axisIdx) {
+        if (!live[axisIdx]) continue;
+        const float minBounds = minB[axisIdx];
+        const float boundsDifference = maxB[axisIdx] - minBounds;
+        const uint32_t* binCount = counts[axisIdx];
+        float leftArea[kPlanes], rightArea[kPlanes];
+        int leftCount[kPlanes], rightCount[kPlanes];
+        int leftSum = 0, rightSum = 0;
+        // AABB::Grow(bin) and AABB::Area (e.x*e.y + e.y*e.z + e.z*e.x, left to right) per lane
+        // An empty bin leaves the running box unchanged (its lo is FLT_MAX, and the running
+        // hi never drops below the FLT_MIN it starts from), so its area is carried over.
+        __m128 llo = _mm_set1_ps(FLT_MAX), lhi = _mm_set1_ps(FLT_MIN), rlo = llo, rhi = lhi;
+        const float empty = Area(llo, lhi);
+        float la = empty, ra = empty;
+        for (int i = 0; i < kPlanes; ++i) {
+            leftSum += binCount[i];
+            leftCount[i] = leftSum;
+            if (binCount[i]) {
+                llo = MinRef(llo, blo[axisIdx][i]);
+                lhi = MaxRef(lhi, bhi[axisIdx][i]);
+                la = Area(llo, lhi);
+            }
+            leftArea[i] = la;
+            rightSum += binCount[kPlanes - i];
+            rightCount[kPlanes - i - 1] = rightSum;
+            if (binCount[kPlanes - i]) {
+                rlo = MinRef(rlo, blo[axisIdx][kPlanes - i]);
+                rhi = MaxRef(rhi, bhi[axisIdx][kPlanes - i]);
+                ra = Area(rlo, rhi);
+            }
+            rightArea[kPlanes - i - 1] = ra;
+        }
+        const float scale = boundsDifference / kBins;
+        for (int i = 0; i < kPlanes; ++i) {
+            const float planeCost = static_cast<float>(leftCount[i]) * leftArea[i] +
+                                    static_cast<float>(rightCount[i]) * rightArea[i];
+            if (planeCost < bestCost) {
+                axis = axisIdx;
+                splitPos = minBounds + scale * static_cast<float>(i + 1);
+                bestCost = planeCost;
+            }
+        }
+    }
+    return bestCost;
+}
+
+// Direct restatement: the reference's passes on a per-triangle cache (kept as the
+// checked fallback for meshes with NaN coordinates and as RTX_HOST_BVH=direct).
+void TriangleMesh::BuildBVHDirect() {
     BVHNode& root = nodes[0];
     root.leftNode = 0;
     root.firstIdx = 0;

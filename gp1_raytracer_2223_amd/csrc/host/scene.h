@@ -82,6 +82,22 @@ private:
     // could depend on the grouping, and no SAH cost can observe that).
     struct TriCache { Vec3 c, v0, v1, v2, lo, hi; };
     std::vector<TriCache> tc_;
+    void BuildBVHDirect();
+
+    // Fast builder (the default; RTX_HOST_BVH=direct selects the one above): the same
+    // split decisions from SSE passes over a compact (centroid, triangle id) array that the
+    // partition permutes in place; the composed permutation is applied to indices, normals
+    // and transformedNormals once at the end, and large subtrees run on a thread pool.
+    struct alignas(16) PTri { float c[3]; uint32_t id; };
+    struct alignas(16) TriBox { float lo[4], hi[4]; };
+    std::vector<PTri> pt_;
+    std::vector<TriBox> box_;
+    std::vector<int32_t> scratchI_;
+    std::vector<Vec3> scratchN_, scratchTN_;
+    bool BuildBVHFast();
+    void BoundsFast(TmpNode& n) const;
+    void SubdivideFast(uint32_t t);
+    float FindBestSplitFast(const BVHNode& node, int& axis, float& splitPos) const;
 };
 
 // dae::Camera (source/Camera.h): the ray-generation state only (Update is input).

@@ -1556,6 +1556,12 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     std::vector<float4> sph, pl, tri, nodes, lights, mats;
     std::vector<uint32_t> sph_mat;
     std::vector<int4> meshes, parts;
+    {
+        size_t nt = 0, nn = 0;
+        for (uint32_t mi = 0; mi < s->n_meshes; ++mi) { nt += s->meshes[mi].n_indices / 3; nn += s->meshes[mi].n_nodes; }
+        tri.reserve(4 * nt);
+        nodes.reserve(2 * nn + 4 * s->n_meshes + 4);
+    }
     bool split_ok = s->n_lights <= static_cast<uint32_t>(kMaxSplitLights);
     double max_ee = 0.0;   // max |e1| * |e2| over the triangles (DevScene::tri_fast)
     int max_depth = 0;     // deepest BVH node over the meshes (stack variant)
@@ -1666,21 +1672,9 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     bool oct_ok = !nodes.empty() && node_bytes <= kOctantMaxNodeBytes && 8 * node_bytes < (1ull << 32);
     for (size_t n = 0; oct_ok && n < nodes.size(); n += 2)
         oct_ok = nodes[n].x <= nodes[n].y && nodes[n].z <= nodes[n].w && nodes[n + 1].x <= nodes[n + 1].y;
-    std::vector<float4> node_img;
-    if (oct_ok) {
-        node_img.assign(8 * node_bytes / 16, f4(0, 0, 0, 0));
-        for (int k = 0; k < 8; ++k) {
-            float4* dst = node_img.data() + k * (node_bytes / 16);
-            const bool mx = k & 1, my = k & 2, mz = k & 4;
-            for (size_t n = 0; n < nodes.size(); n += 2) {
-                const float4 a = nodes[n], b = nodes[n + 1];
-                dst[n] = f4(mx ? a.y : a.x, mx ? a.x : a.y, my ? a.w : a.z, my ? a.z : a.w);
-                dst[n + 1] = f4(mz ? b.y : b.x, mz ? b.x : b.y, b.z, b.w);
-            }
-        }
-    } else {
-        node_img = nodes;
-    }
+    // the node section: 8 octant copies (node_bytes apart, written straight into the
+    // staging image below) or the one array
+    const size_t node_sec = oct_ok ? 8 * node_bytes : nodes.size() * 16;
     for (uint32_t i = 0; i < s->n_lights; ++i) {
         const rtx_light& l = s->lights[i];
         lights.push_back(f4(l.origin[0], l.origin[1], l.origin[2], bitsi(l.type)));
@@ -1698,7 +1692,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     struct Sec { const void* p; size_t n; size_t off; };
     Sec secs[] = {{sph.data(), sph.size() * 16, 0},       {sph_mat.data(), sph_mat.size() * 4, 0},
                   {pl.data(), pl.size() * 16, 0},         {tri.data(), tri.size() * 16, 0},
-                  {node_img.data(), node_img.size() * 16, 0},
+                  {nullptr, node_sec, 0},
                   {meshes.data(), meshes.size() * 16, 0}, {lights.data(), lights.size() * 16, 0},
                   {mats.data(), mats.size() * 16, 0},     {parts.data(), parts.size() * 16, 0}};
     size_t total = 0;
@@ -1720,9 +1714,28 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
         HIP_TRY(c, hipHostMalloc(&B.h, total));
         B.cap = total;
     }
-    std::memset(B.h, 0, total);
-    for (auto& x : secs)
-        if (x.n) std::memcpy(B.h + x.off, x.p, x.n);
+    // sections in place; only the padding up to the next section is cleared (an upload per
+    // animated frame: no full-image memset, no intermediate node image)
+    for (size_t i = 0; i < sizeof secs / sizeof secs[0]; ++i) {
+        const Sec& x = secs[i];
+        const size_t end = i + 1 < sizeof secs / sizeof secs[0] ? secs[i + 1].off : total;
+        if (x.p && x.n) std::memcpy(B.h + x.off, x.p, x.n);
+        if (!x.p && x.n && oct_ok) {   // octant copy k stores (hi, lo) on the axes set in k
+            for (int k = 0; k < 8; ++k) {
+                float4* dst = reinterpret_cast<float4*>(B.h + x.off + k * node_bytes);
+                const bool mx = k & 1, my = k & 2, mz = k & 4;
+                for (size_t n = 0; n < nodes.size(); n += 2) {
+                    const float4 a = nodes[n], b = nodes[n + 1];
+                    dst[n] = f4(mx ? a.y : a.x, mx ? a.x : a.y, my ? a.w : a.z, my ? a.z : a.w);
+                    dst[n + 1] = f4(mz ? b.y : b.x, mz ? b.x : b.y, b.z, b.w);
+                }
+                std::memset(reinterpret_cast<char*>(dst + nodes.size()), 0, node_bytes - nodes.size() * 16);
+            }
+        } else if (!x.p && x.n) {
+            std::memcpy(B.h + x.off, nodes.data(), x.n);
+        }
+        std::memset(B.h + x.off + x.n, 0, end - x.off - x.n);
+    }
     HIP_TRY(c, hipMemcpyAsync(B.d, B.h, total, hipMemcpyHostToDevice, c->stream));
     if (c->sb_cur >= 0) {   // every frame queued so far reads the previous image
         rtx_ctx::SceneBuf& O = c->sb[c->sb_cur];

@@ -73,11 +73,14 @@ public:
     }
 
     const std::vector<uint32_t>& Pixels() const { return m_Pixels; }
+    std::vector<uint32_t>& Pixels() { return m_Pixels; }
+    int Width() const { return m_Width; }
+    int Height() const { return m_Height; }
     rtx_ctx* Context() const { return m_Ctx; }
     LightingMode m_CurrentLightingMode{LightingMode::Combined};
     bool m_ShadowsEnabled{true};
 
-private:
+    // The render parameters of the current state (Renderer::Render reads the same members).
     rtx_render_params Params() const {
         rtx_render_params p{};
         p.width = static_cast<uint32_t>(m_Width);
@@ -88,6 +91,7 @@ private:
         p.stripe_step = 1;
         return p;
     }
+private:
     void Check(int rc, const char* what) const {
         if (rc != RTX_OK) throw std::runtime_error(std::string(what) + ": " + rtx_last_error(m_Ctx));
     }

@@ -16,6 +16,8 @@
 //
 // Subcommands (all binary outputs use the RTXB container read by tests/golden/rtxb.py):
 //   scene  <name> <t|-1> <out>                      flattened scene after Initialize (+Update(t))
+//   scene  <name> <t1,t2,...> <out>                 ... after a sequence of Updates (the BVH
+//                                                   permutation carries over between builds)
 //   render <name> <t|-1> <W> <H> <mode> <shadows> <threads> <out>
 //   bench  <name> <t|-1> <W> <H> <threads> <frames> [mode shadows]   -> one JSON line
 //   obj    <path> <out>                             Utils::ParseOBJ result
@@ -260,10 +262,25 @@ static std::unique_ptr<Scene> make_scene(const std::string& name) {
     return s;
 }
 
+static void apply_update(Scene* s, const std::string& name, float t);
 // Scene_W4_*::Update without the SDL-driven camera part (Scene.cpp:391-400, 431-437,
 // 468-474): yaw = (cos(t)+1)/2 * 2pi applied to every animated mesh.
 static void apply_time(Scene* s, const std::string& name, float t) {
     if (t < 0.f) return;
+    apply_update(s, name, t);
+}
+static void apply_time(Scene* s, const std::string& name, const char* times) {
+    // "t" or a comma-separated sequence "t1,t2,...": one Update per entry, in order
+    std::string list(times);
+    size_t pos = 0;
+    for (;;) {
+        const size_t comma = list.find(',', pos);
+        apply_time(s, name, std::stof(list.substr(pos, comma - pos)));
+        if (comma == std::string::npos) break;
+        pos = comma + 1;
+    }
+}
+static void apply_update(Scene* s, const std::string& name, float t) {
     const auto yawAngle{(cosf(t) + 1.f) / 2.f * PI_2};
     if (name.rfind("file:", 0) == 0) {
         for (const auto m : static_cast<Scene_File*>(s)->m_Spin) { m->RotateY(yawAngle); m->UpdateTransforms(); }
@@ -587,13 +604,13 @@ int main(int argc, char** argv) {
     const std::string cmd = argv[1];
     if (cmd == "scene" && argc == 5) {
         auto s = make_scene(argv[2]);
-        apply_time(s.get(), argv[2], std::stof(argv[3]));
+        apply_time(s.get(), argv[2], argv[3]);
         dump_scene(s.get(), argv[4]);
         return 0;
     }
     if (cmd == "render" && argc == 10) {
         auto s = make_scene(argv[2]);
-        apply_time(s.get(), argv[2], std::stof(argv[3]));
+        apply_time(s.get(), argv[2], argv[3]);
         const int W = std::atoi(argv[4]), H = std::atoi(argv[5]);
         RenderState rs = make_state(W, H, std::atoi(argv[6]), std::atoi(argv[7]) != 0);
         std::vector<uint32_t> px(static_cast<size_t>(W) * H);
@@ -606,7 +623,7 @@ int main(int argc, char** argv) {
     }
     if (cmd == "bench" && (argc == 8 || argc == 10)) {
         auto s = make_scene(argv[2]);
-        apply_time(s.get(), argv[2], std::stof(argv[3]));
+        apply_time(s.get(), argv[2], argv[3]);
         const int W = std::atoi(argv[4]), H = std::atoi(argv[5]);
         const int threads = std::atoi(argv[6]), frames = std::atoi(argv[7]);
         const int mode = argc == 10 ? std::atoi(argv[8]) : 3;

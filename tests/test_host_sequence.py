@@ -1,0 +1,71 @@
+"""Animated frame loops on the host scene layer: after a SEQUENCE of Scene::Update calls
+the world geometry, the BVH node array and the triangle permutation still equal the
+reference's (tests/golden/seq_*.npz, made by tests/golden/make_seq_goldens.py from the
+reference built in place).  Each rebuild permutes the triangles in place
+(source/DataTypes.h:335-363), so build k depends on every earlier one; the single-Update
+goldens cannot see a divergence that appears only after several rebuilds.
+
+Both BVH builders are checked: the default fast one (SIMD passes over a permutation
+array, subtrees on a thread pool) and the direct restatement (RTX_HOST_BVH=direct)."""
+import hashlib
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+G = Path(__file__).resolve().parent / "golden"
+ROOT = G.parents[1]
+
+
+def _digest(m: dict) -> str:
+    links = m["node_links"].reshape(-1, 3).copy()
+    links[links[:, 1] != 0, 2] = 0   # a leaf's leftNode is stale in the reference
+    h = hashlib.sha256()
+    for a in (m["tpositions"], m["indices"], m["tnormals"], m["node_bounds"], links):
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def _scene_name(stem: str) -> str:
+    return "file:" + str(ROOT / "scenes" / (stem[5:] + ".rtxscene")) if stem.startswith("file_") else stem
+
+
+_CHILD = r"""
+import sys, json
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from gp1_raytracer_2223_amd.scene import HostScene
+name, times, checkpoints = sys.argv[2], json.loads(sys.argv[3]), json.loads(sys.argv[4])
+sys.path.insert(0, sys.argv[1] + '/tests')
+from test_host_sequence import _digest
+out = {}
+for n in checkpoints:
+    hs = HostScene(name)
+    for t in times[:n]:
+        hs.update(t)
+    out[str(n)] = [_digest(m) for m in hs.arrays()["meshes"]]
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("builder", ["fast", "direct"])
+@pytest.mark.parametrize("path", sorted(G.glob("seq_*.npz")), ids=lambda p: p.stem)
+def test_update_sequence_matches_reference(path, builder):
+    import json
+    g = np.load(path)
+    times = [float(t) for t in g["times"]]
+    cps = [int(c) for c in g["checkpoints"]]
+    env = dict(os.environ)
+    if builder == "direct":
+        env["RTX_HOST_BVH"] = "direct"
+    else:
+        env.pop("RTX_HOST_BVH", None)
+    # own process: the builder is chosen once per process (environment read at load)
+    r = subprocess.run([sys.executable, "-c", _CHILD, str(ROOT), _scene_name(path.stem[4:]), json.dumps(times),
+                        json.dumps(cps)], capture_output=True, text=True, env=env, check=True)
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    for n in cps:
+        assert got[str(n)] == [str(x) for x in g[f"after{n}"]], f"after {n} updates"
