@@ -7,20 +7,22 @@ state, Combined lighting, shadows on).
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-A step renders ONE frame of the scene (`--mode frame`, the default).  Its rows are cut
-into 16-row stripes dealt round robin over the N ranks (rank r owns stripe s iff
-s % N == r): the frame is tiled across the GPUs — strong scaling, the north
-star's "image tile-partitioned across the GPUs of one node".  At N = 1 a step is exactly
-one reference Renderer::Render frame.  (`--mode views`: the round-1 weak-scaling variant,
-N different camera views per step, one frame's worth of pixels per rank.)
+A step renders N views of the scene (`--mode views`, the default): view f is the reference
+camera moved 0.05 f along x, and every view's rows are cut into 16-row stripes dealt round
+robin over the N ranks (rank r owns view f's stripe s iff s % N == (r - f) mod N; SURVEY
+§8(e)), so every image is tiled across all the GPUs and every rank renders one frame's
+worth of pixels per step — weak scaling, the sharding rule for a path of independent
+pixels.  At N = 1 a step is exactly one reference Renderer::Render frame.  `--mode frame`
+tiles ONE frame per step over the N ranks (strong scaling: each rank renders 1/N of a
+frame, so at 8 GPUs a 1080p frame no longer fills a GPU).
 
 Two timed regions, each bracketed by barrier + stream sync and max-reduced over ranks:
-  1. `value`: K frames with inputs resident in HBM and the frame left in HBM (the
+  1. `value`: K steps with inputs resident in HBM and the frames left in HBM (the
      metric's device throughput);
-  2. `host_gather`: K frames each ALSO gathered into one page-locked host frame shared by
-     all ranks (/dev/shm mapping, hipHostRegister; every rank hipMemcpy2DAsync's only its
-     own stripes over its own PCIe link) — the north star's "independent tiles gathered
-     on host".  PCIe-inclusive, so never `value`.
+  2. `host_gather`: K steps whose frames are ALSO gathered into page-locked host frames
+     shared by all ranks (/dev/shm mapping, hipHostRegister; every rank hipMemcpy2DAsync's
+     only its own stripes over its own PCIe link) — the north star's "independent tiles
+     gathered on host".  PCIe-inclusive, so never `value`.
 No collective on the data path: the ranks' only exchange is a gloo barrier and the
 max-reduce of the timings.
 
@@ -288,7 +290,7 @@ def main() -> int:
     ap.add_argument("--scene", default="W4_Bunny")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--mode", choices=["frame", "views"], default="frame",
+    ap.add_argument("--mode", choices=["frame", "views"], default="views",
                     help="frame: one frame per step tiled over the ranks (strong); views: N views per step (weak)")
     ap.add_argument("--cpu-frames", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -355,32 +357,31 @@ def main() -> int:
     # ---- timed region 1: device-resident frames (`value`)
     elapsed = timed(step, args.steps)
 
-    # ---- timed region 2: the same frames gathered into one host frame shared by the ranks
+    # ---- timed region 2: the same frames gathered into host frames shared by the ranks
     shared = None
     gathered = None
-    if args.mode == "frame":
-        nbytes = W * H * 16    # uint32 pixels + float RGB plane (parity check)
-        tag = f"{os.environ.get('MASTER_PORT', 'solo')}_{os.getuid()}_{os.getppid() if N > 1 else os.getpid()}"
-        if d.rank == 0:
-            shared = SharedFrame.create(tag, nbytes)
-        d.barrier()
-        if d.rank != 0:
-            shared = SharedFrame.attach(tag, nbytes)
-        d.barrier()
-        if d.rank == 0:
-            shared.unlink()   # every rank has it mapped: nothing stays behind in /dev/shm
-        pinned = shared.pin(ctx)
-        host_px = shared.view(np.uint32, W * H)
-        host_rgb = shared.view(np.float32, 3 * W * H, offset=4 * W * H)
-        if not args.no_gather:
-            for i in range(min(args.warmup, 10)):
-                step(i, host_px)
-            sync_all()
-            g_elapsed = timed(lambda i: step(i, host_px), args.steps)
-            gathered = {"mpix_s": round(frame_pixels * args.steps / g_elapsed / 1e6, 3),
-                        "ms_per_frame": round(g_elapsed / args.steps * 1e3, 5), "pinned": bool(pinned),
-                        "target": "one page-locked host frame shared by all ranks (/dev/shm mapping)",
-                        "copy": "hipMemcpy2DAsync of the rank's own 16-row stripes (rtx_gather_async)"}
+    nbytes = nviews * W * H * 16    # uint32 pixels + float RGB plane per view (parity check)
+    tag = f"{os.environ.get('MASTER_PORT', 'solo')}_{os.getuid()}_{os.getppid() if N > 1 else os.getpid()}"
+    if d.rank == 0:
+        shared = SharedFrame.create(tag, nbytes)
+    d.barrier()
+    if d.rank != 0:
+        shared = SharedFrame.attach(tag, nbytes)
+    d.barrier()
+    if d.rank == 0:
+        shared.unlink()   # every rank has it mapped: nothing stays behind in /dev/shm
+    pinned = shared.pin(ctx)
+    host_px = shared.view(np.uint32, nviews * W * H)
+    host_rgb = shared.view(np.float32, 3 * nviews * W * H, offset=4 * nviews * W * H)
+    if not args.no_gather:
+        for i in range(min(args.warmup, 10)):
+            step(i, host_px)
+        sync_all()
+        g_elapsed = timed(lambda i: step(i, host_px), args.steps)
+        gathered = {"mpix_s": round(frame_pixels * args.steps / g_elapsed / 1e6, 3),
+                    "ms_per_step": round(g_elapsed / args.steps * 1e3, 5), "pinned": bool(pinned),
+                    "target": "page-locked host frames (one per view) shared by all ranks (/dev/shm mapping)",
+                    "copy": "hipMemcpy2DAsync of the rank's own 16-row stripes (rtx_gather_async)"}
 
     # Kernel-only time of the same launches, HIP events on the launch stream.
     kernel_ms = C.c_float()
@@ -402,7 +403,8 @@ def main() -> int:
     # context (same schedule state), with colours, gathered into the shared host frame.
     parity = None
     if shared is not None:
-        ctx.render_async(views[0], params, want_rgb=True)
+        abi.check(lib.rtx_render_views_async(ctx.h, views, nviews, C.byref(params), 1), "rtx_render_views_async",
+                  ctx.h)
         ctx.gather_async(host_px, host_rgb)
         ctx.synchronize()
         d.barrier()
@@ -427,7 +429,8 @@ def main() -> int:
         except Exception as e:   # the baseline must not take the headline down
             cpu = {"value": None, "unit": "Mpixels/s", "cores": 0, "kind": "reference", "sample": f"failed: {e}"}
     if d.rank == 0 and shared is not None:
-        parity = parity_report(np.array(host_px), np.array(host_rgb), args.scene, W, H, cpu)
+        # view 0 is the reference camera: the frame the goldens were made from
+        parity = parity_report(np.array(host_px[:W * H]), np.array(host_rgb[:3 * W * H]), args.scene, W, H, cpu)
 
     ms_per_step = elapsed / args.steps * 1e3
     value = frame_pixels * args.steps / elapsed / 1e6
@@ -448,10 +451,12 @@ def main() -> int:
         "dtype": "f32",
         "data": f"synthetic: the reference's {args.scene} scene (Initialize state) built by the host scene layer; "
                 "no datasets",
-        "config": {"workload": (f"{args.scene} {W}x{H}, Combined lighting, shadows on, one frame per step tiled "
-                                f"over {N} rank(s) in 16-row stripes" if strong else
-                                f"{args.scene} {W}x{H}, Combined lighting, shadows on, {N} view(s) per step "
-                                f"striped over {N} rank(s)"),
+        "config": {"workload": (f"{args.scene} {W}x{H}, Combined lighting, shadows on, one frame per step"
+                                if N == 1 else
+                                f"{args.scene} {W}x{H}, Combined lighting, shadows on, one frame per step tiled "
+                                f"over {N} ranks in 16-row stripes" if strong else
+                                f"{args.scene} {W}x{H}, Combined lighting, shadows on, {N} views per step, each "
+                                f"tiled over the {N} ranks in 16-row stripes"),
                    "scene": args.scene, "width": W, "height": H, "views_per_step": nviews,
                    "stripe_rows": 16 if striped else 0,
                    "parallelism": f"image stripes x{N} (no collective)", "frames_in_flight": len(ctxs)},

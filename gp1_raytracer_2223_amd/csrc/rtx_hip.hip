@@ -727,6 +727,10 @@ __device__ __forceinline__ uint32_t q8(float c) {
 #ifndef RTX_MIN_WAVES_PER_EU
 #define RTX_MIN_WAVES_PER_EU 1
 #endif
+// XCD-aware dispatch: runs of this many consecutive dispatch-order entries per XCD (0/1: off)
+#ifndef RTX_XCD_RUN
+#define RTX_XCD_RUN 0
+#endif
 // DEEP: the variant for scenes whose BVH is kStackDepth or more levels deep (a DFS stack of
 // kStackDepthDeep entries per wave in LDS; fewer waves fit a CU, so it is used only then).
 template <bool COUNT, int PHASE, bool DEEP = false>
@@ -752,7 +756,16 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : RTX_MIN_WAVES_PER_EU
     // moment the wave ends (4-wave ones held it until the slowest sibling ended: Bunny
     // -3 %, Synthetic100k -9 %).  Which wave renders a tile never changes a pixel's value.
     const uint32_t b = blockIdx.x;
-    const uint32_t widx = b * kWavesPerBlock + wave;   // wave index in the launch
+    uint32_t widx = b * kWavesPerBlock + wave;   // wave index in the launch
+    if (PHASE == 0 && RTX_XCD_RUN > 1) {
+        // Workgroups go round robin to the 8 XCDs (blockIdx % 8), each with its own L2: give
+        // XCD x runs of RTX_XCD_RUN consecutive dispatch-order entries (neighbouring tiles of
+        // one cost class walk the same BVH nodes) instead of every 8th entry.  A bijection on
+        // the grid, which the host pads to a multiple of 8 * RTX_XCD_RUN.
+        const uint32_t x = b % 8u, k = b / 8u;
+        const uint32_t pos = ((k / RTX_XCD_RUN) * 8u + x) * RTX_XCD_RUN + (k % RTX_XCD_RUN);
+        widx = pos * kWavesPerBlock + wave;
+    }
     uint32_t tile, part = 0, light = 0;
     if (PHASE == 0) {
         if (widx >= F.n_tiles) return;
@@ -1837,7 +1850,9 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     F.counters = c->d_counters;
     const uint32_t ntiles = F.tiles_x * gy * static_cast<uint32_t>(n_views);
     F.n_tiles = ntiles;
-    grid = dim3((ntiles + kWavesPerBlock - 1) / kWavesPerBlock, 1, 1);
+    uint32_t nblocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (RTX_XCD_RUN > 1) nblocks = (nblocks + 8 * RTX_XCD_RUN - 1) / (8 * RTX_XCD_RUN) * (8 * RTX_XCD_RUN);
+    grid = dim3(nblocks, 1, 1);
     // Cost-ordered dispatch (see the kernel): keep one order/cost pair per launch shape.
     if (ntiles > c->sched_cap) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));

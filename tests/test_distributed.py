@@ -78,28 +78,31 @@ def test_stripe_partition_gloo(world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2])
-def test_bench_strong_mode_hip_gloo(world, tmp_path):
+@pytest.mark.parametrize("mode", ["views", "frame"])
+def test_bench_multi_rank_hip_gloo(mode, tmp_path):
     """The real multi-rank path on the HIP renderer: bench.py under torch.distributed.run
-    with `world` gloo ranks pinned to device 0 (RTX_BENCH_DEVICE; the driver's N-GPU runs
-    map rank r to device r).  Each rank renders its 16-row stripes of one Bunny 1080p frame
-    and gathers them into the shared page-locked host frame; rank 0 checks the gathered
-    frame against the reference's SHA-256 (bench.py `parity`)."""
+    with 2 gloo ranks pinned to device 0 (RTX_BENCH_DEVICE; the driver's N-GPU runs map
+    rank r to device r).  `views` (the default, weak scaling): 2 views per step, each
+    striped over both ranks; `frame` (strong): one Bunny 1080p frame per step.  Each rank
+    gathers its stripes into the shared page-locked host frames; rank 0 checks view 0 (the
+    reference camera) against the reference's SHA-256 (bench.py `parity`)."""
     import json
     import subprocess
     import sys
     from pathlib import Path
+    world = 2
     root = Path(__file__).resolve().parents[1]
     env = dict(os.environ, RTX_BENCH_DEVICE="0", MASTER_ADDR="127.0.0.1")
-    port = 29700 + os.getpid() % 200
+    port = 29700 + os.getpid() % 200 + (0 if mode == "views" else 1)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), str(root / "bench.py"), "--gpus", str(world),
-           "--steps", "20", "--warmup", "5", "--no-cpu-baseline"]
+           "--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--mode", mode]
     out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-4000:]
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
     r = json.loads(line)
-    assert r["n_gpus"] == world and r["scaling"] == "strong"
+    assert r["n_gpus"] == world and r["scaling"] == ("weak" if mode == "views" else "strong")
     assert r["parity"]["bit_exact"] is True, r["parity"]
-    assert r["roofline"]["frame_pixels_counted"] == 1920 * 1080   # every pixel exactly once over the ranks
+    views = world if mode == "views" else 1
+    assert r["roofline"]["frame_pixels_counted"] == views * 1920 * 1080   # every pixel exactly once
     assert r["host_gather"]["mpix_s"] > 0

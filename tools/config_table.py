@@ -4,7 +4,8 @@ reference CPU Renderer built in place (oracle/_ref/ref_harness) on the same box'
 GPU: kernel-only ms/frame (HIP events, min of 3 x `iters` launches), algorithmic FLOP of one
 frame (instrumented kernel, SURVEY §8(d) model), end-to-end ms incl. the D2H copy of the
 frame into pageable host memory; frames-in-flight throughput (2 render contexts, frames issued
-round robin, as bench.py).  CPU: median Renderer::Render seconds over `frames` frames.
+round robin, as bench.py).  CPU: median Renderer::Render seconds over `frames` frames on
+sched_getaffinity threads (the reference's hardware_concurrency), cgroup quota recorded.
 Usage (GPU box):  python tools/config_table.py [out.json]
 """
 import ctypes as C
@@ -27,7 +28,7 @@ from gp1_raytracer_2223_amd.renderer import DeviceContext  # noqa: E402
 from gp1_raytracer_2223_amd.scene import HostScene  # noqa: E402
 
 sys.path.insert(0, str(ROOT))
-from bench import FP32_PEAK_TFLOPS, write_obj_from_asset  # noqa: E402
+from bench import FP32_PEAK_TFLOPS, cgroup_cpu_quota, write_obj_from_asset  # noqa: E402
 
 COST = [41, 19, 14, 12, 63, 9, 15, 1, 26, 6, 31, 103]
 CONFIGS = [  # (scene, W, H, cpu frames)
@@ -54,7 +55,10 @@ def cpu_ref(harness, scene, W, H, threads, frames):
 
 def main():
     out_path = Path(sys.argv[1]) if len(sys.argv) > 1 else None
-    threads = min(16, os.cpu_count() or 1)
+    # the reference's hardware_concurrency(): every CPU this process may run on; a cgroup quota
+    # (the GPU box: 16 CPUs of 256) is recorded beside it
+    threads = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
     harness = ROOT / "oracle" / "_ref" / "ref_harness"
     cpu_model = ""
     try:
@@ -110,7 +114,8 @@ def main():
                         "cpu_fnv": r.get("fnv"), "speedup": round(row["mpix_s"] / r["mpix_s"], 1)})
         rows.append(row)
         print(json.dumps(row), flush=True)
-    meta = {"cpu_model": cpu_model, "nproc": os.cpu_count(), "threads": threads, "rows": rows}
+    meta = {"cpu_model": cpu_model, "nproc": os.cpu_count(), "threads": threads, "cgroup_cpu_quota": quota,
+            "rows": rows}
     if out_path:
         out_path.write_text(json.dumps(meta, indent=1))
     ctx.close()

@@ -15,7 +15,8 @@ meta = {}
 for f in sorted(glob.glob(f"{d}/pmc*/run_counter_collection.csv")):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].startswith("void rtx_render_kernel<false, 0>") or "rtx_render_kernel<false>" in r["Kernel_Name"]:
+        k = r["Kernel_Name"]
+        if k.startswith(("void rtx_render_kernel<false, 0>", "void rtx_render_kernel<false, 0, false>")):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
             meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count",
                                       "SGPR_Count")}
