@@ -326,36 +326,37 @@ float TriangleMesh::FindBestSplitFast(const BVHNode& node, int& axis, float& spl
         const float minBounds = minB[axisIdx];
         const float boundsDifference = maxB[axisIdx] - minBounds;
         const uint32_t* binCount = counts[axisIdx];
-        float leftArea[kPlanes], rightArea[kPlanes];
-        int leftCount[kPlanes], rightCount[kPlanes];
-        int leftSum = 0, rightSum = 0;
-        // AABB::Grow(bin) and AABB::Area (e.x*e.y + e.y*e.z + e.z*e.x, left to right) per lane
-        // An empty bin leaves the running box unchanged (its lo is FLT_MAX, and the running
-        // hi never drops below the FLT_MIN it starts from), so its area is carried over.
-        __m128 llo = _mm_set1_ps(FLT_MAX), lhi = _mm_set1_ps(FLT_MIN), rlo = llo, rhi = lhi;
-        const float empty = Area(llo, lhi);
-        float la = empty, ra = empty;
-        for (int i = 0; i < kPlanes; ++i) {
-            leftSum += binCount[i];
-            leftCount[i] = leftSum;
-            if (binCount[i]) {
-                llo = MinRef(llo, blo[axisIdx][i]);
-                lhi = MaxRef(lhi, bhi[axisIdx][i]);
-                la = Area(llo, lhi);
+        // The reference evaluates all 7 planes; only planes right after a non-empty bin with
+        // triangles on both sides can be accepted: an empty side has area inf (its box keeps
+        // FLT_MAX / FLT_MIN) and 0 * inf = NaN never compares below bestCost, and a plane after
+        // an empty bin repeats the previous plane's counts and areas, which the strict < rejects.
+        // A bin's box leaves a running box unchanged when the bin is empty (its lo is FLT_MAX,
+        // and a running hi never drops below the FLT_MIN it starts from).
+        float rightArea[kPlanes];
+        int rightCount[kPlanes];
+        {
+            __m128 rlo = _mm_set1_ps(FLT_MAX), rhi = _mm_set1_ps(FLT_MIN);
+            int rightSum = 0;
+            for (int j = kPlanes; j >= 1; --j) {   // plane j - 1 has bins j..7 on its right
+                if (binCount[j]) {
+                    rightSum += binCount[j];
+                    rlo = MinRef(rlo, blo[axisIdx][j]);
+                    rhi = MaxRef(rhi, bhi[axisIdx][j]);
+                }
+                rightCount[j - 1] = rightSum;
+                if (binCount[j - 1] && rightSum) rightArea[j - 1] = Area(rlo, rhi);
             }
-            leftArea[i] = la;
-            rightSum += binCount[kPlanes - i];
-            rightCount[kPlanes - i - 1] = rightSum;
-            if (binCount[kPlanes - i]) {
-                rlo = MinRef(rlo, blo[axisIdx][kPlanes - i]);
-                rhi = MaxRef(rhi, bhi[axisIdx][kPlanes - i]);
-                ra = Area(rlo, rhi);
-            }
-            rightArea[kPlanes - i - 1] = ra;
         }
         const float scale = boundsDifference / kBins;
+        __m128 llo = _mm_set1_ps(FLT_MAX), lhi = _mm_set1_ps(FLT_MIN);
+        int leftSum = 0;
         for (int i = 0; i < kPlanes; ++i) {
-            const float planeCost = static_cast<float>(leftCount[i]) * leftArea[i] +
+            if (!binCount[i]) continue;
+            leftSum += binCount[i];
+            llo = MinRef(llo, blo[axisIdx][i]);
+            lhi = MaxRef(lhi, bhi[axisIdx][i]);
+            if (!rightCount[i]) continue;
+            const float planeCost = static_cast<float>(leftSum) * Area(llo, lhi) +
                                     static_cast<float>(rightCount[i]) * rightArea[i];
             if (planeCost < bestCost) {
                 axis = axisIdx;
@@ -518,7 +519,10 @@ float TriangleMesh::FindBestSplitPlane(const BVHNode& node, int& axis, float& sp
         const TriCache& t = tc_[k];
         for (int a = 0; a < 3; ++a) {
             if (!live[a]) continue;
-            int b = static_cast<int>((t.c[a] - minB[a]) * scales[a]);
+            const float x = (t.c[a] - minB[a]) * scales[a];
+            // static_cast<int> of a NaN (a NaN vertex) is undefined; the reference indexes out of
+            // bounds there (x86: INT_MIN).  Such a triangle goes to bin 0 here instead of crashing.
+            int b = x >= 0.f ? static_cast<int>(fminf(x, 2147483520.f)) : 0;
             if (kPlanes < b) b = kPlanes;   // std::min(amountOfPlaneBins, b)
             counts[a][b] += 3;
             bins[a][b].minAABB = Vec3::Min(bins[a][b].minAABB, t.lo);

@@ -17,6 +17,7 @@ from __future__ import annotations
 import ctypes as C
 import mmap
 import os
+import tempfile
 
 import numpy as np
 
@@ -40,13 +41,30 @@ class SharedFrame:
         self.buf = np.frombuffer(self.mm, dtype=np.uint8)
         self._pinned = None
 
+    @staticmethod
+    def _dirs() -> list[str]:
+        return [SHM_DIR, tempfile.gettempdir()]
+
     @classmethod
     def create(cls, tag: str, nbytes: int) -> "SharedFrame":
-        return cls(os.path.join(SHM_DIR, f"rtx_frame_{tag}"), nbytes, True)
+        """In /dev/shm when it has room for the frame (a small container /dev/shm would raise
+        SIGBUS on first touch of a page beyond it), else in the temp directory."""
+        for d in cls._dirs():
+            try:
+                st = os.statvfs(d)
+            except OSError:
+                continue
+            if st.f_bavail * st.f_frsize >= nbytes + (64 << 20):
+                return cls(os.path.join(d, f"rtx_frame_{tag}"), nbytes, True)
+        raise OSError(f"no room for a {nbytes}-byte shared frame in {cls._dirs()}")
 
     @classmethod
     def attach(cls, tag: str, nbytes: int) -> "SharedFrame":
-        return cls(os.path.join(SHM_DIR, f"rtx_frame_{tag}"), nbytes, False)
+        for d in cls._dirs():
+            path = os.path.join(d, f"rtx_frame_{tag}")
+            if os.path.exists(path):
+                return cls(path, nbytes, False)
+        raise FileNotFoundError(f"shared frame rtx_frame_{tag} not found in {cls._dirs()}")
 
     def unlink(self) -> None:
         try:

@@ -69,3 +69,25 @@ def test_update_sequence_matches_reference(path, builder):
     got = json.loads(r.stdout.strip().splitlines()[-1])
     for n in cps:
         assert got[str(n)] == [str(x) for x in g[f"after{n}"]], f"after {n} updates"
+
+
+def test_nan_mesh_takes_direct_builder(tmp_path):
+    """A mesh with NaN coordinates (here a NaN scale) cannot use the fast builder's
+    min/max shortcuts (a NaN vertex drops out of min(min(v0, v1), v2) differently from the
+    reference's vertex-by-vertex Grow); it must fall back to the direct restatement, so both
+    settings give the same arrays."""
+    import json
+    f = tmp_path / "nan.rtxscene"
+    f.write_text("camera 0 2 -8 45\nmaterial lambert 1 1 1 1\nplane 0 0 0 0 1 0 1\n"
+                 "mesh lowpoly_bunny2 1 back scale nan 1 1 spin\n"
+                 "mesh simple_cube 1 front translate 1 1 0 spin\nlight point 0 5 -4 50 1 1 1\n")
+    out = {}
+    for builder in ("fast", "direct"):
+        env = dict(os.environ)
+        env.pop("RTX_HOST_BVH", None)
+        if builder == "direct":
+            env["RTX_HOST_BVH"] = "direct"
+        r = subprocess.run([sys.executable, "-c", _CHILD, str(ROOT), "file:" + str(f), json.dumps([0.4, 1.1, 2.5]),
+                            json.dumps([1, 3])], capture_output=True, text=True, env=env, check=True)
+        out[builder] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["fast"] == out["direct"]
