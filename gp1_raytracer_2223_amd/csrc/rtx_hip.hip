@@ -724,6 +724,9 @@ __device__ __forceinline__ uint32_t q8(float c) {
 #ifndef RTX_ABL_SMESH
 #define RTX_ABL_SMESH 0
 #endif
+#ifndef RTX_ABL_LIGHTS
+#define RTX_ABL_LIGHTS 0
+#endif
 #ifndef RTX_MIN_WAVES_PER_EU
 #define RTX_MIN_WAVES_PER_EU 1
 #endif
@@ -926,7 +929,7 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : RTX_MIN_WAVES_PER_EU
         // originOffset = hit.origin + hit.normal * 0.0001f (Renderer.cpp:126)
         const float oox = hx + nx * 0.0001f, ooy = hy + ny * 0.0001f, ooz = hz + nz * 0.0001f;
         const float vx = -dx, vy = -dy, vz = -dz;
-        const uint32_t l_first = PHASE == 2 ? light : 0u, l_end = PHASE == 2 ? light + 1 : S.n_lights;
+        const uint32_t l_first = PHASE == 2 ? light : 0u, l_end = PHASE == 2 ? light + 1 : (RTX_ABL_LIGHTS ? 0u : S.n_lights);
         for (uint32_t li = l_first; li < l_end; ++li) {
             float4 L0, L1;
             ldcb32(S.lights, opaque(li * 32u), L0, L1);

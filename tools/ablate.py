@@ -31,6 +31,12 @@ for name, W, H in [("W4_Bunny", 1920, 1080), ("W3", 1280, 720), ("W4_Reference",
             continue
         p = abi.make_params(W, H, mode, sh)
         ctx.time_frames(cam, p, 5)
+        # ABLATE_WARM=<ms>: render continuously that long first, so the GPU clock has left its
+        # idle state (profiles/r02/warmup_probe.txt) — light variants otherwise run slow clocks
+        import time
+        t_end = time.perf_counter() + float(os.environ.get("ABLATE_WARM", "0")) / 1e3
+        while time.perf_counter() < t_end:
+            ctx.time_frames(cam, p, 50)
         ms = min(ctx.time_frames(cam, p, iters) for _ in range(3))
         flop = None
         if tag == "combined+shadows":

@@ -14,14 +14,14 @@ for L in $LIBS; do
   for grp in "${GRPS[@]}"; do
     i=$((i+1))
     timeout -s KILL 90 rocprofv3 --pmc $grp -d $OUT/$L/g$i -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --inflight 1 \
-      --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/$L.g$i.log 2>&1 || { echo "$L group $i failed"; tail -5 $OUT/$L.g$i.log; exit 1; }
+      --no-cpu-baseline --no-gather ${BENCH_ARGS:-} > $OUT/$L.g$i.log 2>&1 || { echo "$L group $i failed"; tail -5 $OUT/$L.g$i.log; exit 1; }
   done
   python3 - "$OUT/$L" "$L" <<'PY'
 import csv, collections, glob, sys
 agg = collections.defaultdict(list)
 for f in glob.glob(sys.argv[1] + "/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].startswith("void rtx_render_kernel<false, 0>"):
+        if r["Kernel_Name"].startswith(("void rtx_render_kernel<false, 0>", "void rtx_render_kernel<false, 0, false>")):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 m = {k: sum(v) / len(v) for k, v in agg.items()}
 w = m.get("SQ_WAVES", 32400.0)
