@@ -642,8 +642,16 @@ struct RGB {
 
 // Material::Shade (Material.h:41-123) via BRDFs.h; m2.yzw holds (rgb*kd)/PI computed on
 // the host with the same binary32 operations (BRDF::Lambert, BRDFs.h:14-17).
+// LAMBERT: every material the scene's geometry references is Material_Lambert (a uniform fact
+// the host established at upload, see kSpecLambert): the BRDF is the precomputed constant.
+template <bool LAMBERT = false>
 __device__ __forceinline__ RGB shade(const DevScene& S, uint32_t mi, float nx, float ny, float nz, float lx, float ly,
                                      float lz, float vx, float vy, float vz, Counts& cnt, bool count) {
+    if (LAMBERT) {
+        const float4 m2 = ldc(S.materials, 3 * mi + 2);
+        if (count) cnt.c[kShadeLambert]++;
+        return {m2.y, m2.z, m2.w};
+    }
     const float4 m0 = ldc(S.materials, 3 * mi), m1 = ldc(S.materials, 3 * mi + 1), m2 = ldc(S.materials, 3 * mi + 2);
     const int kind = __float_as_int(m0.x);
     RGB c{0.f, 0.f, 0.f};
@@ -736,8 +744,24 @@ __device__ __forceinline__ uint32_t q8(float c) {
 #endif
 // DEEP: the variant for scenes whose BVH is kStackDepth or more levels deep (a DFS stack of
 // kStackDepthDeep entries per wave in LDS; fewer waves fit a CU, so it is used only then).
-template <bool COUNT, int PHASE, bool DEEP = false>
-__global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : RTX_MIN_WAVES_PER_EU) rtx_render_kernel(const DevScene S, const FrameArgs F) {
+// SPEC (kSpec* bits, rtx_kernels.h): uniform facts of the scene and frame the host checked at
+// launch, compiled in instead of branched on (same operations, so the same pixels; fewer
+// uniform branches, selects and registers: Bunny 74.2 -> 68.3 us).
+// The specialised kernel needs 47 VGPRs; asking for 7 waves per SIMD makes the compiler keep it
+// to 94 SGPRs (6 spilled to VGPR lanes, outside the loops), which lets 8 waves fit (the SGPR file
+// caps 102-SGPR kernels at 7): Bunny 68.5 -> 65.4 us, Bunny + 8 lights 488 -> 461 us.  Asking for
+// 8 spills 26 SGPRs and is slower (68 us).
+#ifndef RTX_SPEC_WAVES
+#define RTX_SPEC_WAVES 7
+#endif
+template <bool COUNT, int PHASE, bool DEEP = false, int SPEC = 0>
+__global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : (SPEC ? RTX_SPEC_WAVES : RTX_MIN_WAVES_PER_EU))
+    rtx_render_kernel(const DevScene S, const FrameArgs F) {
+    constexpr bool kLambert = (SPEC & kSpecLambert) != 0, kPoint = (SPEC & kSpecPoint) != 0;
+    constexpr bool kNoSph = (SPEC & kSpecNoSpheres) != 0, kComb = (SPEC & kSpecCombShadows) != 0;
+#define f_mode (kComb ? RTX_MODE_COMBINED : F.mode)
+#define f_shadows (kComb ? 1 : F.shadows)
+#define n_sph (kNoSph ? 0u : S.n_spheres)
     constexpr int kDepth = DEEP ? kStackDepthDeep : kStackDepth;
     __shared__ uint4 stkE[kBlockThreads / 64][kDepth];
     __shared__ unsigned long long stkT[COUNT ? kBlockThreads / 64 : 1][COUNT ? kDepth : 1];
@@ -765,8 +789,9 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : RTX_MIN_WAVES_PER_EU
         // XCD x runs of RTX_XCD_RUN consecutive dispatch-order entries (neighbouring tiles of
         // one cost class walk the same BVH nodes) instead of every 8th entry.  A bijection on
         // the grid, which the host pads to a multiple of 8 * RTX_XCD_RUN.
+        constexpr uint32_t kRun = RTX_XCD_RUN > 1 ? RTX_XCD_RUN : 1;
         const uint32_t x = b % 8u, k = b / 8u;
-        const uint32_t pos = ((k / RTX_XCD_RUN) * 8u + x) * RTX_XCD_RUN + (k % RTX_XCD_RUN);
+        const uint32_t pos = ((k / kRun) * 8u + x) * kRun + (k % kRun);
         widx = pos * kWavesPerBlock + wave;
     }
     uint32_t tile, part = 0, light = 0;
@@ -831,7 +856,7 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : RTX_MIN_WAVES_PER_EU
     float best_t = FLT_MAX, sc_t = FLT_MAX;
     // kind: 0 none, 1 sphere, 2 plane, 3 triangle; best_idx: the record's BYTE offset
     uint32_t best_kind = 0, best_idx = 0;
-    for (uint32_t i = 0; i < S.n_spheres * 16u; i += 16u) {
+    for (uint32_t i = 0; i < n_sph * 16u; i += 16u) {
         const float4 s = ldcb16(S.spheres, opaque(i));
         if (COUNT && valid) cnt.c[kSphere]++;
         const SphereProj q = sphere_perp(s, vr);
@@ -933,13 +958,13 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : RTX_MIN_WAVES_PER_EU
         for (uint32_t li = l_first; li < l_end; ++li) {
             float4 L0, L1;
             ldcb32(S.lights, opaque(li * 32u), L0, L1);
-            const int ltype = __float_as_int(L0.w);
+            const int ltype = kPoint ? RTX_LIGHT_POINT : __float_as_int(L0.w);
             const bool known = (ltype == RTX_LIGHT_POINT || ltype == RTX_LIGHT_DIRECTIONAL);
             float lx = known ? L0.x - oox : 0.f, ly = known ? L0.y - ooy : 0.f, lz = known ? L0.z - ooz : 0.f;
             const float mag = sqrtf(lx * lx + ly * ly + lz * lz);
             div3_exact(lx, ly, lz, mag);
             bool occ = false;
-            if (F.shadows) {
+            if (f_shadows) {
                 // Scene::DoesHit (Scene.cpp:68-96) on Ray{originOffset, l, 1e-4, |l|}; `live` =
                 // lanes still without an occluder (first hit wins, order irrelevant for a bool)
                 unsigned long long sslow;
@@ -951,7 +976,7 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : RTX_MIN_WAVES_PER_EU
                 if (COUNT && did) cnt.c[kShadow]++;
                 // (single-condition loops with a separate exit test: a `&& live` loop
                 // condition is carried as a VGPR boolean by the compiler)
-                for (uint32_t i = 0; i < (PHASE == 2 ? 0u : S.n_spheres * 16u); i += 16u) {
+                for (uint32_t i = 0; i < (PHASE == 2 ? 0u : n_sph * 16u); i += 16u) {
 #if RTX_SPHERE_BREAK
                     if (!live) break;
 #endif
@@ -1028,7 +1053,7 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : RTX_MIN_WAVES_PER_EU
                 continue;
             }
             if (COUNT) cnt.c[kShadeBase]++;
-            if (F.mode == RTX_MODE_COMBINED || F.mode == RTX_MODE_RADIANCE) {
+            if (f_mode == RTX_MODE_COMBINED || f_mode == RTX_MODE_RADIANCE) {
                 // LightUtils::GetRadiance (Utils.h:355-369) at hit.origin
                 float s = 0.f;
                 bool any = true;
@@ -1041,18 +1066,18 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : RTX_MIN_WAVES_PER_EU
                     any = false;
                 }
                 const float rr = any ? L1.x * s : 0.f, rg = any ? L1.y * s : 0.f, rb = any ? L1.z * s : 0.f;
-                if (F.mode == RTX_MODE_RADIANCE) {
+                if (f_mode == RTX_MODE_RADIANCE) {
                     fr += rr; fg += rg; fb += rb;
                 } else {
                     const float oa = smax(nx * lx + ny * ly + nz * lz, 0.f);
-                    const RGB br = shade(S, mat, nx, ny, nz, lx, ly, lz, vx, vy, vz, cnt, COUNT);
+                    const RGB br = shade<kLambert>(S, mat, nx, ny, nz, lx, ly, lz, vx, vy, vz, cnt, COUNT);
                     fr += (rr * oa) * br.r; fg += (rg * oa) * br.g; fb += (rb * oa) * br.b;
                 }
-            } else if (F.mode == RTX_MODE_OBSERVED_AREA) {
+            } else if (f_mode == RTX_MODE_OBSERVED_AREA) {
                 const float oa = smax(nx * lx + ny * ly + nz * lz, 0.f);
                 fr += oa; fg += oa; fb += oa;
-            } else if (F.mode == RTX_MODE_BRDF) {
-                const RGB br = shade(S, mat, nx, ny, nz, lx, ly, lz, vx, vy, vz, cnt, COUNT);
+            } else if (f_mode == RTX_MODE_BRDF) {
+                const RGB br = shade<kLambert>(S, mat, nx, ny, nz, lx, ly, lz, vx, vy, vz, cnt, COUNT);
                 fr += br.r; fg += br.g; fb += br.b;
             }
         }
@@ -1104,6 +1129,10 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : RTX_MIN_WAVES_PER_EU
     }
 }
 
+#undef f_mode
+#undef f_shadows
+#undef n_sph
+
 template __global__ void rtx_render_kernel<false, 0>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<true, 0>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 1>(const DevScene, const FrameArgs);
@@ -1111,6 +1140,7 @@ template __global__ void rtx_render_kernel<false, 2>(const DevScene, const Frame
 template __global__ void rtx_render_kernel<false, 3>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 0, true>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<true, 0, true>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 0, false, kSpecAll>(const DevScene, const FrameArgs);
 
 // Next frames' dispatch order from this frame's per-tile cost: heaviest first, STABLE
 // within a cost class so that tiles rendered together stay spatial neighbours (they walk
@@ -1337,6 +1367,8 @@ struct rtx_ctx {
     uint32_t split_parts = kPartsPerMesh;            // RTX_SPLIT_PARTS (tuning)
     bool split_ok = false;           // the uploaded scene admits split rendering
     bool deep_stack = false;         // the uploaded scene needs rtx_render_kernel<..., DEEP = true>
+    int scene_spec = 0;              // kSpec* facts of the uploaded scene (kernel specialisation)
+    bool no_spec = false;            // RTX_NO_SPEC=1: always the generic kernel (tests)
     unsigned long long* d_hit_key = nullptr;
     uint32_t* d_occ = nullptr;
     rtx_render_params last{};
@@ -1468,6 +1500,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     // RTX_TILE_ORDER=0 disables cost-ordered tile dispatch (identity order every frame)
     if (const char* e = std::getenv("RTX_TILE_ORDER")) c->sched_enabled = std::strcmp(e, "0") != 0;
     // RTX_SPLIT=0 renders heavy tiles in one piece; RTX_SPLIT=force splits every tile
+    if (const char* e = std::getenv("RTX_NO_SPEC")) c->no_spec = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_SPLIT")) c->split_mode = std::strcmp(e, "0") == 0 ? 0u : (std::strcmp(e, "force") == 0 ? 2u : 1u);
     if (const char* e = std::getenv("RTX_SPLIT_PARTS")) {
         const int v = std::atoi(e);
@@ -1780,6 +1813,16 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     c->dev = d;
     // a BVH kStackDepth or more levels deep renders with the deep-stack variant, unsplit
     c->deep_stack = max_depth >= kStackDepth;
+    {   // uniform facts for the specialised kernels: referenced materials all Lambert, every
+        // light a point light, no spheres
+        bool lambert = true, point = true;
+        auto lam = [&](uint32_t m) { lambert = lambert && s->materials[m].kind == RTX_MAT_LAMBERT; };
+        for (uint32_t i = 0; i < s->n_spheres; ++i) lam(s->spheres[i].material);
+        for (uint32_t i = 0; i < s->n_planes; ++i) lam(s->planes[i].material);
+        for (uint32_t i = 0; i < s->n_meshes; ++i) lam(s->meshes[i].material);
+        for (uint32_t i = 0; i < s->n_lights; ++i) point = point && s->lights[i].type == RTX_LIGHT_POINT;
+        c->scene_spec = (lambert ? kSpecLambert : 0) | (point ? kSpecPoint : 0) | (s->n_spheres == 0 ? kSpecNoSpheres : 0);
+    }
     c->split_ok = split_ok && !parts.empty() && !c->deep_stack;
     c->has_scene = true;
     ++c->scene_gen;
@@ -1948,8 +1991,14 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(c->ev_join, s2));
     }
+    // specialised variant when the uniform facts hold (kSpec*, RTX_NO_SPEC=1 forces the generic one)
+    const int spec = c->no_spec ? 0
+                                : c->scene_spec | ((F.mode == RTX_MODE_COMBINED && F.shadows) ? kSpecCombShadows : 0);
     if (c->deep_stack)
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
+    else if (spec == kSpecAll)
+        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecAll>), grid, dim3(kBlockThreads), 0, c->stream,
+                           c->dev, F);
     else
         hipLaunchKernelGGL((rtx_render_kernel<false, 0>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
     HIP_TRY(c, hipGetLastError());

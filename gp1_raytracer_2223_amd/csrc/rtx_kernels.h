@@ -34,6 +34,12 @@ constexpr int kMaxHeavyTiles = 8192;   // heavy wave tiles per frame (hit-key bu
 // noise of 2.0; below 1.25 the split overhead outgrows the tail it removes
 constexpr int kSplitPermille = 1500;
 constexpr int kMaxSplitLights = 32;    // occlusion bits per pixel
+// Kernel specialisation (rtx_render_kernel's SPEC): uniform facts compiled in.
+constexpr int kSpecLambert = 1;        // every material referenced by geometry is Material_Lambert
+constexpr int kSpecPoint = 2;          // every light is a point light
+constexpr int kSpecNoSpheres = 4;      // no spheres
+constexpr int kSpecCombShadows = 8;    // lighting mode Combined, shadows on
+constexpr int kSpecAll = 15;
 
 // Work counters (SURVEY §8(d) cost model; same order as the oracle's).
 enum Counter {
