@@ -746,22 +746,32 @@ __device__ __forceinline__ uint32_t q8(float c) {
 // kStackDepthDeep entries per wave in LDS; fewer waves fit a CU, so it is used only then).
 // SPEC (kSpec* bits, rtx_kernels.h): uniform facts of the scene and frame the host checked at
 // launch, compiled in instead of branched on (same operations, so the same pixels; fewer
-// uniform branches, selects and registers: Bunny 74.2 -> 68.3 us).
-// The specialised kernel needs 47 VGPRs; asking for 7 waves per SIMD makes the compiler keep it
-// to 94 SGPRs (6 spilled to VGPR lanes, outside the loops), which lets 8 waves fit (the SGPR file
-// caps 102-SGPR kernels at 7): Bunny 68.5 -> 65.4 us, Bunny + 8 lights 488 -> 461 us.  Asking for
-// 8 spills 26 SGPRs and is slower (68 us).
+// uniform branches, selects and registers; constant plane / mesh counts unroll their loops:
+// Bunny 74.2 -> 61.2 us with RTX_SPEC_WAVES).
+// Occupancy targets of the specialised kernels.  The fully specialised one needs 46 VGPRs and,
+// asked for 8 waves per SIMD, 78 SGPRs (8 spilled to VGPR lanes, outside the loops): the SGPR
+// file no longer caps it at 7 waves like the generic kernel's 106 SGPRs (Bunny 61.1 -> 60.6 us,
+// Bunny + 8 lights 427 -> 418 us; 10 waves: no gain).  The partial one (non-Lambert
+// materials: 66 VGPRs) stays at 7.
 #ifndef RTX_SPEC_WAVES
-#define RTX_SPEC_WAVES 7
+#define RTX_SPEC_WAVES 8
+#endif
+#ifndef RTX_SPEC_WAVES_PARTIAL
+#define RTX_SPEC_WAVES_PARTIAL 7
 #endif
 template <bool COUNT, int PHASE, bool DEEP = false, int SPEC = 0>
-__global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : (SPEC ? RTX_SPEC_WAVES : RTX_MIN_WAVES_PER_EU))
+__global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
+                                                  : (SPEC == kSpecAll ? RTX_SPEC_WAVES
+                                                                      : (SPEC ? RTX_SPEC_WAVES_PARTIAL : RTX_MIN_WAVES_PER_EU)))
     rtx_render_kernel(const DevScene S, const FrameArgs F) {
     constexpr bool kLambert = (SPEC & kSpecLambert) != 0, kPoint = (SPEC & kSpecPoint) != 0;
     constexpr bool kNoSph = (SPEC & kSpecNoSpheres) != 0, kComb = (SPEC & kSpecCombShadows) != 0;
+    constexpr bool kP5 = (SPEC & kSpecFivePlanes) != 0, kOneMesh = (SPEC & kSpecOneMesh) != 0;
 #define f_mode (kComb ? RTX_MODE_COMBINED : F.mode)
 #define f_shadows (kComb ? 1 : F.shadows)
 #define n_sph (kNoSph ? 0u : S.n_spheres)
+#define n_pl (kP5 ? 5u : S.n_planes)          // constant trip counts: the plane and mesh loops unroll
+#define n_mesh (kOneMesh ? 1u : S.n_meshes)
     constexpr int kDepth = DEEP ? kStackDepthDeep : kStackDepth;
     __shared__ uint4 stkE[kBlockThreads / 64][kDepth];
     __shared__ unsigned long long stkT[COUNT ? kBlockThreads / 64 : 1][COUNT ? kDepth : 1];
@@ -870,7 +880,7 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : (SPEC ? RTX_SPEC_WAV
         best_kind = b ? 1u : best_kind;
         best_idx = b ? i : best_idx;
     }
-    for (uint32_t i = 0; i < ((RTX_ABL_PPLANE) ? 0u : S.n_planes * 32u); i += 32u) {
+    for (uint32_t i = 0; i < ((RTX_ABL_PPLANE) ? 0u : n_pl * 32u); i += 32u) {
         float4 p0, p1;
         ldcb32(S.planes, opaque(i), p0, p1);
         if (COUNT && valid) cnt.c[kPlane]++;
@@ -887,7 +897,7 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : (SPEC ? RTX_SPEC_WAV
         best_idx = b ? i : best_idx;
     }
     if (PHASE == 0) {
-        for (uint32_t mi = 0; mi < ((RTX_ABL_PMESH) ? 0u : S.n_meshes); ++mi) {
+        for (uint32_t mi = 0; mi < ((RTX_ABL_PMESH) ? 0u : n_mesh); ++mi) {
             const int4 M = ldcb16i(S.meshes, opaque(mi * 16u));
             uint32_t sc_tri = 0;
             unsigned long long unused = 0;
@@ -972,7 +982,7 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : (SPEC ? RTX_SPEC_WAV
                 unsigned long long live = hitmask;
                 const bool sfast = (hitmask & sslow) == 0 && S.tri_fast;
                 const int soct =
-                    (RTX_OCTANT && sfast && S.oct_bytes && PHASE == 0 && S.n_meshes) ? batch_octant(sr, hitmask) : -1;
+                    (RTX_OCTANT && sfast && S.oct_bytes && PHASE == 0 && n_mesh) ? batch_octant(sr, hitmask) : -1;
                 if (COUNT && did) cnt.c[kShadow]++;
                 // (single-condition loops with a separate exit test: a `&& live` loop
                 // condition is carried as a VGPR boolean by the compiler)
@@ -992,7 +1002,7 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : (SPEC ? RTX_SPEC_WAV
                 // the same originOffset for every light: the first light computes it and keeps it
                 // in LDS, the others read it back (same value, bit for bit).  One loop version
                 // per case, so no per-plane select.
-                const uint32_t np = (RTX_ABL_SPLANE || PHASE == 2) ? 0u : S.n_planes * 32u;
+                const uint32_t np = (RTX_ABL_SPLANE || PHASE == 2) ? 0u : n_pl * 32u;
                 const bool cache_ok = RTX_PNUM_CACHE && !COUNT && np <= static_cast<uint32_t>(kPlaneCache) * 32u;
                 if (cache_ok && li != l_first) {
                     for (uint32_t i = 0; i < np; i += 32u) {
@@ -1018,7 +1028,7 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : (SPEC ? RTX_SPEC_WAV
                         live &= ~(ballot(t >= sr.tmin) & ballot(t < sr.tmax) & cand);
                     }
                 }
-                for (uint32_t mi = 0; mi < ((RTX_ABL_SMESH || PHASE != 0) ? 0u : S.n_meshes); ++mi) {
+                for (uint32_t mi = 0; mi < ((RTX_ABL_SMESH || PHASE != 0) ? 0u : n_mesh); ++mi) {
                     if (!live) break;
                     float st = 0.f;
                     uint32_t stri = 0;
@@ -1132,6 +1142,8 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2 : (SPEC ? RTX_SPEC_WAV
 #undef f_mode
 #undef f_shadows
 #undef n_sph
+#undef n_pl
+#undef n_mesh
 
 template __global__ void rtx_render_kernel<false, 0>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<true, 0>(const DevScene, const FrameArgs);
@@ -1141,6 +1153,7 @@ template __global__ void rtx_render_kernel<false, 3>(const DevScene, const Frame
 template __global__ void rtx_render_kernel<false, 0, true>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<true, 0, true>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 0, false, kSpecAll>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 0, false, kSpecAll & ~kSpecLambert>(const DevScene, const FrameArgs);
 
 // Next frames' dispatch order from this frame's per-tile cost: heaviest first, STABLE
 // within a cost class so that tiles rendered together stay spatial neighbours (they walk
@@ -1821,7 +1834,8 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
         for (uint32_t i = 0; i < s->n_planes; ++i) lam(s->planes[i].material);
         for (uint32_t i = 0; i < s->n_meshes; ++i) lam(s->meshes[i].material);
         for (uint32_t i = 0; i < s->n_lights; ++i) point = point && s->lights[i].type == RTX_LIGHT_POINT;
-        c->scene_spec = (lambert ? kSpecLambert : 0) | (point ? kSpecPoint : 0) | (s->n_spheres == 0 ? kSpecNoSpheres : 0);
+        c->scene_spec = (lambert ? kSpecLambert : 0) | (point ? kSpecPoint : 0) | (s->n_spheres == 0 ? kSpecNoSpheres : 0) |
+                        (s->n_planes == 5 ? kSpecFivePlanes : 0) | (s->n_meshes == 1 ? kSpecOneMesh : 0);
     }
     c->split_ok = split_ok && !parts.empty() && !c->deep_stack;
     c->has_scene = true;
@@ -1999,6 +2013,9 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
     else if (spec == kSpecAll)
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecAll>), grid, dim3(kBlockThreads), 0, c->stream,
                            c->dev, F);
+    else if (spec == (kSpecAll & ~kSpecLambert))
+        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecAll & ~kSpecLambert>), grid, dim3(kBlockThreads), 0,
+                           c->stream, c->dev, F);
     else
         hipLaunchKernelGGL((rtx_render_kernel<false, 0>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
     HIP_TRY(c, hipGetLastError());

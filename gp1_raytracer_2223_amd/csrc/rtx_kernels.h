@@ -39,7 +39,9 @@ constexpr int kSpecLambert = 1;        // every material referenced by geometry 
 constexpr int kSpecPoint = 2;          // every light is a point light
 constexpr int kSpecNoSpheres = 4;      // no spheres
 constexpr int kSpecCombShadows = 8;    // lighting mode Combined, shadows on
-constexpr int kSpecAll = 15;
+constexpr int kSpecFivePlanes = 16;    // exactly 5 planes (the reference's room: W3, W4, the synthetic scenes)
+constexpr int kSpecOneMesh = 32;       // exactly 1 triangle mesh
+constexpr int kSpecAll = 63;
 
 // Work counters (SURVEY §8(d) cost model; same order as the oracle's).
 enum Counter {
