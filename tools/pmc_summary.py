@@ -16,7 +16,7 @@ for f in sorted(glob.glob(f"{d}/pmc*/run_counter_collection.csv")):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if k.startswith(("void rtx_render_kernel<false, 0>", "void rtx_render_kernel<false, 0, false>")):
+        if k.startswith(("void rtx_render_kernel<false, 0>", "void rtx_render_kernel<false, 0, false")):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
             meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count",
                                       "SGPR_Count")}

@@ -21,7 +21,7 @@ import csv, collections, glob, sys
 agg = collections.defaultdict(list)
 for f in glob.glob(sys.argv[1] + "/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].startswith(("void rtx_render_kernel<false, 0>", "void rtx_render_kernel<false, 0, false>")):
+        if r["Kernel_Name"].startswith(("void rtx_render_kernel<false, 0>", "void rtx_render_kernel<false, 0, false")):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 m = {k: sum(v) / len(v) for k, v in agg.items()}
 w = m.get("SQ_WAVES", 32400.0)
