@@ -642,12 +642,14 @@ struct RGB {
 
 // Material::Shade (Material.h:41-123) via BRDFs.h; m2.yzw holds (rgb*kd)/PI computed on
 // the host with the same binary32 operations (BRDF::Lambert, BRDFs.h:14-17).
-// LAMBERT: every material the scene's geometry references is Material_Lambert (a uniform fact
-// the host established at upload, see kSpecLambert): the BRDF is the precomputed constant.
-template <bool LAMBERT = false>
+// KINDS: the material kinds the scene's geometry can hit (kSpecKind* bits, established by the
+// host at upload; 0 = any).  Only their branches are compiled; a Lambert-only scene's BRDF is
+// the precomputed constant with no dispatch at all.
+template <int KINDS = 0>
 __device__ __forceinline__ RGB shade(const DevScene& S, uint32_t mi, float nx, float ny, float nz, float lx, float ly,
                                      float lz, float vx, float vy, float vz, Counts& cnt, bool count) {
-    if (LAMBERT) {
+    constexpr int K = KINDS ? KINDS : kSpecKindAll;
+    if (K == kSpecKindLambert) {
         const float4 m2 = ldc(S.materials, 3 * mi + 2);
         if (count) cnt.c[kShadeLambert]++;
         return {m2.y, m2.z, m2.w};
@@ -655,12 +657,12 @@ __device__ __forceinline__ RGB shade(const DevScene& S, uint32_t mi, float nx, f
     const float4 m0 = ldc(S.materials, 3 * mi), m1 = ldc(S.materials, 3 * mi + 1), m2 = ldc(S.materials, 3 * mi + 2);
     const int kind = __float_as_int(m0.x);
     RGB c{0.f, 0.f, 0.f};
-    if (kind == RTX_MAT_SOLID_COLOR) {
+    if ((K & kSpecKindSolid) && kind == RTX_MAT_SOLID_COLOR) {
         c = {m0.y, m0.z, m0.w};
-    } else if (kind == RTX_MAT_LAMBERT) {
+    } else if ((K & kSpecKindLambert) && kind == RTX_MAT_LAMBERT) {
         if (count) cnt.c[kShadeLambert]++;
         c = {m2.y, m2.z, m2.w};
-    } else if (kind == RTX_MAT_LAMBERT_PHONG) {
+    } else if ((K & kSpecKindPhong) && kind == RTX_MAT_LAMBERT_PHONG) {
         if (count) { cnt.c[kShadeLambert]++; cnt.c[kShadePhong]++; }
         // BRDF::Phong (BRDFs.h:33-40)
         const float s2 = 2.f * smax(nx * lx + ny * ly + nz * lz, 0.f);
@@ -668,7 +670,7 @@ __device__ __forceinline__ RGB shade(const DevScene& S, uint32_t mi, float nx, f
         const float cosa = smax(rx * vx + ry * vy + rz * vz, 0.f);
         const float spec = m1.y * powf(cosa, m1.z);
         c = {m2.y + spec, m2.z + spec, m2.w + spec};
-    } else if (kind == RTX_MAT_COOK_TORRANCE) {
+    } else if ((K & kSpecKindCT) && kind == RTX_MAT_COOK_TORRANCE) {
         if (count) cnt.c[kShadeCT]++;
         float hx = vx + lx, hy = vy + ly, hz = vz + lz;
         const float hm = sqrtf(hx * hx + hy * hy + hz * hz);
@@ -761,17 +763,20 @@ __device__ __forceinline__ uint32_t q8(float c) {
 #endif
 template <bool COUNT, int PHASE, bool DEEP = false, int SPEC = 0>
 __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
-                                                  : (SPEC == kSpecAll ? RTX_SPEC_WAVES
-                                                                      : (SPEC ? RTX_SPEC_WAVES_PARTIAL : RTX_MIN_WAVES_PER_EU)))
+                                                  : ((SPEC & kSpecKindAll) == kSpecKindLambert
+                                                         ? RTX_SPEC_WAVES
+                                                         : (SPEC ? RTX_SPEC_WAVES_PARTIAL : RTX_MIN_WAVES_PER_EU)))
     rtx_render_kernel(const DevScene S, const FrameArgs F) {
-    constexpr bool kLambert = (SPEC & kSpecLambert) != 0, kPoint = (SPEC & kSpecPoint) != 0;
+    constexpr int kKinds = SPEC & kSpecKindAll;
+    constexpr bool kPoint = (SPEC & kSpecPoint) != 0;
     constexpr bool kNoSph = (SPEC & kSpecNoSpheres) != 0, kComb = (SPEC & kSpecCombShadows) != 0;
     constexpr bool kP5 = (SPEC & kSpecFivePlanes) != 0, kOneMesh = (SPEC & kSpecOneMesh) != 0;
+    constexpr bool kNoMesh = (SPEC & kSpecNoMesh) != 0;
 #define f_mode (kComb ? RTX_MODE_COMBINED : F.mode)
 #define f_shadows (kComb ? 1 : F.shadows)
 #define n_sph (kNoSph ? 0u : S.n_spheres)
 #define n_pl (kP5 ? 5u : S.n_planes)          // constant trip counts: the plane and mesh loops unroll
-#define n_mesh (kOneMesh ? 1u : S.n_meshes)
+#define n_mesh (kNoMesh ? 0u : (kOneMesh ? 1u : S.n_meshes))
     constexpr int kDepth = DEEP ? kStackDepthDeep : kStackDepth;
     __shared__ uint4 stkE[kBlockThreads / 64][kDepth];
     __shared__ unsigned long long stkT[COUNT ? kBlockThreads / 64 : 1][COUNT ? kDepth : 1];
@@ -1080,14 +1085,14 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
                     fr += rr; fg += rg; fb += rb;
                 } else {
                     const float oa = smax(nx * lx + ny * ly + nz * lz, 0.f);
-                    const RGB br = shade<kLambert>(S, mat, nx, ny, nz, lx, ly, lz, vx, vy, vz, cnt, COUNT);
+                    const RGB br = shade<kKinds>(S, mat, nx, ny, nz, lx, ly, lz, vx, vy, vz, cnt, COUNT);
                     fr += (rr * oa) * br.r; fg += (rg * oa) * br.g; fb += (rb * oa) * br.b;
                 }
             } else if (f_mode == RTX_MODE_OBSERVED_AREA) {
                 const float oa = smax(nx * lx + ny * ly + nz * lz, 0.f);
                 fr += oa; fg += oa; fb += oa;
             } else if (f_mode == RTX_MODE_BRDF) {
-                const RGB br = shade<kLambert>(S, mat, nx, ny, nz, lx, ly, lz, vx, vy, vz, cnt, COUNT);
+                const RGB br = shade<kKinds>(S, mat, nx, ny, nz, lx, ly, lz, vx, vy, vz, cnt, COUNT);
                 fr += br.r; fg += br.g; fb += br.b;
             }
         }
@@ -1152,8 +1157,10 @@ template __global__ void rtx_render_kernel<false, 2>(const DevScene, const Frame
 template __global__ void rtx_render_kernel<false, 3>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 0, true>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<true, 0, true>(const DevScene, const FrameArgs);
-template __global__ void rtx_render_kernel<false, 0, false, kSpecAll>(const DevScene, const FrameArgs);
-template __global__ void rtx_render_kernel<false, 0, false, kSpecAll & ~kSpecLambert>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[0]>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[1]>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[2]>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[3]>(const DevScene, const FrameArgs);
 
 // Next frames' dispatch order from this frame's per-tile cost: heaviest first, STABLE
 // within a cost class so that tiles rendered together stay spatial neighbours (they walk
@@ -1826,16 +1833,21 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     c->dev = d;
     // a BVH kStackDepth or more levels deep renders with the deep-stack variant, unsplit
     c->deep_stack = max_depth >= kStackDepth;
-    {   // uniform facts for the specialised kernels: referenced materials all Lambert, every
-        // light a point light, no spheres
-        bool lambert = true, point = true;
-        auto lam = [&](uint32_t m) { lambert = lambert && s->materials[m].kind == RTX_MAT_LAMBERT; };
-        for (uint32_t i = 0; i < s->n_spheres; ++i) lam(s->spheres[i].material);
-        for (uint32_t i = 0; i < s->n_planes; ++i) lam(s->planes[i].material);
-        for (uint32_t i = 0; i < s->n_meshes; ++i) lam(s->meshes[i].material);
+    {   // uniform facts for the specialised kernels (kSpec*): the material kinds the geometry
+        // references, every light a point light, the sphere / plane / mesh counts
+        int kinds = 0;
+        bool point = true;
+        auto kind = [&](uint32_t m) {
+            const int k = s->materials[m].kind;
+            kinds |= (k >= RTX_MAT_SOLID_COLOR && k <= RTX_MAT_COOK_TORRANCE) ? (1 << k) : kSpecKindAll;
+        };
+        for (uint32_t i = 0; i < s->n_spheres; ++i) kind(s->spheres[i].material);
+        for (uint32_t i = 0; i < s->n_planes; ++i) kind(s->planes[i].material);
+        for (uint32_t i = 0; i < s->n_meshes; ++i) kind(s->meshes[i].material);
         for (uint32_t i = 0; i < s->n_lights; ++i) point = point && s->lights[i].type == RTX_LIGHT_POINT;
-        c->scene_spec = (lambert ? kSpecLambert : 0) | (point ? kSpecPoint : 0) | (s->n_spheres == 0 ? kSpecNoSpheres : 0) |
-                        (s->n_planes == 5 ? kSpecFivePlanes : 0) | (s->n_meshes == 1 ? kSpecOneMesh : 0);
+        c->scene_spec = kinds | (point ? kSpecPoint : 0) | (s->n_spheres == 0 ? kSpecNoSpheres : 0) |
+                        (s->n_planes == 5 ? kSpecFivePlanes : 0) | (s->n_meshes == 1 ? kSpecOneMesh : 0) |
+                        (s->n_meshes == 0 ? kSpecNoMesh : 0);
     }
     c->split_ok = split_ok && !parts.empty() && !c->deep_stack;
     c->has_scene = true;
@@ -1972,6 +1984,16 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     return RTX_OK;
 }
 
+// Index into kSpecVariants of the first variant the facts satisfy, -1 for none: every kind the
+// scene references is compiled into the variant, and every other fact the variant assumes holds.
+int spec_variant(int facts) {
+    for (int i = 0; i < static_cast<int>(sizeof kSpecVariants / sizeof kSpecVariants[0]); ++i) {
+        const int v = kSpecVariants[i], vk = v & kSpecKindAll, fk = facts & kSpecKindAll;
+        if ((fk & ~vk) == 0 && ((v & ~kSpecKindAll) & ~facts) == 0) return i;
+    }
+    return -1;
+}
+
 int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
     if (grid.x == 0 || grid.y == 0) return RTX_OK;
     if (count) {
@@ -2005,16 +2027,23 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(c->ev_join, s2));
     }
-    // specialised variant when the uniform facts hold (kSpec*, RTX_NO_SPEC=1 forces the generic one)
-    const int spec = c->no_spec ? 0
-                                : c->scene_spec | ((F.mode == RTX_MODE_COMBINED && F.shadows) ? kSpecCombShadows : 0);
+    // the first specialised variant whose facts the scene and frame satisfy (kSpecVariants;
+    // RTX_NO_SPEC=1 forces the generic kernel)
+    const int facts = c->scene_spec | ((F.mode == RTX_MODE_COMBINED && F.shadows) ? kSpecCombShadows : 0);
+    const int v = c->no_spec ? -1 : spec_variant(facts);
     if (c->deep_stack)
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
-    else if (spec == kSpecAll)
-        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecAll>), grid, dim3(kBlockThreads), 0, c->stream,
-                           c->dev, F);
-    else if (spec == (kSpecAll & ~kSpecLambert))
-        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecAll & ~kSpecLambert>), grid, dim3(kBlockThreads), 0,
+    else if (v == 0)
+        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecVariants[0]>), grid, dim3(kBlockThreads), 0,
+                           c->stream, c->dev, F);
+    else if (v == 1)
+        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecVariants[1]>), grid, dim3(kBlockThreads), 0,
+                           c->stream, c->dev, F);
+    else if (v == 2)
+        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecVariants[2]>), grid, dim3(kBlockThreads), 0,
+                           c->stream, c->dev, F);
+    else if (v == 3)
+        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecVariants[3]>), grid, dim3(kBlockThreads), 0,
                            c->stream, c->dev, F);
     else
         hipLaunchKernelGGL((rtx_render_kernel<false, 0>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);

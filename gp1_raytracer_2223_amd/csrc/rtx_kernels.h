@@ -35,13 +35,31 @@ constexpr int kMaxHeavyTiles = 8192;   // heavy wave tiles per frame (hit-key bu
 constexpr int kSplitPermille = 1500;
 constexpr int kMaxSplitLights = 32;    // occlusion bits per pixel
 // Kernel specialisation (rtx_render_kernel's SPEC): uniform facts compiled in.
-constexpr int kSpecLambert = 1;        // every material referenced by geometry is Material_Lambert
-constexpr int kSpecPoint = 2;          // every light is a point light
-constexpr int kSpecNoSpheres = 4;      // no spheres
-constexpr int kSpecCombShadows = 8;    // lighting mode Combined, shadows on
-constexpr int kSpecFivePlanes = 16;    // exactly 5 planes (the reference's room: W3, W4, the synthetic scenes)
-constexpr int kSpecOneMesh = 32;       // exactly 1 triangle mesh
-constexpr int kSpecAll = 63;
+// Bits 0-3: the material kinds the geometry references (bit RTX_MAT_*; none set = any kind).
+constexpr int kSpecKindSolid = 1 << 0;
+constexpr int kSpecKindLambert = 1 << 1;
+constexpr int kSpecKindPhong = 1 << 2;
+constexpr int kSpecKindCT = 1 << 3;
+constexpr int kSpecKindAll = 15;
+constexpr int kSpecPoint = 16;         // every light is a point light
+constexpr int kSpecNoSpheres = 32;     // no spheres
+constexpr int kSpecCombShadows = 64;   // lighting mode Combined, shadows on
+constexpr int kSpecFivePlanes = 128;   // exactly 5 planes (the reference's room: W3, W4, the synthetic scenes)
+constexpr int kSpecOneMesh = 256;      // exactly 1 triangle mesh
+constexpr int kSpecNoMesh = 512;       // no triangle mesh
+// The compiled variants, most specific first (the launch takes the first one whose facts hold):
+//   0  Lambert only, one mesh, no spheres (W4_Bunny, Synthetic100k, Bunny + 8 lights)
+//   1  Lambert + Cook-Torrance, one mesh, no spheres (W4_Optional)
+//   2  Lambert + Cook-Torrance, spheres, no mesh (W3)
+//   3  Lambert + Cook-Torrance, spheres and meshes (W4_Reference)
+// all with point lights, 5 planes, Combined lighting + shadows.
+constexpr int kSpecCommon = kSpecPoint | kSpecCombShadows | kSpecFivePlanes;
+constexpr int kSpecVariants[] = {
+    kSpecCommon | kSpecKindLambert | kSpecNoSpheres | kSpecOneMesh,
+    kSpecCommon | kSpecKindLambert | kSpecKindCT | kSpecNoSpheres | kSpecOneMesh,
+    kSpecCommon | kSpecKindLambert | kSpecKindCT | kSpecNoMesh,
+    kSpecCommon | kSpecKindLambert | kSpecKindCT,
+};
 
 // Work counters (SURVEY §8(d) cost model; same order as the oracle's).
 enum Counter {
