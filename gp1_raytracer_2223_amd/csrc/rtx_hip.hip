@@ -750,11 +750,11 @@ __device__ __forceinline__ uint32_t q8(float c) {
 // launch, compiled in instead of branched on (same operations, so the same pixels; fewer
 // uniform branches, selects and registers; constant plane / mesh counts unroll their loops:
 // Bunny 74.2 -> 61.2 us with RTX_SPEC_WAVES).
-// Occupancy targets of the specialised kernels.  The fully specialised one needs 46 VGPRs and,
-// asked for 8 waves per SIMD, 78 SGPRs (8 spilled to VGPR lanes, outside the loops): the SGPR
-// file no longer caps it at 7 waves like the generic kernel's 106 SGPRs (Bunny 61.1 -> 60.6 us,
-// Bunny + 8 lights 427 -> 418 us; 10 waves: no gain).  The partial one (non-Lambert
-// materials: 66 VGPRs) stays at 7.
+// Occupancy targets of the specialised kernels.  The variants with a constant mesh count ask for
+// 8 waves per SIMD: the Lambert-only one then needs 47 VGPRs and 78 SGPRs (8 spilled to VGPR
+// lanes, outside the loops), so the SGPR file no longer caps it at 7 waves like the generic
+// kernel's 106 SGPRs (Bunny 61.1 -> 60.6 us, Bunny + 8 lights 427 -> 418 us; 10 waves: no gain);
+// W4_Optional's variant 231 -> 223 us.  The variant with spheres and meshes stays at 7 (8: +4 %).
 #ifndef RTX_SPEC_WAVES
 #define RTX_SPEC_WAVES 8
 #endif
@@ -763,7 +763,7 @@ __device__ __forceinline__ uint32_t q8(float c) {
 #endif
 template <bool COUNT, int PHASE, bool DEEP = false, int SPEC = 0>
 __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
-                                                  : ((SPEC & kSpecKindAll) == kSpecKindLambert
+                                                  : ((SPEC & (kSpecOneMesh | kSpecNoMesh))
                                                          ? RTX_SPEC_WAVES
                                                          : (SPEC ? RTX_SPEC_WAVES_PARTIAL : RTX_MIN_WAVES_PER_EU)))
     rtx_render_kernel(const DevScene S, const FrameArgs F) {
