@@ -31,12 +31,9 @@ def main() -> None:
                                  capture_output=True, text=True).stdout
             notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", str(co)], check=True,
                                    capture_output=True, text=True).stdout
-        for k in KERNELS:
-            m = re.search(rf"<(_Z\d+{k}[^>]*)>:", dis)
-            if not m:
-                continue
-            name = m.group(1)
-            start = m.start()
+        names = sorted(set(re.findall(r"<(_Z\d+rtx_render_kernel[^>]*)>:", dis)))
+        for name in names:
+            start = dis.index(f"<{name}>:")
             body = dis[start:dis.index("s_endpgm", start)]
             ops = collections.Counter()
             for line in body.splitlines():
@@ -50,7 +47,8 @@ def main() -> None:
                         mm = re.search(rf"\.{key}:\s+(\d+)", block)
                         if mm:
                             meta[key] = int(mm.group(1))
-            print(f"{Path(lib).name:28s} {k[-4:-1]:4s} vgpr {meta.get('vgpr_count')} sgpr {meta.get('sgpr_count')} "
+            k = re.sub(r"^_Z\d+rtx_render_kernelI(.*)EvN4rtxd.*$", r"\1", name)
+            print(f"{Path(lib).name:28s} {k:22s} vgpr {meta.get('vgpr_count')} sgpr {meta.get('sgpr_count')} "
                   f"scratch {meta.get('private_segment_fixed_size')}  static v_* {ops['valu']} s_* {ops['salu']}")
 
 
