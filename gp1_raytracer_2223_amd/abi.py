@@ -59,6 +59,11 @@ class Material(C.Structure):
                 ("exponent", C.c_float), ("metalness", C.c_float), ("roughness", C.c_float)]
 
 
+class MeshSource(C.Structure):   # rtx_mesh_source (rtx.h): object-space state of an animated mesh
+    _fields_ = [("positions", C.POINTER(C.c_float)), ("n_positions", C.c_uint32),
+                ("normals", C.POINTER(C.c_float)), ("indices", C.POINTER(C.c_int32)), ("n_indices", C.c_uint32)]
+
+
 class Scene(C.Structure):
     _fields_ = [("spheres", C.POINTER(Sphere)), ("n_spheres", C.c_uint32),
                 ("planes", C.POINTER(Plane)), ("n_planes", C.c_uint32),
@@ -129,6 +134,12 @@ def load_host() -> C.CDLL:
         lib.rtx_host_parse_obj.restype = C.c_int
         lib.rtx_host_obj_to_asset.argtypes = [C.c_char_p, C.c_char_p]
         lib.rtx_host_obj_to_asset.restype = C.c_int
+        lib.rtx_host_scene_spinning.argtypes = [VP, C.POINTER(C.c_int32), C.c_uint32]
+        lib.rtx_host_scene_spinning.restype = C.c_int
+        lib.rtx_host_scene_mesh_source.argtypes = [VP, C.c_uint32, C.POINTER(MeshSource)]
+        lib.rtx_host_scene_mesh_source.restype = C.c_int
+        lib.rtx_host_scene_transforms.argtypes = [VP, C.c_float, C.POINTER(C.c_float)]
+        lib.rtx_host_scene_transforms.restype = C.c_int
         _host = lib
     return _host
 
@@ -139,7 +150,9 @@ HIP_SYMBOLS = ["rtx_abi_version", "rtx_create", "rtx_destroy", "rtx_last_error",
                "rtx_render_views_async", "rtx_time_views", "rtx_count_work_ex", "rtx_split_info",
                "rtx_gather_async", "rtx_host_register", "rtx_host_unregister",
                "rtx_group_create", "rtx_group_destroy", "rtx_group_last_error", "rtx_group_size",
-               "rtx_group_context", "rtx_group_upload_scene", "rtx_group_render", "rtx_schedule_state"]
+               "rtx_group_context", "rtx_group_upload_scene", "rtx_group_render", "rtx_schedule_state",
+               "rtx_anim_create", "rtx_anim_destroy", "rtx_anim_last_error", "rtx_anim_update", "rtx_anim_status",
+               "rtx_anim_download", "rtx_scene_image", "rtx_anim_stamps"]
 
 
 def load_hip() -> C.CDLL:
@@ -218,6 +231,26 @@ def load_hip() -> C.CDLL:
             lib.rtx_group_render.argtypes = [VP, C.POINTER(Camera), C.POINTER(RenderParams), C.POINTER(C.c_uint32),
                                              C.POINTER(C.c_float)]
             lib.rtx_group_render.restype = C.c_int
+        if hasattr(lib, "rtx_scene_image"):
+            lib.rtx_scene_image.argtypes = [VP, VP, C.c_size_t, C.POINTER(C.c_size_t)]
+            lib.rtx_scene_image.restype = C.c_int
+        if hasattr(lib, "rtx_anim_create"):   # absent only in older experiment builds
+            lib.rtx_anim_create.argtypes = [C.POINTER(VP), VP, C.POINTER(Scene), C.POINTER(C.c_int32),
+                                            C.POINTER(MeshSource), C.c_uint32]
+            lib.rtx_anim_create.restype = C.c_int
+            lib.rtx_anim_destroy.argtypes = [VP]
+            lib.rtx_anim_destroy.restype = None
+            lib.rtx_anim_last_error.argtypes = [VP]
+            lib.rtx_anim_last_error.restype = C.c_char_p
+            lib.rtx_anim_update.argtypes = [VP, VP, C.POINTER(C.c_float)]
+            lib.rtx_anim_update.restype = C.c_int
+            lib.rtx_anim_status.argtypes = [VP, C.c_uint32, C.POINTER(C.c_uint32)]
+            lib.rtx_anim_status.restype = C.c_int
+            lib.rtx_anim_download.argtypes = [VP, C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_int32),
+                                              C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(BVHNode)]
+            lib.rtx_anim_download.restype = C.c_int
+            lib.rtx_anim_stamps.argtypes = [VP, C.c_uint32, C.POINTER(C.c_uint32)]
+            lib.rtx_anim_stamps.restype = C.c_int
         _hip = lib
     return _hip
 

@@ -73,6 +73,44 @@ extern "C" int rtx_host_scene_animated(const rtx_host_scene* s) {
     return s->scene->Animated() ? 1 : 0;
 }
 
+extern "C" int rtx_host_scene_spinning(rtx_host_scene* s, int32_t* mesh_ids, uint32_t capacity) {
+    if (!s) return RTX_E_INVALID;
+    const auto spin = s->scene->Spinning();
+    for (size_t i = 0; i < spin.size() && i < capacity && mesh_ids; ++i) {
+        int32_t id = -1;
+        for (size_t k = 0; k < s->scene->m_Meshes.size(); ++k)
+            if (s->scene->m_Meshes[k].get() == spin[i]) id = static_cast<int32_t>(k);
+        mesh_ids[i] = id;
+    }
+    return static_cast<int>(spin.size());
+}
+
+extern "C" int rtx_host_scene_mesh_source(rtx_host_scene* s, uint32_t mesh, rtx_mesh_source* out) {
+    if (!s || !out || mesh >= s->scene->m_Meshes.size()) return RTX_E_INVALID;
+    const rtx::TriangleMesh& m = *s->scene->m_Meshes[mesh];
+    if (m.normals.size() * 3 < m.indices.size()) return RTX_E_INVALID;
+    out->positions = m.positions.empty() ? nullptr : &m.positions[0].x;
+    out->n_positions = static_cast<uint32_t>(m.positions.size());
+    out->normals = m.normals.empty() ? nullptr : &m.normals[0].x;
+    out->indices = m.indices.empty() ? nullptr : m.indices.data();
+    out->n_indices = static_cast<uint32_t>(m.indices.size());
+    return RTX_OK;
+}
+
+extern "C" int rtx_host_scene_transforms(rtx_host_scene* s, float total_time, float* out) {
+    if (!s || !out) return RTX_E_INVALID;
+    const float yaw = rtx::Scene::SpinYaw(total_time);
+    int i = 0;
+    for (rtx::TriangleMesh* m : s->scene->Spinning()) {
+        m->RotateY(yaw);
+        const rtx::Mat4 f = m->scaleTransform * m->rotationTransform * m->translationTransform;   // DataTypes.h:213
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 4; ++c) out[16 * i + 4 * r + c] = f.d[r].at(c);
+        ++i;
+    }
+    return i;
+}
+
 extern "C" int rtx_host_camera_set(rtx_host_scene* s, const float origin[3], float fov_degrees, float pitch,
                                    float yaw) {
     if (!s || !origin) return RTX_E_INVALID;

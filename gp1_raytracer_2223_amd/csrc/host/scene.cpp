@@ -768,6 +768,8 @@ rtx_scene Scene::View() {
     return s;
 }
 
+float Scene::SpinYaw(float t) { return (cosf(t) + 1.f) / 2.f * kPi2; }   // Scene.cpp:394
+
 // ---------------------------------------------------------------- catalogue
 namespace {
 
@@ -876,7 +878,7 @@ protected:
         AddPointLight({-2.5f, 5.f, -5.f}, 70.f, Color{1.f, 0.8f, 0.45f});
         AddPointLight({2.5f, 2.5f, -5.f}, 50.f, Color{0.34f, 0.47f, 0.68f});
     }
-    static float Yaw(float t) { return (cosf(t) + 1.f) / 2.f * kPi2; }   // Scene.cpp:394
+    static float Yaw(float t) { return SpinYaw(t); }
 };
 
 // Scene.cpp:245-286
@@ -946,6 +948,11 @@ public:
         const float yaw = Yaw(t);
         for (auto& m : m_Meshes) { m->RotateY(yaw); m->UpdateTransforms(); }
     }
+    std::vector<TriangleMesh*> Spinning() override {
+        std::vector<TriangleMesh*> v;
+        for (auto& m : m_Meshes) v.push_back(m.get());
+        return v;
+    }
 };
 
 // Scene.cpp:402-437
@@ -973,6 +980,7 @@ public:
         m_Meshes[0]->RotateY(Yaw(t));
         m_Meshes[0]->UpdateTransforms();
     }
+    std::vector<TriangleMesh*> Spinning() override { return {m_Meshes[0].get()}; }
 };
 
 // Bunny + 5 lights at (3.5cos θk, 5.5, 3.5 sin θk − 2), θk = 2πk/5,
@@ -1017,6 +1025,7 @@ public:
         m_Meshes[0]->RotateY(Yaw(t));
         m_Meshes[0]->UpdateTransforms();
     }
+    std::vector<TriangleMesh*> Spinning() override { return {m_Meshes[0].get()}; }
 };
 
 // 250 x 200-quad height field = 100,000 triangles over
@@ -1115,6 +1124,7 @@ public:
     void Update(float t) override {
         for (TriangleMesh* m : m_Spin) { m->RotateY(Yaw(t)); m->UpdateTransforms(); }
     }
+    std::vector<TriangleMesh*> Spinning() override { return m_Spin; }
 
 private:
     static bool F(const std::vector<std::string>& t, size_t i, float& out) {

@@ -133,6 +133,10 @@ public:
     virtual bool Initialize() = 0;
     virtual void Update(float totalTime) { (void)totalTime; }   // animated meshes only
     virtual bool Animated() const { return false; }             // Update moves geometry
+    // The meshes Update(t) turns (RotateY(Yaw(t)) then UpdateTransforms), in mesh order, and
+    // that yaw (Scene.cpp:394): the device-side Update (rtx_anim_*) applies the same turn.
+    virtual std::vector<TriangleMesh*> Spinning() { return {}; }
+    static float SpinYaw(float t);
     Camera& GetCamera() { return m_Camera; }
     const std::string& Name() const { return sceneName; }
     const std::string& Error() const { return m_Error; }

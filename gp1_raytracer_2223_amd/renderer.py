@@ -146,6 +146,72 @@ class DeviceGroup:
         return px, rgb
 
 
+class DeviceAnimation:
+    """Owns one rtx_anim: Scene::Update of a host scene's turning meshes done on the device
+    (transform, the reference's binned-SAH rebuild, scene image) — SURVEY §8(f)1.
+    `DeviceAnimation(scene, ctx)` registers the scene's current state and uploads it to
+    `ctx`; `update(t, ctx)` queues Update(t) into `ctx`'s scene image."""
+
+    def __init__(self, scene, ctx: DeviceContext):
+        self.lib = abi.load_hip()
+        self.scene = scene
+        ids = scene.spinning()
+        if not ids:
+            raise ValueError(f"scene {scene.name!r} has no turning mesh")
+        s, _ = scene.view()
+        srcs = (abi.MeshSource * len(ids))(*[scene.mesh_source(i) for i in ids])
+        cids = (C.c_int32 * len(ids))(*ids)
+        h = C.c_void_p()
+        rc = self.lib.rtx_anim_create(C.byref(h), ctx.h, C.byref(s), cids, srcs, len(ids))
+        if rc != abi.RTX_OK:
+            why = (self.lib.rtx_anim_last_error(None) or b"").decode(errors="replace")
+            raise RuntimeError(f"rtx_anim_create failed with code {rc}: {why}")
+        self.h = h
+        self.mesh_ids = list(ids)
+        self.n_tris = [s.meshes[i].n_indices // 3 for i in ids]
+        self.n_positions = [s.meshes[i].n_positions for i in ids]
+
+    def _check(self, rc, what):
+        if rc != abi.RTX_OK:
+            why = (self.lib.rtx_anim_last_error(self.h) or b"").decode(errors="replace")
+            raise RuntimeError(f"{what} failed with code {rc}: {why}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.rtx_anim_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def update(self, total_time: float, ctx: DeviceContext) -> None:
+        m = self.scene.transforms(total_time)
+        self._check(self.lib.rtx_anim_update(self.h, ctx.h, m.ctypes.data_as(C.POINTER(C.c_float))),
+                    "rtx_anim_update")
+
+    def status(self, i: int = 0) -> np.ndarray:
+        st = (C.c_uint32 * 4)()
+        self._check(self.lib.rtx_anim_status(self.h, i, st), "rtx_anim_status")
+        return np.array(list(st), np.uint32)
+
+    def download(self, i: int = 0) -> dict:
+        """Registered mesh i in the reference's form (TriangleMesh after UpdateTransforms)."""
+        T, V = self.n_tris[i], self.n_positions[i]
+        pos = np.zeros(3 * V, np.float32)
+        idx = np.zeros(3 * T, np.int32)
+        nrm = np.zeros(3 * T, np.float32)
+        tn = np.zeros(3 * T, np.float32)
+        nodes = (abi.BVHNode * (3 * T))()
+        f = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))  # noqa: E731
+        self._check(self.lib.rtx_anim_download(self.h, i, f(pos), idx.ctypes.data_as(C.POINTER(C.c_int32)), f(nrm),
+                                               f(tn), nodes), "rtx_anim_download")
+        raw = np.ctypeslib.as_array(C.cast(nodes, C.POINTER(C.c_uint32)), shape=(3 * T * 9,)).copy().reshape(-1, 9)
+        return {"tpositions": pos, "indices": idx, "normals": nrm, "tnormals": tn, "nodes": raw}
+
+
 class Renderer:
     def __init__(self, width: int, height: int, device: int = 0, stripe: tuple[int, int, int] | None = None,
                  pixel_format=abi.XRGB8888):

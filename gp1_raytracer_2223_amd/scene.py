@@ -57,6 +57,29 @@ class HostScene:
             abi.check(r, "rtx_host_scene_animated")
         return bool(r)
 
+    # ---- device-side Update (rtx_anim_*) ------------------------------------------
+    def spinning(self) -> list[int]:
+        """Indices of the meshes Update(t) turns."""
+        ids = (C.c_int32 * 64)()
+        n = self._lib.rtx_host_scene_spinning(self._h, ids, 64)
+        if n < 0:
+            abi.check(n, "rtx_host_scene_spinning")
+        return [int(ids[i]) for i in range(min(n, 64))]
+
+    def mesh_source(self, mesh: int) -> abi.MeshSource:
+        """Object-space state of a mesh (pointers into the scene, valid until its next update)."""
+        src = abi.MeshSource()
+        abi.check(self._lib.rtx_host_scene_mesh_source(self._h, mesh, C.byref(src)), "rtx_host_scene_mesh_source")
+        return src
+
+    def transforms(self, total_time: float) -> np.ndarray:
+        """Update(t)'s finalTransform per turning mesh (16 floats each) without rebuilding."""
+        out = np.zeros(16 * 64, np.float32)
+        n = self._lib.rtx_host_scene_transforms(self._h, float(total_time), out.ctypes.data_as(C.POINTER(C.c_float)))
+        if n < 0:
+            abi.check(n, "rtx_host_scene_transforms")
+        return out[: 16 * n].copy()
+
     def set_camera(self, origin, fov_degrees: float = 45.0, pitch: float = 0.0, yaw: float = 0.0) -> None:
         o = (C.c_float * 3)(*origin)
         abi.check(self._lib.rtx_host_camera_set(self._h, o, fov_degrees, pitch, yaw), "rtx_host_camera_set")

@@ -223,6 +223,9 @@ int rtx_time_views(rtx_ctx* ctx, const rtx_camera* cams, int n_views, const rtx_
                    int iters, float* mean_ms);
 /* Bytes of HBM the uploaded scene image occupies. */
 int rtx_scene_bytes(const rtx_ctx* ctx, uint64_t* bytes);
+/* Diagnostics: copy the context's current scene image (DESIGN.md §2 layout) after its queued
+ * work; `bytes` gets the image size (out may be NULL to query it). */
+int rtx_scene_image(rtx_ctx* ctx, void* out, size_t capacity, size_t* bytes);
 /* Instrumented render: the same traversal with per-ray work counters (12 x uint64, in
  * the order pixels, sphere, plane, slab, tri, hit, shadow, occluded, shade_base,
  * shade_lambert, shade_phong, shade_ct — the SURVEY §8(d) FLOP model).  Not timed. */
@@ -267,6 +270,49 @@ int rtx_group_upload_scene(rtx_group* group, const rtx_scene* scene);
  * (the group assigns the stripes).  out_pixels: width*height uint32; out_rgb may be NULL. */
 int rtx_group_render(rtx_group* group, const rtx_camera* cam, const rtx_render_params* params,
                      uint32_t* out_pixels, float* out_rgb);
+
+/* ---- animated meshes: Scene::Update on the device -------------------
+ * Replaces, per animated frame, the host's TriangleMesh::UpdateTransforms + BuildBVH
+ * (source/DataTypes.h:210-236, 294-483, called from Scene_W4_*::Update, Scene.cpp:391-400,
+ * 431-437, 468-474) followed by rtx_upload_scene: the transform, the reference's binned-SAH
+ * rebuild (bit-identical node array and triangle permutation, which the next Update starts
+ * from) and the scene image are produced in HBM by one workgroup per mesh. */
+/* The object-space state UpdateTransforms starts from: positions (never permuted), the
+ * per-triangle normals and the index array in the order the last BuildBVH left them. */
+typedef struct rtx_mesh_source {
+    const float* positions;   /* 3 * n_positions floats, object space                   */
+    uint32_t n_positions;
+    const float* normals;     /* 3 per triangle, object space (TriangleMesh::normals)    */
+    const int32_t* indices;   /* n_indices = 3 * triangles                               */
+    uint32_t n_indices;
+} rtx_mesh_source;
+typedef struct rtx_anim rtx_anim;
+/* Register meshes mesh_ids[0..n) of `scene` (its current flattened state, what
+ * rtx_upload_scene takes) as device-animated, with their object-space state src[0..n), and
+ * upload the scene to `ctx` with rebuild-sized regions reserved for them.  n <= 8; the
+ * meshes must be NaN-free with BVHs under 40 levels. */
+int rtx_anim_create(rtx_anim** out, rtx_ctx* ctx, const rtx_scene* scene, const int32_t* mesh_ids,
+                    const rtx_mesh_source* src, uint32_t n);
+void rtx_anim_destroy(rtx_anim* anim);
+/* Reason for the anim's last error; with NULL, why this thread's last create failed. */
+const char* rtx_anim_last_error(const rtx_anim* anim);
+/* One Update: registered mesh i gets finalTransform = transforms[16 i .. 16 i + 15] (the
+ * reference's Matrix, data[0..3] row-major).  Queued on ctx's stream after the previous
+ * update (whichever context on the anim's device ran it); frames rendered on ctx
+ * afterwards see the new geometry.  Build errors are reported by rtx_anim_status. */
+int rtx_anim_update(rtx_anim* anim, rtx_ctx* ctx, const float* transforms);
+/* Waits for the last update.  status = {error bits (1: NaN vertex, 2: BVH too deep for the
+ * render stack; the frames rendered from it are invalid), deepest level, nodesUsed,
+ * frontier parts}; returns RTX_E_UNSUPPORTED when error bits are set. */
+int rtx_anim_status(rtx_anim* anim, uint32_t i, uint32_t status[4]);
+/* Waits for the last update and copies registered mesh i's state in the reference's own
+ * form: transformedPositions (3V), indices (3T), normals (object space, 3T),
+ * transformedNormals (3T), the node array pBVHNodes (3T entries).  NULL skips a part. */
+/* Diagnostics: 128 status words of the last update of registered mesh i (0-3 as above,
+ * 8-62 phase stamps of the device build at 100 MHz). */
+int rtx_anim_stamps(rtx_anim* anim, uint32_t i, uint32_t out[128]);
+int rtx_anim_download(rtx_anim* anim, uint32_t i, float* positions, int32_t* indices, float* normals,
+                      float* transformed_normals, rtx_bvh_node* nodes);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,179 @@
+"""Scene::Update on the device (rtx_anim_*): the transform and the reference's
+binned-SAH rebuild of the turning meshes run in HBM (csrc/rtx_anim.hip) and write the scene
+image directly.  Checked against the host layer's Update, which is itself bit-identical to
+the reference (tests/test_host_scene.py, test_host_sequence.py):
+  * after each of a sequence of Updates, the device state equals the host's bit for bit —
+    transformedPositions, the permuted indices and normals, transformedNormals, the node
+    array (every field the reference writes; a leaf's leftNode is the stale value the
+    reference leaves there) — so the chain of permutations is followed exactly;
+  * frames rendered from the device-built image equal frames of the host-built upload,
+    pixels and float planes, including cost-ordered / split frames, and the oracle's;
+  * updates alternating over two contexts (frames in flight) chain through one state."""
+import numpy as np
+import pytest
+
+import oracle_bind
+from gp1_raytracer_2223_amd import abi
+from gp1_raytracer_2223_amd.renderer import DeviceAnimation, DeviceContext
+from gp1_raytracer_2223_amd.scene import HostScene
+
+pytestmark = pytest.mark.gpu
+
+SCENES = ["W4_Bunny", "W4_Optional", "W4_Reference", "Bunny8Lights", "file:scenes/gallery.rtxscene"]
+TIMES = [1.3, 2.7, 0.4, 4.1, 5.9, 3.3]
+
+
+def _scene(name):
+    if name.startswith("file:"):
+        from pathlib import Path
+        return HostScene("file:" + str(Path(__file__).resolve().parents[1] / name[5:]))
+    return HostScene(name)
+
+
+def _compare_state(anim, ref_scene, k):
+    got = anim.download(k)
+    mesh = anim.mesh_ids[k]
+    want = ref_scene.arrays()["meshes"][mesh]
+    assert np.array_equal(got["tpositions"].view(np.uint32), want["tpositions"].view(np.uint32))
+    assert np.array_equal(got["indices"], want["indices"])
+    assert np.array_equal(got["tnormals"].view(np.uint32), want["tnormals"].view(np.uint32))
+    src = ref_scene.mesh_source(mesh)
+    T = src.n_indices // 3
+    want_n = np.ctypeslib.as_array(src.normals, shape=(3 * T,)).copy()
+    assert np.array_equal(got["normals"].view(np.uint32), want_n.view(np.uint32))
+    st = anim.status(k)
+    used = int(st[2])
+    wb = want["node_bounds"].reshape(-1, 6)
+    wl = want["node_links"].reshape(-1, 3)
+    assert used == len(wb), f"nodesUsed {used} vs {len(wb)}"
+    gn = got["nodes"][:used]
+    assert np.array_equal(gn[:, :6], wb.view(np.uint32)), "node bounds differ"
+    assert np.array_equal(gn[:, 6:8], wl[:, :2]), "firstIdx / idxCount differ"
+    inner = wl[:, 1] == 0
+    assert np.array_equal(gn[inner, 8], wl[inner, 2]), "leftNode of inner nodes differs"
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_device_update_state_matches_host(gpu_ctx, name):
+    dev_scene, host_scene = _scene(name), _scene(name)
+    anim = DeviceAnimation(dev_scene, gpu_ctx)
+    for t in TIMES:
+        anim.update(t, gpu_ctx)
+        host_scene.update(t)
+        assert list(anim.status(0)[:1]) == [0]
+        for k in range(len(anim.mesh_ids)):
+            _compare_state(anim, host_scene, k)
+    anim.close()
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_device_update_frames_match_host_upload(name):
+    dev_scene, host_scene = _scene(name), _scene(name)
+    a, b = DeviceContext(0), DeviceContext(0)
+    anim = DeviceAnimation(dev_scene, a)
+    p = abi.make_params(480, 270)
+    for t in TIMES[:4]:
+        anim.update(t, a)
+        host_scene.update(t)
+        s, cam = host_scene.view()
+        b.upload(s)
+        for _ in range(3):   # the first frame measures tile costs; later ones run cost-ordered / split
+            apx, argb = a.render(cam, p)
+            bpx, brgb = b.render(cam, p)
+            assert np.array_equal(apx, bpx), f"{name} t={t}: {(apx != bpx).sum()} pixels differ"
+            assert np.array_equal(argb.view(np.uint32), brgb.view(np.uint32))
+    anim.close()
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("name", ["W4_Bunny", "W4_Optional"])
+def test_device_update_matches_oracle_full_resolution(name):
+    """1080p frames from the device-built scene after an Update, cost-ordered and split,
+    against the oracle's render of the host-updated scene (bit-exact on Lambert scenes, within
+    the north-star tolerance where Cook-Torrance's powf is involved)."""
+    dev_scene, host_scene = _scene(name), _scene(name)
+    ctx = DeviceContext(0)
+    anim = DeviceAnimation(dev_scene, ctx)
+    anim.update(1.3, ctx)
+    host_scene.update(1.3)
+    s, cam = host_scene.view()
+    p = abi.make_params(1920, 1080)
+    for _ in range(4):
+        gpx, grgb = ctx.render(cam, p)
+    rpx, rrgb = oracle_bind.render(s, cam, p)
+    if name == "W4_Bunny":
+        assert np.array_equal(gpx, rpx)
+    else:
+        assert float(np.abs(grgb - rrgb).max()) <= 1e-4
+        d = np.abs(gpx.view(np.uint8).astype(np.int16) - rpx.view(np.uint8).astype(np.int16))
+        assert int(d.max()) <= 1
+    anim.close()
+    ctx.close()
+
+
+def test_device_update_frames_in_flight_two_contexts():
+    """Updates alternate between two contexts (frames in flight): each context's image holds
+    the Update it was given, and the permutation chain runs through both."""
+    dev_scene, host_scene = _scene("W4_Optional"), _scene("W4_Optional")
+    a, b, ref = DeviceContext(0), DeviceContext(0), DeviceContext(0)
+    anim = DeviceAnimation(dev_scene, a)
+    p = abi.make_params(320, 180)
+    ctxs = [a, b]
+    for i, t in enumerate(TIMES):
+        c = ctxs[i % 2]
+        anim.update(t, c)
+        host_scene.update(t)
+        s, cam = host_scene.view()
+        ref.upload(s)
+        gpx, _ = c.render(cam, p)
+        rpx, _ = ref.render(cam, p)
+        assert np.array_equal(gpx, rpx), f"update {i} (t={t}) on context {i % 2}"
+    _compare_state(anim, host_scene, 0)
+    anim.close()
+    for c in (a, b, ref):
+        c.close()
+
+
+def _image(ctx):
+    import ctypes as C
+    lib = abi.load_hip()
+    n = C.c_size_t()
+    abi.check(lib.rtx_scene_image(ctx.h, None, 0, C.byref(n)), "rtx_scene_image")
+    buf = np.zeros(n.value // 4, np.uint32)
+    abi.check(lib.rtx_scene_image(ctx.h, buf.ctypes.data, n.value, C.byref(n)), "rtx_scene_image")
+    return buf
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_device_update_image_equals_host_built_image(name):
+    """The whole scene image after device Updates equals, word for word, the image the upload
+    path lays out from the host-updated scene (registration of a second anim = host build)."""
+    d, h = _scene(name), _scene(name)
+    c1, c2 = DeviceContext(0), DeviceContext(0)
+    a1 = DeviceAnimation(d, c1)
+    for t in TIMES[:3]:
+        a1.update(t, c1)
+        h.update(t)
+    a2 = DeviceAnimation(h, c2)
+    i1, i2 = _image(c1), _image(c2)
+    assert len(i1) == len(i2)
+    bad = np.nonzero(i1 != i2)[0]
+    assert len(bad) == 0, f"{len(bad)} words differ, first at byte {4 * bad[0]}"
+    for x in (a1, a2, c1, c2):
+        x.close()
+
+
+def test_anim_create_rejects_bad_input(gpu_ctx):
+    hs = HostScene("W4_Bunny")
+    s, _ = hs.view()
+    lib = abi.load_hip()
+    import ctypes as C
+    h = C.c_void_p()
+    src = (abi.MeshSource * 1)(hs.mesh_source(0))
+    bad = (C.c_int32 * 1)(5)   # no mesh 5
+    assert lib.rtx_anim_create(C.byref(h), gpu_ctx.h, C.byref(s), bad, src, 1) == abi.RTX_E_INVALID
+    assert lib.rtx_anim_last_error(None)
+    ok = (C.c_int32 * 1)(0)
+    assert lib.rtx_anim_create(C.byref(h), gpu_ctx.h, C.byref(s), ok, src, 0) == abi.RTX_E_INVALID
+    assert lib.rtx_anim_create(C.byref(h), gpu_ctx.h, C.byref(s), ok, src, 9) != abi.RTX_OK

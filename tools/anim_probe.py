@@ -1,0 +1,91 @@
+"""Device-side Update probe: frames of the device-built scene vs the host upload, per render
+path switch, and the Update's device time.  Usage (GPU box): python tools/anim_probe.py [scene]"""
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+from gp1_raytracer_2223_amd import abi  # noqa: E402
+
+abi.load_hip()
+from gp1_raytracer_2223_amd.renderer import DeviceAnimation, DeviceContext  # noqa: E402
+from gp1_raytracer_2223_amd.scene import HostScene  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else "W4_Reference"
+W, H = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (480, 270)
+dev, host = HostScene(name), HostScene(name)
+a, b = DeviceContext(0), DeviceContext(0)
+anim = DeviceAnimation(dev, a)
+p = abi.make_params(W, H)
+s, cam = host.view()
+b.upload(s)
+for mode in (3, 0):
+    p.lighting_mode = mode
+    apx, _ = a.render(cam, p)
+    bpx, _ = b.render(cam, p)
+    print(f"registration image, mode {mode}: {(apx != bpx).sum()} px differ, nonzero {np.count_nonzero(apx)}/{np.count_nonzero(bpx)}")
+p.lighting_mode = 3
+for t in (1.3, 2.7):
+    anim.update(t, a)
+    host.update(t)
+    s, cam = host.view()
+    b.upload(s)
+    print("status", anim.status(0))
+    for k in range(3):
+        apx, _ = a.render(cam, p)
+        bpx, _ = b.render(cam, p)
+        print(f"t={t} frame {k}: {(apx != bpx).sum()} px differ, nonzero {np.count_nonzero(apx)}/{np.count_nonzero(bpx)}")
+# device Update cost: back-to-back updates on one context
+a.synchronize()
+for n in (1, 50):
+    t0 = time.perf_counter()
+    for i in range(n):
+        anim.update(0.01 * i, a)
+    anim.status(0)
+    dt = (time.perf_counter() - t0) / n
+    print(f"{name}: {n} device Updates: {dt * 1e3:.3f} ms each (host enqueue + device, serialized)")
+t0 = time.perf_counter()
+for i in range(50):
+    host.update(0.01 * i)
+print(f"{name}: host Update {(time.perf_counter() - t0) / 50 * 1e3:.3f} ms each")
+
+# phase stamps of the last device build (100 MHz)
+st = (C.c_uint32 * 64)() if False else None
+# scene image of the device Update vs the registration (host-built) image of the same state
+import ctypes as C  # noqa: E402
+lib = abi.load_hip()
+
+
+def image(ctx):
+    n = C.c_size_t()
+    abi.check(lib.rtx_scene_image(ctx.h, None, 0, C.byref(n)), "rtx_scene_image")
+    buf = np.zeros(n.value // 4, np.uint32)
+    abi.check(lib.rtx_scene_image(ctx.h, buf.ctypes.data, n.value, C.byref(n)), "rtx_scene_image")
+    return buf
+
+
+d2, h2 = HostScene(name), HostScene(name)
+c1, c2 = DeviceContext(0), DeviceContext(0)
+an1 = DeviceAnimation(d2, c1)
+an1.update(1.3, c1)
+h2.update(1.3)
+an2 = DeviceAnimation(h2, c2)
+i1, i2 = image(c1), image(c2)
+diff = np.nonzero(i1 != i2)[0]
+print(f"image words {len(i1)} / {len(i2)}, differing words {len(diff)}")
+if len(diff):
+    runs = np.split(diff, np.nonzero(np.diff(diff) > 1)[0] + 1)
+    for r in runs[:12]:
+        print(f"  words {r[0]}..{r[-1]} (byte {4 * r[0]}): dev {i1[r[0]:r[0] + 8]} host {i2[r[0]:r[0] + 8]}")
+
+st = (C.c_uint32 * 128)()
+abi.check(lib.rtx_anim_stamps(an1.h, 0, st), "rtx_anim_stamps")
+w = [int(x) for x in st]
+t0 = w[8]
+us = lambda x: (x - t0) / 100.0  # noqa: E731
+lv = [us(w[10 + d]) for d in range(w[1] + 1)]
+print(f"build phases (us from start): setup {us(w[9]):.1f}, levels {[round(x, 1) for x in lv]}, "
+      f"numbered {us(w[60]):.1f}, written {us(w[61]):.1f}, frontier {us(w[62]):.1f}")

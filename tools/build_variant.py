@@ -22,7 +22,8 @@ def main() -> int:
            "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize",
            "-mllvm", "-structurizecfg-skip-uniform-regions=true",
            *([f for f in flags if not any(a.startswith(f.split("=")[0]) for a in args)]), "-fPIC", "-shared",
-           "-Wall", f"-I{ROOT / 'include'}", f"-I{PKG / 'csrc'}", *args, str(src), "-o", str(out)]
+           "-Wall", f"-I{ROOT / 'include'}", f"-I{PKG / 'csrc'}", *args, str(src),
+           str(PKG / "csrc" / "rtx_anim.hip"), str(PKG / "csrc" / "rtx_group.cpp"), "-o", str(out)]
     print(" ".join(cmd[-4:]), flush=True)
     return subprocess.call(cmd)
 
