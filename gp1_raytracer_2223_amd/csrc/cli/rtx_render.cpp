@@ -4,6 +4,7 @@
 //
 //   rtx_render <scene> [width height] [--time T] [--mode 0..3] [--no-shadows]
 //              [--frames N] [--out file.bmp] [--assets dir] [--benchmark [windows]] [--inflight F]
+//              [--device-update]
 //
 // --benchmark runs the reference's frame loop (main.cpp:86-100: Scene::Update with the
 // timer's total time, Render into the host pixel buffer, Timer::Update) under its F6
@@ -64,9 +65,11 @@ struct Benchmark {
 // behind the current frame's GPU work.  Every frame is still fully rendered and in host
 // memory before it counts: the benchmark ticks when frame k's context has finished.
 // inflight = 1 is the reference's serial loop.
+// --device-update: the animated meshes' Update (transform + BVH rebuild + scene image) runs on
+// the device (rtx_anim_*); the host only computes the frame's transforms.
 // With `seq` (--sequence t1,t2,...): no timer; frame k is Update(seq[k]) and is written to
 // `<stem>_<k>.bmp` when it completes (the pipelined loop's frames, checked by the tests).
-int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int inflight,
+int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int inflight, bool device_update,
                   const std::vector<float>* seq = nullptr, const std::string& stem = "") {
     const bool animated = rtx_host_scene_animated(hs) == 1;
     const size_t npx = static_cast<size_t>(r.Width()) * r.Height();
@@ -98,6 +101,22 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
         rc = 1;
         return false;
     };
+    // device-side Update: register the scene's turning meshes on the first context
+    rtx_anim* anim = nullptr;
+    std::vector<float> mats;
+    if (device_update && animated) {
+        std::vector<int32_t> ids(64);
+        const int ns = rtx_host_scene_spinning(hs, ids.data(), 64);
+        std::vector<rtx_mesh_source> src(ns > 0 ? ns : 0);
+        for (int i = 0; i < ns; ++i) rtx_host_scene_mesh_source(hs, static_cast<uint32_t>(ids[i]), &src[i]);
+        rtx_host_scene_view(hs, &s, &cam);
+        if (ns <= 0 || rtx_anim_create(&anim, ctx[0], &s, ids.data(), src.data(), static_cast<uint32_t>(ns)) != RTX_OK) {
+            std::fprintf(stderr, "rtx_anim_create: %s\n", rtx_anim_last_error(nullptr));
+            for (size_t i = 1; i < ctx.size(); ++i) rtx_destroy(ctx[i]);
+            return 1;
+        }
+        mats.resize(16 * static_cast<size_t>(ns));
+    }
     for (;;) {
         const int f = static_cast<int>(queued % inflight);
         if (queued >= inflight) {   // frame queued - inflight (this context's) completes
@@ -122,10 +141,20 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
             continue;
         }
         const Clock::time_point f0 = Clock::now();
-        if (animated) rtx_host_scene_update(hs, seq ? (*seq)[queued] : static_cast<float>(secs(start, f0)));  // Scene::Update
+        const float tnow = seq ? (*seq)[queued] : static_cast<float>(secs(start, f0));
+        if (anim) rtx_host_scene_transforms(hs, tnow, mats.data());   // the turn Update(t) applies
+        else if (animated) rtx_host_scene_update(hs, tnow);                // Scene::Update
         const Clock::time_point f1 = Clock::now();
         if (!ok(rtx_host_scene_view(hs, &s, &cam), "rtx_host_scene_view", nullptr)) break;
-        if ((animated || queued < inflight) && !ok(rtx_upload_scene(ctx[f], &s), "rtx_upload_scene", ctx[f])) break;
+        if (anim) {
+            if (rtx_anim_update(anim, ctx[f], mats.data()) != RTX_OK) {
+                std::fprintf(stderr, "rtx_anim_update: %s\n", rtx_anim_last_error(anim));
+                rc = 1;
+                break;
+            }
+        } else if ((animated || queued < inflight) && !ok(rtx_upload_scene(ctx[f], &s), "rtx_upload_scene", ctx[f])) {
+            break;
+        }
         const Clock::time_point f2 = Clock::now();
         if (!ok(rtx_render_async(ctx[f], &cam, &p, 0), "rtx_render_async", ctx[f])) break;  // Renderer::Render
         if (!ok(rtx_gather_async(ctx[f], buf[f].data(), nullptr), "rtx_gather_async", ctx[f])) break;
@@ -136,6 +165,14 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
         ++queued;
     }
     for (int f = 0; f < inflight; ++f) rtx_synchronize(ctx[f]);
+    if (anim) {
+        uint32_t st[4];
+        if (rtx_anim_status(anim, 0, st) != RTX_OK) {
+            std::fprintf(stderr, "device Update failed: %s\n", rtx_anim_last_error(anim));
+            rc = 1;
+        }
+        rtx_anim_destroy(anim);
+    }
     if (last >= 0) r.Pixels() = buf[last];   // the last completed frame (SaveBufferToImage)
     for (int f = 0; f < inflight; ++f) rtx_host_unregister(ctx[f], buf[f].data());
     for (size_t i = 1; i < ctx.size(); ++i) rtx_destroy(ctx[i]);
@@ -150,8 +187,9 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
     out << "LOW = " << b.low << std::endl;
     out << "AVG = " << b.avg << std::endl;
     const double n = static_cast<double>(queued);
-    std::printf("frames %ld%s, %d in flight: per frame update %.3f ms, upload %.3f ms, queue %.3f ms, "
-                "wait for GPU %.3f ms\n", frames, animated ? " (animated)" : "", inflight, t_update / n * 1e3,
+    std::printf("frames %ld%s%s, %d in flight: per frame update %.3f ms, upload %.3f ms, queue %.3f ms, "
+                "wait for GPU %.3f ms\n", frames, animated ? " (animated)" : "", device_update ? " device Update" : "",
+                inflight, t_update / n * 1e3,
                 t_upload / n * 1e3, t_queue / n * 1e3, t_wait / std::max(1.0, double(frames)) * 1e3);
     return 0;
 }
@@ -161,14 +199,15 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s <scene> [width height] [--time T] [--mode M] [--no-shadows] [--frames N] "
-                             "[--out f.bmp] [--assets dir] [--benchmark [windows]] [--inflight F]\n", argv[0]);
+                             "[--out f.bmp] [--assets dir] [--benchmark [windows]] [--inflight F] [--device-update]\n",
+                     argv[0]);
         return 2;
     }
     std::string scene = argv[1], out = "RayTracing_Buffer.bmp", assets;
     int W = 640, H = 480, mode = 3, frames = 1, bench = 0, inflight = 2;
     std::vector<float> seq;
     float t = -1.f;
-    bool shadows = true;
+    bool shadows = true, device_update = false;
     int pos = 0;
     for (int i = 2; i < argc; ++i) {
         std::string a = argv[i];
@@ -185,6 +224,7 @@ int main(int argc, char** argv) {
             }
         }
         else if (a == "--inflight" && i + 1 < argc) inflight = std::max(1, std::min(8, std::atoi(argv[++i])));
+        else if (a == "--device-update") device_update = true;
         else if (a == "--out" && i + 1 < argc) out = argv[++i];
         else if (a == "--assets" && i + 1 < argc) assets = argv[++i];
         else if (a == "--benchmark") bench = (i + 1 < argc && std::atoi(argv[i + 1]) > 0) ? std::atoi(argv[++i]) : 10;
@@ -207,12 +247,12 @@ int main(int argc, char** argv) {
             // --sequence t1,...: the pipelined frame loop over fixed Update times, frame k
             // written to <out stem>_<k>.bmp
             const std::string stem = out.size() > 4 && out.substr(out.size() - 4) == ".bmp" ? out.substr(0, out.size() - 4) : out;
-            rc = run_benchmark(r, hs, 0, inflight, &seq, stem);
+            rc = run_benchmark(r, hs, 0, inflight, device_update, &seq, stem);
             rtx_host_scene_destroy(hs);
             return rc;
         }
         if (bench) {
-            rc = run_benchmark(r, hs, bench, inflight);
+            rc = run_benchmark(r, hs, bench, inflight, device_update);
         } else {
             r.Render(hs, true);
             auto t0 = Clock::now();

@@ -21,8 +21,8 @@ constexpr int kAnimThreads = 512;                // one workgroup per mesh
 constexpr int kAnimWaves = kAnimThreads / 64;
 constexpr int kMaxAnimMeshes = 8;                // animated meshes per launch
 constexpr int kMaxAnimParts = 128;               // frontier entries per mesh (kPartsPerMesh)
-constexpr int kLdsWordsPerTri = 11;              // 9 build floats + 2 permutation words
-constexpr int kLdsTris = 3456;                   // meshes up to this size build from LDS (149 KB + 3.6 KB static)
+constexpr int kLdsBytesPerTri = 50;              // 9 build floats, 2 permutation words, 3 16-bit ranks
+constexpr int kLdsTris = 3136;                   // meshes up to this size build from LDS (153 KB + 3.6 KB static)
 
 // A node of the build tree before the reference's numbering (64 B).
 struct alignas(16) TmpNode {

@@ -18,6 +18,7 @@
 
 #include <cfloat>
 #include <cstdint>
+#include <type_traits>
 
 #include "rtx_anim.h"
 #include "rtx_kernels.h"
@@ -56,17 +57,20 @@ __device__ __forceinline__ float area(const float lo[3], const float hi[3]) {   
 
 // The build arrays by triangle id and the two permutation buffers, in the workgroup's LDS
 // (meshes up to kLdsTris triangles) or in HBM (MeshDev::soa / perm): generic pointers.
+template <class S>   // S: the partition scratch type (16-bit in LDS, 32-bit in HBM)
 struct Arr {
     float *cx, *cy, *cz;         // centroid (v0 + v1 + v2) * 0.3333f
     float *lx, *ly, *lz;         // triangle box min(min(v0, v1), v2)
     float *hx, *hy, *hz;         //              max(max(v0, v1), v2)
     uint32_t* perm[2];           // build position -> triangle id
+    S *lb, *rs, *rk;             // partition scratch: left bigs / right smalls by rank, rank by position
     __device__ float c(int ax, uint32_t id) const { return ax == 0 ? cx[id] : (ax == 1 ? cy[id] : cz[id]); }
 };
 
 struct Bounds {
     float l0 = FLT_MAX, l1 = FLT_MAX, l2 = FLT_MAX, h0 = FLT_MIN, h1 = FLT_MIN, h2 = FLT_MIN;
-    __device__ void grow(const Arr& A, uint32_t id) {   // UpdateNodeBounds over one triangle
+    template <class AR>
+    __device__ void grow(const AR& A, uint32_t id) {   // UpdateNodeBounds over one triangle
         l0 = rmin(l0, A.lx[id]); l1 = rmin(l1, A.ly[id]); l2 = rmin(l2, A.lz[id]);
         h0 = rmax(h0, A.hx[id]); h1 = rmax(h1, A.hy[id]); h2 = rmax(h2, A.hz[id]);
     }
@@ -101,8 +105,8 @@ struct Team {
 // Bounds of the triangle boxes at build positions [a, b) (UpdateNodeBounds: a triangle's box
 // min(min(v0, v1), v2) grows a node exactly as its three vertices in order do); team lane 0
 // ends with the fold of the whole range (lane i absorbs the later chunk of lane i + off).
-template <int G>
-__device__ __forceinline__ Bounds team_bounds(const Team<G>& tm, const Arr& A, const uint32_t* perm, uint32_t a,
+template <int G, class AR>
+__device__ __forceinline__ Bounds team_bounds(const Team<G>& tm, const AR& A, const uint32_t* perm, uint32_t a,
                                               uint32_t b) {
     Bounds B;
     uint32_t s, e;
@@ -141,7 +145,8 @@ struct Bins {
             bc[q] = 0u;
         }
     }
-    __device__ void add(const Arr& A, uint32_t id, int ax, float minBounds, float scale) {
+    template <class AR>
+    __device__ void add(const AR& A, uint32_t id, int ax, float minBounds, float scale) {
         const float x = (A.c(ax, id) - minBounds) * scale;
         // static_cast<int> of x >= 0 (a NaN x only comes from a NaN vertex: flagged, bin 0)
         int bi = x >= 0.f ? static_cast<int>(fminf(x, 2147483520.f)) : 0;
@@ -202,8 +207,8 @@ struct Bins {
 
 // Centroid bounds of positions [a, b): min from FLT_MAX, max from FLT_MIN (the reference's
 // minBounds / maxBounds, DataTypes.h:404-419), the three axes in one fold; valid in lane 0.
-template <int G>
-__device__ __forceinline__ Bounds team_centroid_bounds(const Team<G>& tm, const Arr& A, const uint32_t* perm,
+template <int G, class AR>
+__device__ __forceinline__ Bounds team_centroid_bounds(const Team<G>& tm, const AR& A, const uint32_t* perm,
                                                        uint32_t a, uint32_t b) {
     Bounds C;
     uint32_t s, e;
@@ -227,8 +232,8 @@ __device__ __forceinline__ Bounds team_centroid_bounds(const Team<G>& tm, const 
 }
 
 // One axis's bins over positions [a, b); valid in team lane 0.
-template <int G>
-__device__ __forceinline__ void team_bins(const Team<G>& tm, const Arr& A, const uint32_t* perm, uint32_t a,
+template <int G, class AR>
+__device__ __forceinline__ void team_bins(const Team<G>& tm, const AR& A, const uint32_t* perm, uint32_t a,
                                           uint32_t b, int ax, float minBounds, float scale, Bins& bins) {
     bins.clear();
     uint32_t s, e;
@@ -257,8 +262,8 @@ __device__ __forceinline__ void team_bins(const Team<G>& tm, const Arr& A, const
 
 // FindBestSplitPlane (DataTypes.h:398-483) for the node at [a, a + n) by one team: the best
 // cost (FLT_MAX when no axis is live) with axis / pos, uniform over the team.
-template <int G>
-__device__ __forceinline__ float team_best_split(const Team<G>& tm, const Arr& A, const uint32_t* perm, uint32_t a,
+template <int G, class AR>
+__device__ __forceinline__ float team_best_split(const Team<G>& tm, const AR& A, const uint32_t* perm, uint32_t a,
                                                  uint32_t n, int& axis, float& pos) {
     const Bounds C = team_first(tm, team_centroid_bounds(tm, A, perm, a, a + n));
     const float cl[3] = {C.l0, C.l1, C.l2}, ch[3] = {C.h0, C.h1, C.h2};
@@ -290,8 +295,8 @@ __device__ __forceinline__ float team_best_split(const Team<G>& tm, const Arr& A
 //   big p >= pL             -> p - 1
 // The ranks of positions [lo, hi) are assigned with the rank bases lbase / rbase (the counts
 // of left bigs before lo / right smalls after hi): one team, or one wave of a workgroup.
-template <int G>
-__device__ __forceinline__ void team_ranks(const Team<G>& tm, const Arr& A, const uint32_t* src, const MeshDev& M,
+template <int G, class AR>
+__device__ __forceinline__ void team_ranks(const Team<G>& tm, const AR& A, const uint32_t* src, const MeshDev& M,
                                            uint32_t first, uint32_t lo, uint32_t hi, uint32_t pL, int axis,
                                            float pos, uint32_t lbase, uint32_t rbase) {
     auto small = [&](uint32_t q) { return A.c(axis, src[first + q]) < pos; };
@@ -303,8 +308,8 @@ __device__ __forceinline__ void team_ranks(const Team<G>& tm, const Arr& A, cons
         const unsigned long long m = tm.ballot(b);
         if (b) {
             const uint32_t r = carry + tm.below(m);
-            M.lb[first + r] = q;
-            M.rk[first + q] = r;
+            A.lb[first + r] = q;
+            A.rk[first + q] = r;
         }
         carry += __popcll(m);
     }
@@ -318,25 +323,26 @@ __device__ __forceinline__ void team_ranks(const Team<G>& tm, const Arr& A, cons
         const unsigned long long m = tm.ballot(sm);
         if (sm) {
             const uint32_t r = carry + tm.below(m);
-            M.rs[first + r] = p;
-            M.rk[first + p] = r;
+            A.rs[first + r] = p;
+            A.rk[first + p] = r;
         }
         carry += __popcll(m);
         top -= cnt;
     }
 }
 // Destination of position q once every rank is known.
-__device__ __forceinline__ uint32_t part_dest(const MeshDev& M, uint32_t first, uint32_t n, uint32_t q, uint32_t pL,
+template <class AR>
+__device__ __forceinline__ uint32_t part_dest(const AR& A, uint32_t first, uint32_t n, uint32_t q, uint32_t pL,
                                               bool big) {
     if (q < pL) {
         if (!big) return q;
-        const uint32_t m = M.rk[first + q];
-        return m == 0u ? n - 1u : M.rs[first + m - 1u] - 1u;
+        const uint32_t m = A.rk[first + q];
+        return m == 0u ? n - 1u : static_cast<uint32_t>(A.rs[first + m - 1u]) - 1u;
     }
-    return big ? q - 1u : M.lb[first + M.rk[first + q]];
+    return big ? q - 1u : static_cast<uint32_t>(A.lb[first + A.rk[first + q]]);
 }
-template <int G>
-__device__ __forceinline__ uint32_t team_count_small(const Team<G>& tm, const Arr& A, const uint32_t* src,
+template <int G, class AR>
+__device__ __forceinline__ uint32_t team_count_small(const Team<G>& tm, const AR& A, const uint32_t* src,
                                                      uint32_t first, uint32_t lo, uint32_t hi, int axis, float pos) {
     uint32_t S = 0;
     for (uint32_t base = lo; base < hi; base += G) {
@@ -345,8 +351,8 @@ __device__ __forceinline__ uint32_t team_count_small(const Team<G>& tm, const Ar
     }
     return S;
 }
-template <int G>
-__device__ __forceinline__ void team_partition(const Team<G>& tm, const Arr& A, const uint32_t* src, uint32_t* dst,
+template <int G, class AR>
+__device__ __forceinline__ void team_partition(const Team<G>& tm, const AR& A, const uint32_t* src, uint32_t* dst,
                                                const MeshDev& M, uint32_t first, uint32_t n, int axis, float pos,
                                                uint32_t& S_out) {
     const uint32_t S = team_count_small(tm, A, src, first, 0u, n, axis, pos);
@@ -355,7 +361,7 @@ __device__ __forceinline__ void team_partition(const Team<G>& tm, const Arr& A, 
     __threadfence_block();
     for (uint32_t q = tm.tl; q < n; q += G) {
         const uint32_t id = src[first + q];
-        dst[first + part_dest(M, first, n, q, pL, !(A.c(axis, id) < pos))] = id;
+        dst[first + part_dest(A, first, n, q, pL, !(A.c(axis, id) < pos))] = id;
     }
     __threadfence_block();
     S_out = S;
@@ -402,8 +408,8 @@ __device__ __forceinline__ void add_children(const MeshDev& M, Lists& Ls, uint32
 }
 
 // One node by one team of G lanes (a wave, or 8 lanes).
-template <int G>
-__device__ __forceinline__ void team_node(const Team<G>& tm, const Arr& A, uint32_t* src, uint32_t* dst,
+template <int G, class AR>
+__device__ __forceinline__ void team_node(const Team<G>& tm, const AR& A, uint32_t* src, uint32_t* dst,
                                           const MeshDev& M, Lists& Ls, uint32_t cl, uint32_t t, uint32_t depth) {
     const TmpNode X = M.tmp[t];
     const uint32_t n = X.count;
@@ -454,7 +460,8 @@ __device__ __forceinline__ Bounds wg_fold_bounds(const WgScratch& W) {   // wave
 }
 
 // One huge node by the whole workgroup: wave w takes the w-th contiguous eighth of the range.
-__device__ void wg_node(const Arr& A, uint32_t* src, uint32_t* dst, const MeshDev& M, Lists& Ls, WgScratch& W,
+template <class AR>
+__device__ void wg_node(const AR& A, uint32_t* src, uint32_t* dst, const MeshDev& M, Lists& Ls, WgScratch& W,
                         uint32_t cl, uint32_t t, uint32_t depth, uint32_t tid) {
     const uint32_t lane = tid & 63u, wave = tid >> 6;
     const Team<64> tm(lane);
@@ -543,7 +550,7 @@ __device__ void wg_node(const Arr& A, uint32_t* src, uint32_t* dst, const MeshDe
     __syncthreads();
     for (uint32_t q = tid; q < n; q += kAnimThreads) {
         const uint32_t id = src[first + q];
-        dst[first + part_dest(M, first, n, q, pL, !(A.c(axis, id) < pos))] = id;
+        dst[first + part_dest(A, first, n, q, pL, !(A.c(axis, id) < pos))] = id;
     }
     __syncthreads();
     if (S == 0u || S == n) {
@@ -568,7 +575,8 @@ __device__ void wg_node(const Arr& A, uint32_t* src, uint32_t* dst, const MeshDe
 // One node of at most kTinyNode triangles by ONE lane: the reference's own serial passes
 // (bounds folds, bins, sweep, the swap loop itself), in place on `src`, then copied to `dst`
 // so that both permutation buffers hold the range.
-__device__ __forceinline__ void lane_node(const Arr& A, uint32_t* src, uint32_t* dst, const MeshDev& M, Lists& Ls, uint32_t cl,
+template <class AR>
+__device__ __forceinline__ void lane_node(const AR& A, uint32_t* src, uint32_t* dst, const MeshDev& M, Lists& Ls, uint32_t cl,
                           uint32_t t, uint32_t depth) {
     const TmpNode X = M.tmp[t];
     const uint32_t first = X.first, n = X.count;
@@ -643,16 +651,20 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
     __shared__ Lists Ls;
     __shared__ uint32_t s_fr[kMaxAnimParts][3];
     __shared__ uint32_t s_nfr;
-    // build arrays: LDS when the launch reserved room for this mesh, else HBM
-    Arr A;
+    // build arrays: in LDS when every mesh of the launch fits (LDS), else in HBM
+    using Scratch = std::conditional_t<LDS, uint16_t, uint32_t>;
+    Arr<Scratch> A;
     {
-        constexpr bool lds = LDS;
-        float* base = lds ? s_dyn : M.soa;
+        float* base = LDS ? s_dyn : M.soa;
         A.cx = base; A.cy = base + T; A.cz = base + 2 * T;
         A.lx = base + 3 * T; A.ly = base + 4 * T; A.lz = base + 5 * T;
         A.hx = base + 6 * T; A.hy = base + 7 * T; A.hz = base + 8 * T;
-        A.perm[0] = lds ? reinterpret_cast<uint32_t*>(s_dyn + 9 * T) : M.perm[0];
-        A.perm[1] = lds ? reinterpret_cast<uint32_t*>(s_dyn + 10 * T) : M.perm[1];
+        A.perm[0] = LDS ? reinterpret_cast<uint32_t*>(s_dyn + 9 * T) : M.perm[0];
+        A.perm[1] = LDS ? reinterpret_cast<uint32_t*>(s_dyn + 10 * T) : M.perm[1];
+        uint16_t* s16 = reinterpret_cast<uint16_t*>(s_dyn + 11 * T);
+        A.lb = LDS ? reinterpret_cast<Scratch*>(s16) : reinterpret_cast<Scratch*>(M.lb);
+        A.rs = LDS ? reinterpret_cast<Scratch*>(s16 + T) : reinterpret_cast<Scratch*>(M.rs);
+        A.rk = LDS ? reinterpret_cast<Scratch*>(s16 + 2 * T) : reinterpret_cast<Scratch*>(M.rk);
     }
     // diagnostic phase stamps (s_memrealtime, 100 MHz): status[8] start, [9] set-up done,
     // [10 + d] level d done, [60] numbered, [61] written, [62] frontier done

@@ -2507,7 +2507,7 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
         ANIM_CREATE_TRY(anim_alloc(a, &d.perm[0], T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.perm[1], T));
         if (T > static_cast<size_t>(rtxa::kLdsTris)) a->lds_big = true;
-        a->lds_bytes = std::max<uint32_t>(a->lds_bytes, static_cast<uint32_t>(T * rtxa::kLdsWordsPerTri * 4));
+        a->lds_bytes = std::max<uint32_t>(a->lds_bytes, static_cast<uint32_t>((T * rtxa::kLdsBytesPerTri + 15) / 16 * 16));
         ANIM_CREATE_TRY(anim_alloc(a, &d.lb, T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.rs, T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.rk, T));

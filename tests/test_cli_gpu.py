@@ -53,18 +53,23 @@ def _channels(px: np.ndarray) -> np.ndarray:
     return np.stack([(px >> s) & 0xFF for s in (16, 8, 0)], -1).astype(np.int32)
 
 
-@pytest.mark.parametrize("scene,inflight,exact", [("W4_Bunny", 2, True), ("W4_Optional", 2, False),
-                                                  ("W4_Optional", 3, False), ("W4_Reference", 1, False)])
-def test_pipelined_frame_loop_matches_oracle(tmp_path, scene, inflight, exact):
+@pytest.mark.parametrize("scene,inflight,exact,device", [("W4_Bunny", 2, True, False), ("W4_Optional", 2, False, False),
+                                                         ("W4_Optional", 3, False, False),
+                                                         ("W4_Reference", 1, False, False),
+                                                         ("W4_Bunny", 2, True, True), ("W4_Optional", 3, False, True),
+                                                         ("W4_Reference", 2, False, True)])
+def test_pipelined_frame_loop_matches_oracle(tmp_path, scene, inflight, exact, device):
     """The overlapped frame loop (frame k+1's Update and BVH rebuild on the host while frame
     k renders on another context) renders every frame of an animated sequence exactly as
-    the reference's serial loop: Update(t_k) on one persistent scene, then Render."""
+    the reference's serial loop: Update(t_k) on one persistent scene, then Render.  With
+    --device-update the Update itself runs on the device (rtx_anim_*)."""
     if not EXE.exists():
         pytest.skip("rtx_render not built")
     W, H = 160, 120
     times = [0.3, 0.9, 1.7, 2.2, 3.1]
     subprocess.run([str(EXE), scene, str(W), str(H), "--sequence", ",".join(map(str, times)), "--inflight",
-                    str(inflight), "--out", str(tmp_path / "f.bmp")], check=True, cwd=tmp_path, timeout=120)
+                    str(inflight), "--out", str(tmp_path / "f.bmp")] + (["--device-update"] if device else []),
+                   check=True, cwd=tmp_path, timeout=120)
     hs = HostScene(scene)
     for k, t in enumerate(times):
         hs.update(t)

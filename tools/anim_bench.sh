@@ -10,3 +10,10 @@ for cfg in "W4_Optional 1920 1080" "W4_Bunny 1920 1080" "Bunny8Lights 3840 2160"
     timeout -k 10 60 $EXE $cfg --benchmark ${1:-3} --inflight $f --out /tmp/anim.bmp --assets ../../gp1_raytracer_2223_amd/assets | grep -v "BENCHMARK\|wrote" || exit 1
   done
 done
+# the same loop with the Update on the device (rtx_anim_*)
+for cfg in "W4_Optional 1920 1080" "W4_Bunny 1920 1080" "W4_Reference 1920 1080"; do
+  for f in 1 3; do
+    echo "== $cfg inflight $f device-update"
+    timeout -k 10 60 $EXE $cfg --benchmark ${1:-3} --inflight $f --device-update --out /tmp/anim.bmp --assets ../../gp1_raytracer_2223_amd/assets | grep -v "BENCHMARK\|wrote" || exit 1
+  done
+done
