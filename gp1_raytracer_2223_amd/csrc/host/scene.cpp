@@ -264,7 +264,12 @@ void TriangleMesh::SubdivideFast(uint32_t t) {
     n.l = static_cast<int32_t>(L);
     n.r = static_cast<int32_t>(R);
     BuildPool& pool = BuildPool::Get();
-    if (pool.Workers() > 0 && tmp_[L].count >= 3 * 2048 && tmp_[R].count >= 3 * 2048) {
+    static const uint32_t par = [] {   // RTX_HOST_PAR_TRIS: fork subtrees with at least this many triangles a side
+        const char* e = std::getenv("RTX_HOST_PAR_TRIS");
+        const int v = e ? std::atoi(e) : 2048;
+        return static_cast<uint32_t>(v > 0 ? v : 2048);
+    }();
+    if (pool.Workers() > 0 && tmp_[L].count >= 3 * par && tmp_[R].count >= 3 * par) {
         BuildPool::Task task;
         task.fn = [this, L] { SubdivideFast(L); };
         pool.Submit(&task);

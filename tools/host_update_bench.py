@@ -21,9 +21,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for scene in sys.argv[1:] or ["W4_Optional", "W4_Bunny"]:
     for label, env in [("direct", {"RTX_HOST_BVH": "direct"}), ("fast x1", {"RTX_HOST_THREADS": "1"}),
                        ("fast x2", {"RTX_HOST_THREADS": "2"}), ("fast x4", {"RTX_HOST_THREADS": "4"}),
-                       ("fast x8", {"RTX_HOST_THREADS": "8"})]:
+                       ("fast x8", {"RTX_HOST_THREADS": "8"}),
+                       ("x8 fork>=256", {"RTX_HOST_THREADS": "8", "RTX_HOST_PAR_TRIS": "256"}),
+                       ("x8 fork>=128", {"RTX_HOST_THREADS": "8", "RTX_HOST_PAR_TRIS": "128"}),
+                       ("x8 fork>=64", {"RTX_HOST_THREADS": "8", "RTX_HOST_PAR_TRIS": "64"}),
+                       ("x4 fork>=128", {"RTX_HOST_THREADS": "4", "RTX_HOST_PAR_TRIS": "128"})]:
         e = dict(os.environ)
         e.pop("RTX_HOST_BVH", None)
         e.update(env)
         r = subprocess.run([sys.executable, "-c", CHILD, ROOT, scene], env=e, capture_output=True, text=True, check=True)
-        print(f"{scene:12s} {label:8s} update {r.stdout.strip()} ms", flush=True)
+        print(f"{scene:12s} {label:13s} update {r.stdout.strip()} ms", flush=True)
