@@ -29,8 +29,10 @@ max-reduce of the timings.
 Frames in flight (--inflight, default 2): consecutive steps go round robin to that many
 render contexts on the rank's GPU (each its own stream, frame buffer and tile schedule),
 so frame k+1 starts while frame k's last waves drain.  `roofline.kernel_ms` is the
-serialized launch time of ONE context (HIP events on its stream), the figure a rocprofv3
-kernel trace of `--inflight 1` shows.
+serialized launch time of ONE context (HIP events on its stream, mean of 1000 launches), the
+figure a rocprofv3 kernel trace of `--inflight 1` shows.  It is measured first, before the W
+warm-up steps: those 1000 launches (~60 ms) also take the GPU from its idle clock to its
+steady rendering clock, which a short run's few warm-up steps do not.
 
 After timing, the gathered frame is checked against the reference: `parity` carries the
 SHA-256 comparison with tests/golden/config_<scene>_<W>x<H>.npz (the frame the reference
@@ -282,6 +284,9 @@ def parity_report(px: np.ndarray, rgb: np.ndarray, scene: str, width: int, heigh
     return out
 
 
+K_KERNEL_LAUNCHES = 1000   # launches averaged for roofline.kernel_ms
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -350,6 +355,15 @@ def main() -> int:
         d.barrier()
         return d.max(time.perf_counter() - t0)
 
+    # Kernel-only time of the same launches (HIP events on the launch stream), the roofline's
+    # denominator: the mean of kKernelLaunches serialized launches, taken first — it also brings
+    # the GPU from its idle clock to the steady rendering clock (profiles/r02/warmup_probe.txt),
+    # which the requested W warm-up steps alone (the driver uses 5) do not.
+    kernel_ms = C.c_float()
+    abi.check(lib.rtx_time_views(ctx.h, views, nviews, C.byref(params), K_KERNEL_LAUNCHES,
+                                 C.byref(kernel_ms)), "rtx_time_views", ctx.h)
+    kernel_ms = kernel_ms.value
+
     for i in range(args.warmup):
         step(i)
     sync_all()
@@ -382,12 +396,6 @@ def main() -> int:
                     "ms_per_step": round(g_elapsed / args.steps * 1e3, 5), "pinned": bool(pinned),
                     "target": "page-locked host frames (one per view) shared by all ranks (/dev/shm mapping)",
                     "copy": "hipMemcpy2DAsync of the rank's own 16-row stripes (rtx_gather_async)"}
-
-    # Kernel-only time of the same launches, HIP events on the launch stream.
-    kernel_ms = C.c_float()
-    abi.check(lib.rtx_time_views(ctx.h, views, nviews, C.byref(params), min(args.steps, 200),
-                                 C.byref(kernel_ms)), "rtx_time_views", ctx.h)
-    kernel_ms = kernel_ms.value
 
     # Algorithmic work of one launch (SURVEY §8(d) FLOP model) from the instrumented kernel.
     counts_total = np.zeros(12, np.uint64)
@@ -467,14 +475,16 @@ def main() -> int:
                      # north star: the HBM roofline fraction, reported beside the VALU one
                      "hbm_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
                      if traffic and kernel_ms > 0 else None,
-                     "kernel": "rtx_render_kernel<false, 0> (+ split phases 1-3 when tiles are heavy)",
-                     "kernel_ms": round(kernel_ms, 5),
+                     "kernel": "rtx_render_kernel<false, 0, false, SPEC> (the specialised variant the scene's "
+                               "facts select; + split phases 1-3 when tiles are heavy)",
+                     "kernel_ms": round(kernel_ms, 5), "kernel_launches": K_KERNEL_LAUNCHES,
                      "flop_per_launch": flop, "pixels_per_launch": pixels_per_rank,
                      "flop_per_pixel": round(flop / max(pixels_per_rank, 1), 2),
                      "frame_flop_all_ranks": frame_flop, "frame_pixels_counted": frame_counted,
                      "note": "FP32 VALU-bound path (no dense contraction, 4 B/pixel of HBM output); "
                              "FLOP = SURVEY §8(d) algorithmic model counted by the instrumented kernel; "
-                             "kernel_ms/achieved are rank 0's launches"},
+                             "kernel_ms/achieved are rank 0's launches (mean of kernel_launches serialized launches, "
+                             "timed before the warm-up)"},
         "cpu_baseline": cpu,
         "parity": parity,
         "host_gather": gathered,

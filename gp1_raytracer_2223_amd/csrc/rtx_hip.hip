@@ -2245,10 +2245,18 @@ extern "C" int rtx_time_views(rtx_ctx* c, const rtx_camera* cams, int n_views, c
     if (!mean_ms || iters <= 0) return RTX_E_INVALID;
     FrameArgs F;
     dim3 grid;
+    // every launch is prepared like a real frame: the first frame of a launch shape measures
+    // tile costs, the next ones run in the cost order (and split the heavy tiles) it yields,
+    // and every kSchedPeriod-th frame measures again
     int rc = prepare(c, cams, n_views, p, false, F, grid);
     if (rc != RTX_OK) return rc;
     HIP_TRY(c, hipEventRecord(c->ev0, c->stream));
     for (int i = 0; i < iters; ++i) {
+        if (i > 0) {
+            remember(c, p, n_views, false);
+            rc = prepare(c, cams, n_views, p, false, F, grid);
+            if (rc != RTX_OK) return rc;
+        }
         rc = launch(c, F, grid, false);
         if (rc != RTX_OK) return rc;
     }
