@@ -2514,7 +2514,8 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
         ANIM_CREATE_TRY(anim_alloc(a, &d.soa, 9 * T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.perm[0], T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.perm[1], T));
-        if (T > static_cast<size_t>(rtxa::kLdsTris)) a->lds_big = true;
+        // RTX_ANIM_HBM=1 builds from HBM whatever the size (tests: the large-mesh path)
+        if (T > static_cast<size_t>(rtxa::kLdsTris) || std::getenv("RTX_ANIM_HBM")) a->lds_big = true;
         a->lds_bytes = std::max<uint32_t>(a->lds_bytes, static_cast<uint32_t>((T * rtxa::kLdsBytesPerTri + 15) / 16 * 16));
         ANIM_CREATE_TRY(anim_alloc(a, &d.lb, T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.rs, T));

@@ -135,6 +135,21 @@ def test_device_update_frames_in_flight_two_contexts():
         c.close()
 
 
+@pytest.mark.parametrize("name", ["W4_Optional", "file:scenes/gallery.rtxscene"])
+def test_device_update_hbm_build_path(gpu_ctx, name, monkeypatch):
+    """Meshes above the LDS capacity (3,136 triangles) build from HBM: the same kernel with
+    its arrays in memory (forced here with RTX_ANIM_HBM=1 on the catalogue meshes)."""
+    monkeypatch.setenv("RTX_ANIM_HBM", "1")   # read at rtx_anim_create
+    dev_scene, host_scene = _scene(name), _scene(name)
+    anim = DeviceAnimation(dev_scene, gpu_ctx)
+    for t in TIMES[:3]:
+        anim.update(t, gpu_ctx)
+        host_scene.update(t)
+        for k in range(len(anim.mesh_ids)):
+            _compare_state(anim, host_scene, k)
+    anim.close()
+
+
 def _image(ctx):
     import ctypes as C
     lib = abi.load_hip()
