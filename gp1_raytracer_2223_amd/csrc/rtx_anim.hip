@@ -79,11 +79,12 @@ struct Bounds {
     }
 };
 
-// A team: G consecutive lanes of one wave handle one node (G = 64: the whole wave; G = 8:
-// eight nodes per wave).  Control flow is uniform within a team (trip counts depend only on
-// the node), so team shuffles and ballots see every lane of the team.
+// A team: G consecutive lanes of one wave handle one node (G = 64: the whole wave; G = 16:
+// one DPP row, four nodes per wave).  Control flow is uniform within a team (trip counts
+// depend only on the node), so team reductions and ballots see every lane of the team.
 template <int G>
 struct Team {
+    static_assert(G == 16 || G == 64, "teams are DPP rows or whole waves");
     uint32_t tl, tb;   // lane within the team, the team's first lane in the wave
     __device__ explicit Team(uint32_t lane) : tl(lane % G), tb(lane - lane % G) {}
     __device__ unsigned long long ballot(bool p) const {
@@ -91,20 +92,68 @@ struct Team {
         return G == 64 ? b : (b >> tb) & ((1ull << G) - 1ull);
     }
     __device__ uint32_t below(unsigned long long m) const { return __popcll(m & ((1ull << tl) - 1ull)); }
-    template <class V> __device__ V down(V v, uint32_t off) const { return __shfl_down(v, off, G); }
-    template <class V> __device__ V first(V v) const { return __shfl(v, 0, G); }
     // contiguous chunk [s, e) of positions [a, a + n) for this lane: folds stay in order
     __device__ void chunk(uint32_t a, uint32_t n, uint32_t& s, uint32_t& e) const {
         const uint32_t c = (n + G - 1u) / G;
         s = a + min(n, tl * c);
         e = a + min(n, tl * c + c);
     }
-    __device__ bool absorbs(uint32_t off) const { return (tl & (2u * off - 1u)) == 0u; }
 };
 
+// In-order team folds without LDS round trips: DPP row_shl:n (lane i reads lane i + n of its
+// row; a source beyond the row yields the fold identity) halves the row in four steps, lane 16r
+// ending with the in-order fold of row r; rows are combined in order from v_readlane values
+// (G = 64) or the row fold is broadcast with row_newbcast:0 (G = 16).  Every result is the
+// team's fold, in every lane of the team.
+template <int N>
+__device__ __forceinline__ uint32_t dpp_shl(uint32_t v, uint32_t identity) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(identity), static_cast<int>(v),
+                                                             0x100 + N, 0xf, 0xf, false));
+}
+__device__ __forceinline__ uint32_t dpp_row_bcast0(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x150, 0xf, 0xf, false));
+}
+struct OpMin {
+    static constexpr float kId = FLT_MAX;
+    __device__ static float f(float m, float x) { return rmin(m, x); }
+};
+struct OpMax {
+    static constexpr float kId = FLT_MIN;
+    __device__ static float f(float m, float x) { return rmax(m, x); }
+};
+template <int G, class Op>
+__device__ __forceinline__ float team_fold(float v) {
+    const uint32_t id = __float_as_uint(Op::kId);
+    v = Op::f(v, __uint_as_float(dpp_shl<1>(__float_as_uint(v), id)));
+    v = Op::f(v, __uint_as_float(dpp_shl<2>(__float_as_uint(v), id)));
+    v = Op::f(v, __uint_as_float(dpp_shl<4>(__float_as_uint(v), id)));
+    v = Op::f(v, __uint_as_float(dpp_shl<8>(__float_as_uint(v), id)));
+    if (G == 16) return __uint_as_float(dpp_row_bcast0(__float_as_uint(v)));
+    const uint32_t u = __float_as_uint(v);
+    const float r0 = __uint_as_float(__builtin_amdgcn_readlane(u, 0)), r1 = __uint_as_float(__builtin_amdgcn_readlane(u, 16));
+    const float r2 = __uint_as_float(__builtin_amdgcn_readlane(u, 32)), r3 = __uint_as_float(__builtin_amdgcn_readlane(u, 48));
+    return Op::f(Op::f(Op::f(r0, r1), r2), r3);
+}
+template <int G>
+__device__ __forceinline__ uint32_t team_sum(uint32_t v) {
+    v += dpp_shl<1>(v, 0u);
+    v += dpp_shl<2>(v, 0u);
+    v += dpp_shl<4>(v, 0u);
+    v += dpp_shl<8>(v, 0u);
+    if (G == 16) return dpp_row_bcast0(v);
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+           __builtin_amdgcn_readlane(v, 48);
+}
+template <int G>
+__device__ __forceinline__ Bounds team_fold(const Bounds& B) {
+    Bounds R;
+    R.l0 = team_fold<G, OpMin>(B.l0); R.l1 = team_fold<G, OpMin>(B.l1); R.l2 = team_fold<G, OpMin>(B.l2);
+    R.h0 = team_fold<G, OpMax>(B.h0); R.h1 = team_fold<G, OpMax>(B.h1); R.h2 = team_fold<G, OpMax>(B.h2);
+    return R;
+}
+
 // Bounds of the triangle boxes at build positions [a, b) (UpdateNodeBounds: a triangle's box
-// min(min(v0, v1), v2) grows a node exactly as its three vertices in order do); team lane 0
-// ends with the fold of the whole range (lane i absorbs the later chunk of lane i + off).
+// min(min(v0, v1), v2) grows a node exactly as its three vertices in order do), every lane.
 template <int G, class AR>
 __device__ __forceinline__ Bounds team_bounds(const Team<G>& tm, const AR& A, const uint32_t* perm, uint32_t a,
                                               uint32_t b) {
@@ -113,22 +162,7 @@ __device__ __forceinline__ Bounds team_bounds(const Team<G>& tm, const AR& A, co
     tm.chunk(a, b - a, s, e);
 #pragma unroll 4
     for (uint32_t k = s; k < e; ++k) B.grow(A, perm[k]);
-    for (uint32_t off = 1; off < static_cast<uint32_t>(G); off <<= 1) {
-        const float o0 = tm.down(B.l0, off), o1 = tm.down(B.l1, off), o2 = tm.down(B.l2, off);
-        const float p0 = tm.down(B.h0, off), p1 = tm.down(B.h1, off), p2 = tm.down(B.h2, off);
-        if (tm.absorbs(off)) {
-            B.l0 = rmin(B.l0, o0); B.l1 = rmin(B.l1, o1); B.l2 = rmin(B.l2, o2);
-            B.h0 = rmax(B.h0, p0); B.h1 = rmax(B.h1, p1); B.h2 = rmax(B.h2, p2);
-        }
-    }
-    return B;
-}
-template <int G>
-__device__ __forceinline__ Bounds team_first(const Team<G>& tm, const Bounds& B) {
-    Bounds R;
-    R.l0 = tm.first(B.l0); R.l1 = tm.first(B.l1); R.l2 = tm.first(B.l2);
-    R.h0 = tm.first(B.h0); R.h1 = tm.first(B.h1); R.h2 = tm.first(B.h2);
-    return R;
+    return team_fold<G>(B);
 }
 
 constexpr int kBins = 8, kPlanes = kBins - 1;
@@ -206,7 +240,7 @@ struct Bins {
 };
 
 // Centroid bounds of positions [a, b): min from FLT_MAX, max from FLT_MIN (the reference's
-// minBounds / maxBounds, DataTypes.h:404-419), the three axes in one fold; valid in lane 0.
+// minBounds / maxBounds, DataTypes.h:404-419), the three axes in one fold, every lane.
 template <int G, class AR>
 __device__ __forceinline__ Bounds team_centroid_bounds(const Team<G>& tm, const AR& A, const uint32_t* perm,
                                                        uint32_t a, uint32_t b) {
@@ -220,18 +254,10 @@ __device__ __forceinline__ Bounds team_centroid_bounds(const Team<G>& tm, const 
         C.l0 = rmin(C.l0, x); C.l1 = rmin(C.l1, y); C.l2 = rmin(C.l2, z);
         C.h0 = rmax(C.h0, x); C.h1 = rmax(C.h1, y); C.h2 = rmax(C.h2, z);
     }
-    for (uint32_t off = 1; off < static_cast<uint32_t>(G); off <<= 1) {
-        const float o0 = tm.down(C.l0, off), o1 = tm.down(C.l1, off), o2 = tm.down(C.l2, off);
-        const float p0 = tm.down(C.h0, off), p1 = tm.down(C.h1, off), p2 = tm.down(C.h2, off);
-        if (tm.absorbs(off)) {
-            C.l0 = rmin(C.l0, o0); C.l1 = rmin(C.l1, o1); C.l2 = rmin(C.l2, o2);
-            C.h0 = rmax(C.h0, p0); C.h1 = rmax(C.h1, p1); C.h2 = rmax(C.h2, p2);
-        }
-    }
-    return C;
+    return team_fold<G>(C);
 }
 
-// One axis's bins over positions [a, b); valid in team lane 0.
+// One axis's bins over positions [a, b), every lane.
 template <int G, class AR>
 __device__ __forceinline__ void team_bins(const Team<G>& tm, const AR& A, const uint32_t* perm, uint32_t a,
                                           uint32_t b, int ax, float minBounds, float scale, Bins& bins) {
@@ -240,22 +266,13 @@ __device__ __forceinline__ void team_bins(const Team<G>& tm, const AR& A, const 
     tm.chunk(a, b - a, s, e);
 #pragma unroll 2
     for (uint32_t k = s; k < e; ++k) bins.add(A, perm[k], ax, minBounds, scale);
-    for (uint32_t off = 1; off < static_cast<uint32_t>(G); off <<= 1) {
-        const bool take = tm.absorbs(off);
 #pragma unroll
-        for (int q = 0; q < kBins; ++q) {
-            const uint32_t oc = tm.down(bins.bc[q], off);
-            float ol[3], oh[3];
+    for (int q = 0; q < kBins; ++q) {
+        bins.bc[q] = team_sum<G>(bins.bc[q]);
 #pragma unroll
-            for (int c = 0; c < 3; ++c) { ol[c] = tm.down(bins.bl[q][c], off); oh[c] = tm.down(bins.bh[q][c], off); }
-            if (take) {
-                bins.bc[q] += oc;
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    bins.bl[q][c] = rmin(bins.bl[q][c], ol[c]);
-                    bins.bh[q][c] = rmax(bins.bh[q][c], oh[c]);
-                }
-            }
+        for (int c = 0; c < 3; ++c) {
+            bins.bl[q][c] = team_fold<G, OpMin>(bins.bl[q][c]);
+            bins.bh[q][c] = team_fold<G, OpMax>(bins.bh[q][c]);
         }
     }
 }
@@ -265,7 +282,7 @@ __device__ __forceinline__ void team_bins(const Team<G>& tm, const AR& A, const 
 template <int G, class AR>
 __device__ __forceinline__ float team_best_split(const Team<G>& tm, const AR& A, const uint32_t* perm, uint32_t a,
                                                  uint32_t n, int& axis, float& pos) {
-    const Bounds C = team_first(tm, team_centroid_bounds(tm, A, perm, a, a + n));
+    const Bounds C = team_centroid_bounds(tm, A, perm, a, a + n);
     const float cl[3] = {C.l0, C.l1, C.l2}, ch[3] = {C.h0, C.h1, C.h2};
     float bestCost = FLT_MAX;
 #pragma unroll
@@ -275,11 +292,8 @@ __device__ __forceinline__ float team_best_split(const Team<G>& tm, const AR& A,
         if (fabsf(boundsDifference) < FLT_EPSILON) continue;
         Bins bins;
         team_bins(tm, A, perm, a, a + n, ax, minBounds, kBins / boundsDifference, bins);
-        bins.sweep(ax, minBounds, boundsDifference, bestCost, axis, pos);   // lane 0's bins decide
+        bins.sweep(ax, minBounds, boundsDifference, bestCost, axis, pos);   // the same in every lane
     }
-    bestCost = tm.first(bestCost);
-    axis = tm.first(axis);
-    pos = tm.first(pos);
     return bestCost;
 }
 
@@ -375,8 +389,8 @@ __device__ __forceinline__ void team_copy(const Team<G>& tm, const uint32_t* src
 }
 
 // Node classes by size: huge nodes are processed by the whole workgroup one at a time, large
-// ones by a wave, small ones by 8 lanes, tiny ones by one lane each (every class folds at
-// most 8 positions per lane, except the huge ones' eighths).
+// ones by a wave, small ones by a 16-lane row, tiny ones by one lane each (every class folds
+// at most 8 positions per lane, except the huge ones' eighths).
 constexpr uint32_t kHugeNode = 512, kLargeNode = 64, kTinyNode = 8;
 __device__ __forceinline__ uint32_t node_class(uint32_t n) {
     return n > kHugeNode ? 0u : (n > kLargeNode ? 1u : (n > kTinyNode ? 2u : 3u));
@@ -407,7 +421,7 @@ __device__ __forceinline__ void add_children(const MeshDev& M, Lists& Ls, uint32
     }
 }
 
-// One node by one team of G lanes (a wave, or 8 lanes).
+// One node by one team of G lanes (a wave, or a 16-lane row).
 template <int G, class AR>
 __device__ __forceinline__ void team_node(const Team<G>& tm, const AR& A, uint32_t* src, uint32_t* dst,
                                           const MeshDev& M, Lists& Ls, uint32_t cl, uint32_t t, uint32_t depth) {
@@ -731,18 +745,23 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
         if (n0 + n1 + n2 + n3 == 0) break;
         uint32_t* src = cr ? A.perm[1] : A.perm[0];   // (selects: a dynamic index would put A in scratch)
         uint32_t* dst = cr ? A.perm[0] : A.perm[1];
+        if (tid == 0 && depth < 12) {   // diagnostics: node count per class at this level
+            M.status[64 + 4 * depth] = n0; M.status[65 + 4 * depth] = n1;
+            M.status[66 + 4 * depth] = n2; M.status[67 + 4 * depth] = n3;
+        }
         for (uint32_t j = 0; j < n0; ++j) {
             wg_node(A, src, dst, M, Ls, W, cl, M.lvl[0 + cl][j], depth, tid);
             __syncthreads();
         }
+        if (tid == 0 && depth < 12) M.status[112 + depth] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
         {
             const Team<64> tm(lane);
             for (uint32_t j = wave; j < n1; j += kAnimWaves) team_node(tm, A, src, dst, M, Ls, cl, M.lvl[2 + cl][j], depth);
         }
         {
-            const Team<8> tm(lane);
-            constexpr uint32_t kTeams = kAnimThreads / 8;
-            for (uint32_t j = tid / 8u; j < n2; j += kTeams) team_node(tm, A, src, dst, M, Ls, cl, M.lvl[4 + cl][j], depth);
+            const Team<16> tm(lane);
+            constexpr uint32_t kTeams = kAnimThreads / 16;
+            for (uint32_t j = tid / 16u; j < n2; j += kTeams) team_node(tm, A, src, dst, M, Ls, cl, M.lvl[4 + cl][j], depth);
         }
         for (uint32_t j = tid; j < n3; j += kAnimThreads) lane_node(A, src, dst, M, Ls, cl, M.lvl[6 + cl][j], depth);
         __syncthreads();

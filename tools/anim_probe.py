@@ -87,5 +87,9 @@ w = [int(x) for x in st]
 t0 = w[8]
 us = lambda x: (x - t0) / 100.0  # noqa: E731
 lv = [us(w[10 + d]) for d in range(w[1] + 1)]
+for d in range(min(12, w[1] + 1)):
+    start_d = w[9] if d == 0 else w[10 + d - 1]
+    print(f"  level {d}: nodes huge/large/small/tiny {w[64 + 4 * d]}/{w[65 + 4 * d]}/{w[66 + 4 * d]}/{w[67 + 4 * d]}, "
+          f"huge part {(w[112 + d] - start_d) / 100:.1f} us, level {(w[10 + d] - start_d) / 100:.1f} us")
 print(f"build phases (us from start): setup {us(w[9]):.1f}, levels {[round(x, 1) for x in lv]}, "
       f"numbered {us(w[60]):.1f}, written {us(w[61]):.1f}, frontier {us(w[62]):.1f}")
