@@ -46,9 +46,9 @@ def build_host(force: bool = False) -> Path:
     LIB.mkdir(exist_ok=True)
     out = LIB / "librtx_host.so"
     srcs = [CSRC / "host" / "scene.cpp", CSRC / "host" / "host_api.cpp"]
-    deps = srcs + list((CSRC / "host").glob("*.h")) + [INC / "rtx.h", INC / "rtx_host.h"]
+    deps = srcs + list((CSRC / "host").glob("*.h")) + [INC / "rtx.h", INC / "rtx_host.h", Path(__file__)]
     if force or _stale(out, deps):
-        _run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared", "-pthread",
+        _run(["g++", "-std=c++17", "-O3", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared", "-pthread",
               "-Wall", "-Wextra", f"-I{INC}", *srcs, "-o", out, "-ldl"])
     return out
 

@@ -256,7 +256,10 @@ void TriangleMesh::SubdivideFast(uint32_t t) {
     const int leftCount = 3 * i - static_cast<int>(n.first);
     if (leftCount == 0 || static_cast<uint32_t>(leftCount) == n.count) return;
 
-    const uint32_t L = __atomic_fetch_add(&tmpUsed_, 2u, __ATOMIC_RELAXED), R = L + 1;
+    // A node of n triangles owns the 2n - 1 temp slots from its own: the left subtree the
+    // 2nL - 1 after it, the right one the rest.  No shared counter, so subtrees built on
+    // different threads never touch one cache line (Emit renumbers in reference order).
+    const uint32_t L = t + 1, R = t + 2 * (static_cast<uint32_t>(leftCount) / 3);
     tmp_[L] = {n.first, static_cast<uint32_t>(leftCount), {}, {}, -1, -1};
     tmp_[R] = {static_cast<uint32_t>(3 * i), n.count - static_cast<uint32_t>(leftCount), {}, {}, -1, -1};
     BoundsFast(tmp_[L]);
@@ -266,8 +269,8 @@ void TriangleMesh::SubdivideFast(uint32_t t) {
     BuildPool& pool = BuildPool::Get();
     static const uint32_t par = [] {   // RTX_HOST_PAR_TRIS: fork subtrees with at least this many triangles a side
         const char* e = std::getenv("RTX_HOST_PAR_TRIS");
-        const int v = e ? std::atoi(e) : 2048;
-        return static_cast<uint32_t>(v > 0 ? v : 2048);
+        const int v = e ? std::atoi(e) : 128;
+        return static_cast<uint32_t>(v > 0 ? v : 128);
     }();
     if (pool.Workers() > 0 && tmp_[L].count >= 3 * par && tmp_[R].count >= 3 * par) {
         BuildPool::Task task;

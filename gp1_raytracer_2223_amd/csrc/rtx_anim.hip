@@ -29,12 +29,6 @@ namespace {
 __device__ __forceinline__ float rmin(float m, float x) { return (x < m) ? x : m; }   // std::min(m, x)
 __device__ __forceinline__ float rmax(float m, float x) { return (m < x) ? x : m; }   // std::max(m, x)
 __device__ __forceinline__ float fbits(uint32_t u) { return __uint_as_float(u); }
-__device__ __forceinline__ uint32_t ubits(float f) { return __float_as_uint(f); }
-__device__ __forceinline__ float comp(const float4 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
-__device__ __forceinline__ uint32_t below(unsigned long long m) {   // set bits of m below this lane
-    return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
-                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-}
 
 // Matrix::TransformPoint / TransformVector (Matrix.cpp:35-56), m = rows data[0..3] (xyz):
 // left-to-right sums of products, no contraction.

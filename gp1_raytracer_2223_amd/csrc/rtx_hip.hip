@@ -1165,6 +1165,21 @@ template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[1]>(co
 template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[2]>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[3]>(const DevScene, const FrameArgs);
 
+// Octant copies 1..7 of an uploaded node array from copy 0 (blockIdx.y + 1 = octant k):
+// copy k stores (hi, lo) on the axes set in k, the same swap the host applies for small
+// arrays (upload_scene).  Zero padding maps to zero padding.  `n2` node records of 32 B per
+// copy (padding included), copies `stride` float4 apart.
+__global__ void __launch_bounds__(256) rtx_octant_expand(float4* __restrict__ nodes, uint32_t n2, uint32_t stride) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n2) return;
+    const uint32_t k = blockIdx.y + 1u;
+    const float4 a = nodes[2u * i], b = nodes[2u * i + 1u];
+    const bool mx = k & 1u, my = k & 2u, mz = k & 4u;
+    float4* dst = nodes + static_cast<size_t>(k) * stride;
+    dst[2u * i] = make_float4(mx ? a.y : a.x, mx ? a.x : a.y, my ? a.w : a.z, my ? a.z : a.w);
+    dst[2u * i + 1u] = make_float4(mz ? b.y : b.x, mz ? b.x : b.y, b.z, b.w);
+}
+
 // Next frames' dispatch order from this frame's per-tile cost: heaviest first, STABLE
 // within a cost class so that tiles rendered together stay spatial neighbours (they walk
 // the same BVH nodes: scalar-cache locality).  The order is (class, tile index): the same
@@ -1819,6 +1834,10 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         HIP_TRY(c, hipHostMalloc(&B.h, total));
         B.cap = total;
     }
+    // Large node arrays send copy 0 only and the device writes copies 1..7 (rtx_octant_expand):
+    // 1/8 of the node bytes over PCIe and of the host's staging writes (an upload per animated
+    // frame).  Small ones are cheaper as host writes than as one more launch.
+    const bool oct_dev = oct_ok && node_bytes >= kOctantDeviceMinBytes;
     // sections in place; only the padding up to the next section is cleared (an upload per
     // animated frame: no full-image memset, no intermediate node image)
     for (size_t i = 0; i < sizeof secs / sizeof secs[0]; ++i) {
@@ -1826,7 +1845,7 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         const size_t end = i + 1 < sizeof secs / sizeof secs[0] ? secs[i + 1].off : total;
         if (x.p && x.n) std::memcpy(B.h + x.off, x.p, x.n);
         if (!x.p && x.n && oct_ok) {   // octant copy k stores (hi, lo) on the axes set in k
-            for (int k = 0; k < 8; ++k) {
+            for (int k = 0; k < (oct_dev ? 1 : 8); ++k) {
                 float4* dst = reinterpret_cast<float4*>(B.h + x.off + k * node_bytes);
                 const bool mx = k & 1, my = k & 2, mz = k & 4;
                 for (size_t n = 0; n < nodes.size(); n += 2) {
@@ -1841,7 +1860,17 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         }
         std::memset(B.h + x.off + x.n, 0, end - x.off - x.n);
     }
-    HIP_TRY(c, hipMemcpyAsync(B.d, B.h, total, hipMemcpyHostToDevice, c->stream));
+    if (oct_dev) {   // everything but copies 1..7, which the device writes
+        const size_t c1 = secs[4].off + node_bytes, c8 = secs[4].off + 8 * node_bytes;
+        HIP_TRY(c, hipMemcpyAsync(B.d, B.h, c1, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(B.d + c8, B.h + c8, total - c8, hipMemcpyHostToDevice, c->stream));
+        const uint32_t n2 = static_cast<uint32_t>(node_bytes / 32);
+        hipLaunchKernelGGL(rtx_octant_expand, dim3((n2 + 255) / 256, 7), dim3(256), 0, c->stream,
+                           reinterpret_cast<float4*>(B.d + secs[4].off), n2, static_cast<uint32_t>(node_bytes / 16));
+        HIP_TRY(c, hipGetLastError());
+    } else {
+        HIP_TRY(c, hipMemcpyAsync(B.d, B.h, total, hipMemcpyHostToDevice, c->stream));
+    }
     if (c->sb_cur >= 0) {   // every frame queued so far reads the previous image
         rtx_ctx::SceneBuf& O = c->sb[c->sb_cur];
         HIP_TRY(c, hipEventRecord(O.done, c->stream));

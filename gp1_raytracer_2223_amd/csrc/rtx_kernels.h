@@ -110,6 +110,7 @@ struct DevScene {
 };
 
 constexpr size_t kOctantMaxNodeBytes = size_t(1) << 20;   // octant node copies only below this (per copy)
+constexpr size_t kOctantDeviceMinBytes = size_t(64) << 10;   // from this size copies 1..7 are written on the device
 constexpr int kMaxViews = 8;   // views (camera positions) rendered by one launch
 
 struct ViewCam {
