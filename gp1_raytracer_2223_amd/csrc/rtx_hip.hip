@@ -162,6 +162,36 @@ __device__ __forceinline__ float plane_num(const float4 p0, const float4 p1, con
 __device__ __forceinline__ float plane_den(const float4 p1, const Ray& r) {
     return r.dx * p1.x + r.dy * p1.y + r.dz * p1.z;
 }
+// The room's planes (kSpecRoomPlanes, rtx_kernels.h): plane k's normal is zero except on axis
+// A = kRoomAxes[k], and its origin is finite with |p0| <= 2^64.  For a ray with a finite origin
+// every other term of HitTest_Plane's two dot products is a signed zero (p0 - o cannot
+// overflow), so the reference's num and den equal
+//   num = (p0_A - o_A) * n_A,   den = d_A * n_A
+// whenever these are non-zero (x + +-0 = x, inf included).  When either is zero the quotient is
+// +-0, +-inf or NaN, which fails t >= tmin > 0 or t < tmax <= FLT_MAX in both forms, whatever the
+// zero's sign; so does a NaN / infinite direction component, which leaves den 0, +-inf or NaN
+// here and NaN in the reference (a normalised direction is finite unless its length was 0 or
+// inf).  Same hits, same t: 2 + 1 VALU instead of 8 + 5 per plane test.
+template <int A>
+__device__ __forceinline__ float room_num(const float4 p0, const float4 p1, const Ray& r) {
+    return A == 0 ? (p0.x - r.ox) * p1.x : (A == 1 ? (p0.y - r.oy) * p1.y : (p0.z - r.oz) * p1.z);
+}
+template <int A>
+__device__ __forceinline__ float room_den(const float4 p1, const Ray& r) {
+    return A == 0 ? r.dx * p1.x : (A == 1 ? r.dy * p1.y : r.dz * p1.z);
+}
+// f(integral_constant<int, k>) for the room's planes k = 0..4, in order
+template <class Fn>
+__device__ __forceinline__ void for_room_planes(Fn&& f) {
+    f(std::integral_constant<int, 0>{});
+    f(std::integral_constant<int, 1>{});
+    f(std::integral_constant<int, 2>{});
+    f(std::integral_constant<int, 3>{});
+    f(std::integral_constant<int, 4>{});
+}
+__device__ __forceinline__ bool finite3(float x, float y, float z) {
+    return __builtin_isfinite(x) & __builtin_isfinite(y) & __builtin_isfinite(z);
+}
 // Over-inclusive is harmless (it only decides whether the division runs): equal sign bits
 // admit zeros and NaNs too, which then fail the range test on t.
 __device__ __forceinline__ unsigned long long plane_same_sign(float num, float den) {
@@ -775,6 +805,7 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
     constexpr bool kNoSph = (SPEC & kSpecNoSpheres) != 0, kComb = (SPEC & kSpecCombShadows) != 0;
     constexpr bool kP5 = (SPEC & kSpecFivePlanes) != 0, kOneMesh = (SPEC & kSpecOneMesh) != 0;
     constexpr bool kNoMesh = (SPEC & kSpecNoMesh) != 0;
+    constexpr bool kRoom = (SPEC & kSpecRoomPlanes) != 0 && (SPEC & kSpecFivePlanes) != 0;
 #define f_mode (kComb ? RTX_MODE_COMBINED : F.mode)
 #define f_shadows (kComb ? 1 : F.shadows)
 #define n_sph (kNoSph ? 0u : S.n_spheres)
@@ -888,7 +919,23 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
         best_kind = b ? 1u : best_kind;
         best_idx = b ? i : best_idx;
     }
-    for (uint32_t i = 0; i < ((RTX_ABL_PPLANE) ? 0u : n_pl * 32u); i += 32u) {
+    // the room's planes as single products (room_num), for a wave whose ray origins are finite
+    const bool room_p = kRoom && !RTX_ABL_PPLANE && (active & ~ballot(finite3(vr.ox, vr.oy, vr.oz))) == 0;
+    if (room_p) {
+        for_room_planes([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            float4 p0, p1;
+            ldcb32(S.planes, k * 32u, p0, p1);
+            const float t = room_num<kRoomAxes[k]>(p0, p1, vr) / room_den<kRoomAxes[k]>(p1, vr);
+            const bool h = valid & (t >= vr.tmin) & (t < vr.tmax);
+            sc_t = h ? t : sc_t;
+            const bool b = h & (t < best_t);
+            best_t = b ? t : best_t;
+            best_kind = b ? 2u : best_kind;
+            best_idx = b ? static_cast<uint32_t>(k * 32) : best_idx;
+        });
+    }
+    for (uint32_t i = 0; i < ((RTX_ABL_PPLANE || room_p) ? 0u : n_pl * 32u); i += 32u) {
         float4 p0, p1;
         ldcb32(S.planes, opaque(i), p0, p1);
         if (COUNT && valid) cnt.c[kPlane]++;
@@ -972,6 +1019,9 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
         // originOffset = hit.origin + hit.normal * 0.0001f (Renderer.cpp:126)
         const float oox = hx + nx * 0.0001f, ooy = hy + ny * 0.0001f, ooz = hz + nz * 0.0001f;
         const float vx = -dx, vy = -dy, vz = -dz;
+        // shadow rays start at originOffset for every light: one finiteness test for all of them
+        const bool room_s =
+            kRoom && PHASE != 2 && !RTX_ABL_SPLANE && (hitmask & ~ballot(finite3(oox, ooy, ooz))) == 0;
         const uint32_t l_first = PHASE == 2 ? light : 0u, l_end = PHASE == 2 ? light + 1 : (RTX_ABL_LIGHTS ? 0u : S.n_lights);
         for (uint32_t li = l_first; li < l_end; ++li) {
             float4 L0, L1;
@@ -1010,9 +1060,20 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
                 // the same originOffset for every light: the first light computes it and keeps it
                 // in LDS, the others read it back (same value, bit for bit).  One loop version
                 // per case, so no per-plane select.
-                const uint32_t np = (RTX_ABL_SPLANE || PHASE == 2) ? 0u : n_pl * 32u;
+                const uint32_t np = (RTX_ABL_SPLANE || PHASE == 2 || room_s) ? 0u : n_pl * 32u;
                 const bool cache_ok = RTX_PNUM_CACHE && !COUNT && np <= static_cast<uint32_t>(kPlaneCache) * 32u;
-                if (cache_ok && li != l_first) {
+                if (room_s) {   // single products (room_num): cheaper than the cached numerator
+                    for_room_planes([&](auto kc) {
+                        constexpr int k = decltype(kc)::value;
+                        float4 p0, p1;
+                        ldcb32(S.planes, k * 32u, p0, p1);
+                        const float num = room_num<kRoomAxes[k]>(p0, p1, sr), den = room_den<kRoomAxes[k]>(p1, sr);
+                        const unsigned long long cand = plane_cand(num, den, sr.tmax) & live;
+                        if (!cand) return;
+                        const float t = num / den;
+                        live &= ~(ballot(t >= sr.tmin) & ballot(t < sr.tmax) & cand);
+                    });
+                } else if (cache_ok && li != l_first) {
                     for (uint32_t i = 0; i < np; i += 32u) {
                         float4 p0, p1;
                         ldcb32(S.planes, opaque(i), p0, p1);
@@ -1164,6 +1225,7 @@ template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[0]>(co
 template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[1]>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[2]>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[3]>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[4]>(const DevScene, const FrameArgs);
 
 // Octant copies 1..7 of an uploaded node array from copy 0 (blockIdx.y + 1 = octant k):
 // copy k stores (hi, lo) on the axes set in k, the same swap the host applies for small
@@ -1910,9 +1972,20 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         for (uint32_t i = 0; i < s->n_planes; ++i) kind(s->planes[i].material);
         for (uint32_t i = 0; i < s->n_meshes; ++i) kind(s->meshes[i].material);
         for (uint32_t i = 0; i < s->n_lights; ++i) point = point && s->lights[i].type == RTX_LIGHT_POINT;
+        // the room's planes (kSpecRoomPlanes): one non-zero normal component each, on axis
+        // kRoomAxes[k], and origins finite within 2^64
+        bool room = s->n_planes == 5;
+        for (uint32_t i = 0; room && i < 5; ++i) {
+            const rtx_plane& p = s->planes[i];
+            for (int a = 0; a < 3; ++a) {
+                const float n = p.normal[a], o = p.origin[a];
+                room = room && (a == kRoomAxes[i] ? (std::isfinite(n) && n != 0.f) : n == 0.f) &&
+                       std::isfinite(o) && std::fabs(o) <= 0x1p64f;
+            }
+        }
         c->scene_spec = kinds | (point ? kSpecPoint : 0) | (s->n_spheres == 0 ? kSpecNoSpheres : 0) |
                         (s->n_planes == 5 ? kSpecFivePlanes : 0) | (s->n_meshes == 1 ? kSpecOneMesh : 0) |
-                        (s->n_meshes == 0 ? kSpecNoMesh : 0);
+                        (s->n_meshes == 0 ? kSpecNoMesh : 0) | (room ? kSpecRoomPlanes : 0);
     }
     c->split_ok = split_ok && !parts.empty() && !c->deep_stack;
     c->has_scene = true;
@@ -2119,6 +2192,9 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
                            c->stream, c->dev, F);
     else if (v == 3)
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecVariants[3]>), grid, dim3(kBlockThreads), 0,
+                           c->stream, c->dev, F);
+    else if (v == 4)
+        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecVariants[4]>), grid, dim3(kBlockThreads), 0,
                            c->stream, c->dev, F);
     else
         hipLaunchKernelGGL((rtx_render_kernel<false, 0>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);

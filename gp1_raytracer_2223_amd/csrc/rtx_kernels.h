@@ -47,17 +47,26 @@ constexpr int kSpecCombShadows = 64;   // lighting mode Combined, shadows on
 constexpr int kSpecFivePlanes = 128;   // exactly 5 planes (the reference's room: W3, W4, the synthetic scenes)
 constexpr int kSpecOneMesh = 256;      // exactly 1 triangle mesh
 constexpr int kSpecNoMesh = 512;       // no triangle mesh
+// The 5 planes are the reference's room (RoomPlanes, Scene.cpp:263-267): plane k's normal has
+// exactly one non-zero component, on axis kRoomAxes[k], and every origin coordinate is finite
+// with magnitude <= 2^64.  Then, for a ray with a finite origin, HitTest_Plane's two dot
+// products reduce to that axis's product whenever it is non-zero, and when it is zero the
+// plane cannot be hit either way (rtx_hip.hip, room_plane_t).
+constexpr int kSpecRoomPlanes = 1024;
+constexpr int kRoomAxes[5] = {2, 1, 1, 0, 0};
 // The compiled variants, most specific first (the launch takes the first one whose facts hold):
 //   0  Lambert only, one mesh, no spheres (W4_Bunny, Synthetic100k, Bunny + 8 lights)
 //   1  Lambert + Cook-Torrance, one mesh, no spheres (W4_Optional)
 //   2  Lambert + Cook-Torrance, spheres, no mesh (W3)
 //   3  Lambert + Cook-Torrance, spheres and meshes (W4_Reference)
-// all with point lights, 5 planes, Combined lighting + shadows.
+//   4  as 3 for five planes of any other arrangement
+// all with point lights, 5 planes, Combined lighting + shadows; 0-3 in the room.
 constexpr int kSpecCommon = kSpecPoint | kSpecCombShadows | kSpecFivePlanes;
 constexpr int kSpecVariants[] = {
-    kSpecCommon | kSpecKindLambert | kSpecNoSpheres | kSpecOneMesh,
-    kSpecCommon | kSpecKindLambert | kSpecKindCT | kSpecNoSpheres | kSpecOneMesh,
-    kSpecCommon | kSpecKindLambert | kSpecKindCT | kSpecNoMesh,
+    kSpecCommon | kSpecRoomPlanes | kSpecKindLambert | kSpecNoSpheres | kSpecOneMesh,
+    kSpecCommon | kSpecRoomPlanes | kSpecKindLambert | kSpecKindCT | kSpecNoSpheres | kSpecOneMesh,
+    kSpecCommon | kSpecRoomPlanes | kSpecKindLambert | kSpecKindCT | kSpecNoMesh,
+    kSpecCommon | kSpecRoomPlanes | kSpecKindLambert | kSpecKindCT,
     kSpecCommon | kSpecKindLambert | kSpecKindCT,
 };
 

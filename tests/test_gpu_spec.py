@@ -54,3 +54,31 @@ def test_specialised_bunny_bit_exact_vs_oracle(gpu_ctx, name):
     gpx, grgb = gpu_ctx.render(cam, p)
     rpx, rrgb = oracle_bind.render(s, cam, p)
     assert np.array_equal(gpx, rpx) and np.array_equal(grgb.view(np.uint32), rrgb.view(np.uint32))
+
+
+# Camera origins around the room planes' single-product form (room_num, kSpecRoomPlanes): on a
+# plane (num = 0), on two planes at once, far outside the room, huge but finite (the 2^64
+# no-overflow bound is on the planes, not the ray), and non-finite (the wave falls back to the
+# full dot products).  481 x 271 puts a pixel column and row exactly on the view axis, so
+# direction components are exactly zero there (den = 0 on the planes across that axis).
+ROOM_ORIGINS = [(0.0, 0.0, -30.0), (5.0, 0.0, -30.0), (0.0, 5.0, 10.0), (-20.0, 3.0, 40.0),
+                (1e30, 2e30, -3e30), (3e38, -3e38, 1.0), (float("inf"), 3.0, -30.0), (float("nan"), 3.0, -30.0)]
+
+
+@pytest.mark.parametrize("origin", ROOM_ORIGINS)
+def test_room_planes_edge_origins_equal_generic(gpu_ctx, generic_ctx, origin):
+    hs = HostScene("W4_Bunny")
+    s, cam = hs.view()
+    for k in range(3):
+        cam.origin[k] = origin[k]
+    p = abi.make_params(481, 271)
+    gpu_ctx.upload(s)
+    generic_ctx.upload(s)
+    for _ in range(2):
+        apx, argb = gpu_ctx.render(cam, p)
+        bpx, brgb = generic_ctx.render(cam, p)
+        assert np.array_equal(apx, bpx), f"{origin}: {(apx != bpx).sum()} pixels differ"
+        assert np.array_equal(argb.view(np.uint32), brgb.view(np.uint32))
+    if all(np.isfinite(origin)) and max(abs(x) for x in origin) < 1e3:
+        rpx, rrgb = oracle_bind.render(s, cam, p)
+        assert np.array_equal(apx, rpx) and np.array_equal(argb.view(np.uint32), rrgb.view(np.uint32))
