@@ -162,23 +162,29 @@ __device__ __forceinline__ float plane_num(const float4 p0, const float4 p1, con
 __device__ __forceinline__ float plane_den(const float4 p1, const Ray& r) {
     return r.dx * p1.x + r.dy * p1.y + r.dz * p1.z;
 }
-// The room's planes (kSpecRoomPlanes, rtx_kernels.h): plane k's normal is zero except on axis
-// A = kRoomAxes[k], and its origin is finite with |p0| <= 2^64.  For a ray with a finite origin
-// every other term of HitTest_Plane's two dot products is a signed zero (p0 - o cannot
-// overflow), so the reference's num and den equal
-//   num = (p0_A - o_A) * n_A,   den = d_A * n_A
-// whenever these are non-zero (x + +-0 = x, inf included).  When either is zero the quotient is
-// +-0, +-inf or NaN, which fails t >= tmin > 0 or t < tmax <= FLT_MAX in both forms, whatever the
-// zero's sign; so does a NaN / infinite direction component, which leaves den 0, +-inf or NaN
-// here and NaN in the reference (a normalised direction is finite unless its length was 0 or
-// inf).  Same hits, same t: 2 + 1 VALU instead of 8 + 5 per plane test.
+// The room's planes (kSpecRoomPlanes, rtx_kernels.h): plane k's normal is s = +-1 on axis
+// A = kRoomAxes[k] and zero elsewhere, its origin finite with |p0| <= 2^64.  For a ray with a
+// finite origin every other term of HitTest_Plane's two dot products is a signed zero (p0 - o
+// cannot overflow), so the reference's num and den are s * a and s * d with
+//   a = p0_A - o_A,   d = d_A
+// whenever those are non-zero (x + +-0 = x, inf included), and its t = num / den = a / d (IEEE
+// division is sign-symmetric); the same-sign and beyond tests of plane_cand read the same
+// signs and magnitudes.  When a or d is zero the quotient is +-0, +-inf or NaN, which fails
+// t >= tmin > 0 or t < tmax <= FLT_MAX in both forms whatever the zero's sign; so does a NaN /
+// infinite direction component, which leaves d 0, +-inf or NaN here and den NaN in the
+// reference (a normalised direction is finite unless its length was 0 or inf).  Same hits,
+// same t, 1 VALU instead of 13 before the division.
 template <int A>
-__device__ __forceinline__ float room_num(const float4 p0, const float4 p1, const Ray& r) {
-    return A == 0 ? (p0.x - r.ox) * p1.x : (A == 1 ? (p0.y - r.oy) * p1.y : (p0.z - r.oz) * p1.z);
+__device__ __forceinline__ float room_a(const float4 p0, const Ray& r) {
+    return A == 0 ? p0.x - r.ox : (A == 1 ? p0.y - r.oy : p0.z - r.oz);
 }
 template <int A>
-__device__ __forceinline__ float room_den(const float4 p1, const Ray& r) {
-    return A == 0 ? r.dx * p1.x : (A == 1 ? r.dy * p1.y : r.dz * p1.z);
+__device__ __forceinline__ float room_d(const Ray& r) {
+    return A == 0 ? r.dx : (A == 1 ? r.dy : r.dz);
+}
+template <int A>
+__device__ __forceinline__ float room_inv(const Ray& r) {
+    return A == 0 ? r.ix : (A == 1 ? r.iy : r.iz);
 }
 // f(integral_constant<int, k>) for the room's planes k = 0..4, in order
 template <class Fn>
@@ -919,14 +925,24 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
         best_kind = b ? 1u : best_kind;
         best_idx = b ? i : best_idx;
     }
-    // the room's planes as single products (room_num), for a wave whose ray origins are finite
+    // the room's planes as a / d (room_a), for a wave whose ray origins are finite.  The camera
+    // numerators come from the host (ViewCam::room_a); in a FAST wave every d is inside div_rn's
+    // divisor domain with its RN(1/d) already in the ray, so when the host found the numerators
+    // inside theirs too, t = RN(a / d) costs 3 VALU instead of the 11 of IEEE `/`.
     const bool room_p = kRoom && !RTX_ABL_PPLANE && (active & ~ballot(finite3(vr.ox, vr.oy, vr.oz))) == 0;
     if (room_p) {
+        const bool mk = fast && V.room_fast;
         for_room_planes([&](auto kc) {
             constexpr int k = decltype(kc)::value;
-            float4 p0, p1;
-            ldcb32(S.planes, k * 32u, p0, p1);
-            const float t = room_num<kRoomAxes[k]>(p0, p1, vr) / room_den<kRoomAxes[k]>(p1, vr);
+            constexpr int A = kRoomAxes[k];
+            float t;
+            if (mk) {
+                t = div_rn(V.room_a[k], room_d<A>(vr), room_inv<A>(vr));
+            } else {
+                float4 p0, p1;
+                ldcb32(S.planes, k * 32u, p0, p1);
+                t = room_a<A>(p0, vr) / room_d<A>(vr);
+            }
             const bool h = valid & (t >= vr.tmin) & (t < vr.tmax);
             sc_t = h ? t : sc_t;
             const bool b = h & (t < best_t);
@@ -1062,12 +1078,13 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
                 // per case, so no per-plane select.
                 const uint32_t np = (RTX_ABL_SPLANE || PHASE == 2 || room_s) ? 0u : n_pl * 32u;
                 const bool cache_ok = RTX_PNUM_CACHE && !COUNT && np <= static_cast<uint32_t>(kPlaneCache) * 32u;
-                if (room_s) {   // single products (room_num): cheaper than the cached numerator
+                if (room_s) {   // a / d (room_a): cheaper than the cached numerator
                     for_room_planes([&](auto kc) {
                         constexpr int k = decltype(kc)::value;
+                        constexpr int A = kRoomAxes[k];
                         float4 p0, p1;
                         ldcb32(S.planes, k * 32u, p0, p1);
-                        const float num = room_num<kRoomAxes[k]>(p0, p1, sr), den = room_den<kRoomAxes[k]>(p1, sr);
+                        const float num = room_a<A>(p0, sr), den = room_d<A>(sr);
                         const unsigned long long cand = plane_cand(num, den, sr.tmax) & live;
                         if (!cand) return;
                         const float t = num / den;
@@ -1468,6 +1485,7 @@ struct rtx_ctx {
     bool split_ok = false;           // the uploaded scene admits split rendering
     bool deep_stack = false;         // the uploaded scene needs rtx_render_kernel<..., DEEP = true>
     int scene_spec = 0;              // kSpec* facts of the uploaded scene (kernel specialisation)
+    float room_p0[5] = {};           // kSpecRoomPlanes: plane k's origin on axis kRoomAxes[k]
     bool no_spec = false;            // RTX_NO_SPEC=1: always the generic kernel (tests)
     unsigned long long* d_hit_key = nullptr;
     uint32_t* d_occ = nullptr;
@@ -1972,17 +1990,18 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         for (uint32_t i = 0; i < s->n_planes; ++i) kind(s->planes[i].material);
         for (uint32_t i = 0; i < s->n_meshes; ++i) kind(s->meshes[i].material);
         for (uint32_t i = 0; i < s->n_lights; ++i) point = point && s->lights[i].type == RTX_LIGHT_POINT;
-        // the room's planes (kSpecRoomPlanes): one non-zero normal component each, on axis
-        // kRoomAxes[k], and origins finite within 2^64
+        // the room's planes (kSpecRoomPlanes): normal +-1 on axis kRoomAxes[k], zero elsewhere,
+        // origins finite within 2^64
         bool room = s->n_planes == 5;
         for (uint32_t i = 0; room && i < 5; ++i) {
             const rtx_plane& p = s->planes[i];
             for (int a = 0; a < 3; ++a) {
                 const float n = p.normal[a], o = p.origin[a];
-                room = room && (a == kRoomAxes[i] ? (std::isfinite(n) && n != 0.f) : n == 0.f) &&
-                       std::isfinite(o) && std::fabs(o) <= 0x1p64f;
+                room = room && (a == kRoomAxes[i] ? (n == 1.f || n == -1.f) : n == 0.f) && std::isfinite(o) &&
+                       std::fabs(o) <= 0x1p64f;
             }
         }
+        for (uint32_t i = 0; room && i < 5; ++i) c->room_p0[i] = s->planes[i].origin[kRoomAxes[i]];
         c->scene_spec = kinds | (point ? kSpecPoint : 0) | (s->n_spheres == 0 ? kSpecNoSpheres : 0) |
                         (s->n_planes == 5 ? kSpecFivePlanes : 0) | (s->n_meshes == 1 ? kSpecOneMesh : 0) |
                         (s->n_meshes == 0 ? kSpecNoMesh : 0) | (room ? kSpecRoomPlanes : 0);
@@ -2045,6 +2064,16 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
             F.cam[v].up[k] = cams[v].up[k]; F.cam[v].forward[k] = cams[v].forward[k];
         }
         F.cam[v].fov = cams[v].fov;
+        if (c->scene_spec & kSpecRoomPlanes) {   // the room planes' camera numerators (ViewCam)
+            bool ok = true;
+            for (int k = 0; k < 5; ++k) {
+                const float a = c->room_p0[k] - cams[v].origin[kRoomAxes[k]];
+                const float aa = std::fabs(a);
+                F.cam[v].room_a[k] = a;
+                ok = ok && (a == 0.f || (aa >= 0x1p-60f && aa <= 0x1p60f));
+            }
+            F.cam[v].room_fast = ok ? 1u : 0u;
+        }
     }
     F.aspect = static_cast<int>(p->width) / static_cast<float>(static_cast<int>(p->height));  // Renderer.cpp:30
     F.inv_width = 1.f / static_cast<float>(static_cast<int>(p->width));
@@ -2478,6 +2507,7 @@ struct rtx_anim {
     DevScene dev{};                       // pointers relative to the image base
     bool split_ok = false;
     int spec = 0;
+    float room_p0[5] = {};   // rtx_ctx::room_p0 of the registration upload
     std::string sig;
     hipEvent_t ev = nullptr;              // the last update
     uint32_t lds_bytes = 0;               // dynamic LDS of the build launch
@@ -2597,6 +2627,7 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
     a->dev.tri_fast = lay.max_ee <= 0x1p55 ? 1u : 0u;
     a->split_ok = c->split_ok;
     a->spec = c->scene_spec;
+    std::memcpy(a->room_p0, c->room_p0, sizeof a->room_p0);
     a->sig = c->scene_sig;
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t id = static_cast<uint32_t>(ids[i]);
@@ -2714,6 +2745,7 @@ extern "C" int rtx_anim_update(rtx_anim* a, rtx_ctx* c, const float* transforms)
     c->deep_stack = false;
     c->split_ok = a->split_ok;
     c->scene_spec = a->spec;
+    std::memcpy(c->room_p0, a->room_p0, sizeof c->room_p0);
     c->has_scene = true;
     ++c->scene_gen;
     c->scene_sig = a->sig;

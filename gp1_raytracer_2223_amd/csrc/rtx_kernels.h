@@ -47,11 +47,10 @@ constexpr int kSpecCombShadows = 64;   // lighting mode Combined, shadows on
 constexpr int kSpecFivePlanes = 128;   // exactly 5 planes (the reference's room: W3, W4, the synthetic scenes)
 constexpr int kSpecOneMesh = 256;      // exactly 1 triangle mesh
 constexpr int kSpecNoMesh = 512;       // no triangle mesh
-// The 5 planes are the reference's room (RoomPlanes, Scene.cpp:263-267): plane k's normal has
-// exactly one non-zero component, on axis kRoomAxes[k], and every origin coordinate is finite
-// with magnitude <= 2^64.  Then, for a ray with a finite origin, HitTest_Plane's two dot
-// products reduce to that axis's product whenever it is non-zero, and when it is zero the
-// plane cannot be hit either way (rtx_hip.hip, room_plane_t).
+// The 5 planes are the reference's room (RoomPlanes, Scene.cpp:263-267): plane k's normal is
+// +-1 on axis kRoomAxes[k] and zero elsewhere, and every origin coordinate is finite with
+// magnitude <= 2^64.  Then, for a ray with a finite origin, HitTest_Plane's quotient is
+// (p0_A - o_A) / d_A whenever the plane can be hit (rtx_hip.hip, room_a).
 constexpr int kSpecRoomPlanes = 1024;
 constexpr int kRoomAxes[5] = {2, 1, 1, 0, 0};
 // The compiled variants, most specific first (the launch takes the first one whose facts hold):
@@ -128,7 +127,11 @@ struct ViewCam {
     float up[3];
     float forward[3];
     float fov;
-    float _pad[3];
+    // room planes (kSpecRoomPlanes): p0_A - origin_A per plane, binary32 on the host, and
+    // whether all five are 0 or in [2^-60, 2^60] (div_rn's numerator domain, rtx_fastdiv.h)
+    float room_a[5];
+    uint32_t room_fast;
+    float _pad[1];
 };
 
 struct FrameArgs {

@@ -57,11 +57,13 @@ def test_specialised_bunny_bit_exact_vs_oracle(gpu_ctx, name):
 
 
 # Camera origins around the room planes' single-product form (room_num, kSpecRoomPlanes): on a
-# plane (num = 0), on two planes at once, far outside the room, huge but finite (the 2^64
+# plane (num = 0), on two planes at once, far outside the room, numerators outside div_rn's
+# domain (|a| < 2^-60 or > 2^60: the IEEE quotient instead), huge but finite (the 2^64
 # no-overflow bound is on the planes, not the ray), and non-finite (the wave falls back to the
 # full dot products).  481 x 271 puts a pixel column and row exactly on the view axis, so
 # direction components are exactly zero there (den = 0 on the planes across that axis).
 ROOM_ORIGINS = [(0.0, 0.0, -30.0), (5.0, 0.0, -30.0), (0.0, 5.0, 10.0), (-20.0, 3.0, 40.0),
+                (1e-20, 1e-25, -30.0), (0.0, 1e19, -30.0),
                 (1e30, 2e30, -3e30), (3e38, -3e38, 1.0), (float("inf"), 3.0, -30.0), (float("nan"), 3.0, -30.0)]
 
 
