@@ -271,11 +271,13 @@ __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const flo
 // skipped — no lane hits it — else true with the reject score in `rej_out` and t in `t`.
 // (A uniform flag rather than a reject value: a phi of the reject compare is carried as a
 // lane mask and rebuilt with v_cndmask + v_cmp per triangle.)
-template <bool FAST>
+// CB (kSpecCullBack): the mesh culls back faces, so cs is +1 for camera rays and -1 for shadow
+// rays (ANY) and cs * cullDot is +-cullDot exactly: a source negation instead of a multiply.
+template <bool FAST, bool CB = false, bool ANY = false>
 __device__ __forceinline__ bool tri_t_wave(const float4 A, const float4 B, const float4 C, float cs, const Ray& r,
                                            unsigned long long act, float& rej_out, float& t) {
     const float cullDot = A.w * r.dx + B.w * r.dy + C.w * r.dz;
-    float rej = fmaxf(FLT_EPSILON - fabsf(cullDot), cs * cullDot);
+    float rej = fmaxf(FLT_EPSILON - fabsf(cullDot), CB ? (ANY ? -cullDot : cullDot) : cs * cullDot);
     if ((ballot(!(rej > 0.f)) & act) == 0) return false;
     const float hx = r.dy * C.z - r.dz * C.y;
     const float hy = -(r.dx * C.z - r.dz * C.x);
@@ -523,7 +525,7 @@ constexpr int kPlaneCache = 8;   // planes whose shadow-ray numerators are kept 
 // VGPR boolean or a lane-mask flow variable), a dead end leaves it as an empty "leaf", and
 // the pop loop is the only other path.  Same visits, tests and order as bvh_walk.
 // `nb` is the node copy the slab form reads (the octant's (near, far) copy for kSlabOct).
-template <bool ANY, int SLAB>
+template <bool ANY, int SLAB, bool CB = false>
 __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, const Ray& r, uint32_t link,
                               uint32_t ntri, unsigned long long m, unsigned long long mask, uint32_t lane, uint4* stk,
                               float& sc_t, uint32_t& sc_tri, unsigned long long& live, const uint32_t* occ_word,
@@ -582,7 +584,7 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                 float t;
 #if RTX_TRI_EARLY
                 float rej;
-                if (!tri_t_wave<FAST>(T.a, T.b, T.c, cs, r, ANY ? (m & live) : m, rej, t)) continue;
+                if (!tri_t_wave<FAST, CB, ANY>(T.a, T.b, T.c, cs, r, ANY ? (m & live) : m, rej, t)) continue;
 #else
                 const float rej = tri_t<FAST>(T.a, T.b, T.c, cs, r, t);
 #endif
@@ -614,7 +616,7 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
 }
 
 // SLAB = kSlabOct: `oct` is the batch's octant (batch_octant), else ignored.
-template <bool ANY, int SLAB, bool COUNT>
+template <bool ANY, int SLAB, bool COUNT, bool CB = false>
 __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int oct, unsigned long long mask,
                               uint32_t lane, uint4* stk, unsigned long long* sT, float& sc_t, uint32_t& sc_tri,
                               unsigned long long& live, Counts& cnt) {
@@ -632,7 +634,7 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
         (OCT ? slab_mask<kSlabOct>(b0, b1, r) : slab_mask<FAST ? kSlabFast : kSlabExact>(b0, b1, r)) & mask;
     if (m == 0) return;
     if (RTX_LEAN_WALK && !COUNT && !RTX_STAMPS)
-        bvh_walk_lean<ANY, OCT ? kSlabOct : (FAST ? kSlabFast : kSlabExact)>(
+        bvh_walk_lean<ANY, OCT ? kSlabOct : (FAST ? kSlabFast : kSlabExact), CB>(
             S, nb, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask, lane, stk, sc_t,
             sc_tri, live, nullptr, 0u);
     else
@@ -812,6 +814,7 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
     constexpr bool kP5 = (SPEC & kSpecFivePlanes) != 0, kOneMesh = (SPEC & kSpecOneMesh) != 0;
     constexpr bool kNoMesh = (SPEC & kSpecNoMesh) != 0;
     constexpr bool kRoom = (SPEC & kSpecRoomPlanes) != 0 && (SPEC & kSpecFivePlanes) != 0;
+    constexpr bool kCullBack = (SPEC & kSpecCullBack) != 0 && !COUNT;
 #define f_mode (kComb ? RTX_MODE_COMBINED : F.mode)
 #define f_shadows (kComb ? 1 : F.shadows)
 #define n_sph (kNoSph ? 0u : S.n_spheres)
@@ -973,11 +976,14 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
             uint32_t sc_tri = 0;
             unsigned long long unused = 0;
             if (poct >= 0)
-                mesh_traverse<false, kSlabOct, COUNT>(S, M, vr, poct, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
+                mesh_traverse<false, kSlabOct, COUNT, kCullBack>(S, M, vr, poct, active, lane, stk, sT, sc_t, sc_tri,
+                                                                 unused, cnt);
             else if (fast)
-                mesh_traverse<false, kSlabFast, COUNT>(S, M, vr, 0, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
+                mesh_traverse<false, kSlabFast, COUNT, kCullBack>(S, M, vr, 0, active, lane, stk, sT, sc_t, sc_tri,
+                                                                  unused, cnt);
             else
-                mesh_traverse<false, kSlabExact, COUNT>(S, M, vr, 0, active, lane, stk, sT, sc_t, sc_tri, unused, cnt);
+                mesh_traverse<false, kSlabExact, COUNT, kCullBack>(S, M, vr, 0, active, lane, stk, sT, sc_t, sc_tri,
+                                                                   unused, cnt);
             if (sc_t < best_t) { best_t = sc_t; best_kind = 3; best_idx = sc_tri; }
         }
     } else if (PHASE == 1) {
@@ -1120,11 +1126,14 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
                     uint32_t stri = 0;
                     const int4 M = ldcb16i(S.meshes, opaque(mi * 16u));
                     if (soct >= 0)
-                        mesh_traverse<true, kSlabOct, COUNT>(S, M, sr, soct, live, lane, stk, sT, st, stri, live, cnt);
+                        mesh_traverse<true, kSlabOct, COUNT, kCullBack>(S, M, sr, soct, live, lane, stk, sT, st, stri,
+                                                                        live, cnt);
                     else if (sfast)
-                        mesh_traverse<true, kSlabFast, COUNT>(S, M, sr, 0, live, lane, stk, sT, st, stri, live, cnt);
+                        mesh_traverse<true, kSlabFast, COUNT, kCullBack>(S, M, sr, 0, live, lane, stk, sT, st, stri,
+                                                                         live, cnt);
                     else
-                        mesh_traverse<true, kSlabExact, COUNT>(S, M, sr, 0, live, lane, stk, sT, st, stri, live, cnt);
+                        mesh_traverse<true, kSlabExact, COUNT, kCullBack>(S, M, sr, 0, live, lane, stk, sT, st, stri,
+                                                                          live, cnt);
                 }
                 if (PHASE == 2) {
                     const int4 E = ldc(S.parts, part);
@@ -1990,6 +1999,8 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         for (uint32_t i = 0; i < s->n_planes; ++i) kind(s->planes[i].material);
         for (uint32_t i = 0; i < s->n_meshes; ++i) kind(s->meshes[i].material);
         for (uint32_t i = 0; i < s->n_lights; ++i) point = point && s->lights[i].type == RTX_LIGHT_POINT;
+        bool cull_back = true;   // kSpecCullBack: every mesh culls back faces
+        for (uint32_t i = 0; i < s->n_meshes; ++i) cull_back = cull_back && s->meshes[i].cull_mode == RTX_CULL_BACK;
         // the room's planes (kSpecRoomPlanes): normal +-1 on axis kRoomAxes[k], zero elsewhere,
         // origins finite within 2^64
         bool room = s->n_planes == 5;
@@ -2004,7 +2015,8 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         for (uint32_t i = 0; room && i < 5; ++i) c->room_p0[i] = s->planes[i].origin[kRoomAxes[i]];
         c->scene_spec = kinds | (point ? kSpecPoint : 0) | (s->n_spheres == 0 ? kSpecNoSpheres : 0) |
                         (s->n_planes == 5 ? kSpecFivePlanes : 0) | (s->n_meshes == 1 ? kSpecOneMesh : 0) |
-                        (s->n_meshes == 0 ? kSpecNoMesh : 0) | (room ? kSpecRoomPlanes : 0);
+                        (s->n_meshes == 0 ? kSpecNoMesh : 0) | (room ? kSpecRoomPlanes : 0) |
+                        (cull_back ? kSpecCullBack : 0);
     }
     c->split_ok = split_ok && !parts.empty() && !c->deep_stack;
     c->has_scene = true;

@@ -53,17 +53,18 @@ constexpr int kSpecNoMesh = 512;       // no triangle mesh
 // (p0_A - o_A) / d_A whenever the plane can be hit (rtx_hip.hip, room_a).
 constexpr int kSpecRoomPlanes = 1024;
 constexpr int kRoomAxes[5] = {2, 1, 1, 0, 0};
+constexpr int kSpecCullBack = 2048;    // every mesh culls back faces (the cull sign is known)
 // The compiled variants, most specific first (the launch takes the first one whose facts hold):
-//   0  Lambert only, one mesh, no spheres (W4_Bunny, Synthetic100k, Bunny + 8 lights)
-//   1  Lambert + Cook-Torrance, one mesh, no spheres (W4_Optional)
+//   0  Lambert only, one back-face-culled mesh, no spheres (W4_Bunny, Synthetic100k, Bunny + 8 lights)
+//   1  Lambert + Cook-Torrance, one back-face-culled mesh, no spheres (W4_Optional)
 //   2  Lambert + Cook-Torrance, spheres, no mesh (W3)
 //   3  Lambert + Cook-Torrance, spheres and meshes (W4_Reference)
 //   4  as 3 for five planes of any other arrangement
 // all with point lights, 5 planes, Combined lighting + shadows; 0-3 in the room.
 constexpr int kSpecCommon = kSpecPoint | kSpecCombShadows | kSpecFivePlanes;
 constexpr int kSpecVariants[] = {
-    kSpecCommon | kSpecRoomPlanes | kSpecKindLambert | kSpecNoSpheres | kSpecOneMesh,
-    kSpecCommon | kSpecRoomPlanes | kSpecKindLambert | kSpecKindCT | kSpecNoSpheres | kSpecOneMesh,
+    kSpecCommon | kSpecRoomPlanes | kSpecCullBack | kSpecKindLambert | kSpecNoSpheres | kSpecOneMesh,
+    kSpecCommon | kSpecRoomPlanes | kSpecCullBack | kSpecKindLambert | kSpecKindCT | kSpecNoSpheres | kSpecOneMesh,
     kSpecCommon | kSpecRoomPlanes | kSpecKindLambert | kSpecKindCT | kSpecNoMesh,
     kSpecCommon | kSpecRoomPlanes | kSpecKindLambert | kSpecKindCT,
     kSpecCommon | kSpecKindLambert | kSpecKindCT,
