@@ -934,13 +934,16 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
     // inside theirs too, t = RN(a / d) costs 3 VALU instead of the 11 of IEEE `/`.
     const bool room_p = kRoom && !RTX_ABL_PPLANE && (active & ~ballot(finite3(vr.ox, vr.oy, vr.oz))) == 0;
     if (room_p) {
-        const bool mk = fast && V.room_fast;
+        // the view's record through a readfirstlane'd index: scalar loads (the view index
+        // itself stays a VGPR value; making it uniform everywhere measured slower)
+        const ViewCam& VU = F.cam[uni(view)];
+        const bool mk = fast && VU.room_fast;
         for_room_planes([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             constexpr int A = kRoomAxes[k];
             float t;
             if (mk) {
-                t = div_rn(V.room_a[k], room_d<A>(vr), room_inv<A>(vr));
+                t = div_rn(VU.room_a[k], room_d<A>(vr), room_inv<A>(vr));
             } else {
                 float4 p0, p1;
                 ldcb32(S.planes, k * 32u, p0, p1);
