@@ -5,6 +5,7 @@ in.  It performs the same operations, so its frames must equal the generic kerne
 bit (RTX_NO_SPEC=1 context) — checked on every scene and on animated states, including the
 frames after the first (cost-ordered dispatch) — and the reference's (the oracle)."""
 import os
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -84,3 +85,38 @@ def test_room_planes_edge_origins_equal_generic(gpu_ctx, generic_ctx, origin):
     if all(np.isfinite(origin)) and max(abs(x) for x in origin) < 1e3:
         rpx, rrgb = oracle_bind.render(s, cam, p)
         assert np.array_equal(apx, rpx) and np.array_equal(argb.view(np.uint32), rrgb.view(np.uint32))
+
+
+# Five planes that are NOT the room fact (kSpecRoomPlanes): a normal of length 2, an origin beyond
+# 2^64, and the room's planes in another order.  The launch then takes the variant without the
+# fact (kSpecVariants[4]); frames still equal the generic kernel's and the oracle's.
+_BUNNY_FILE = Path(__file__).resolve().parents[1] / "scenes" / "w4_bunny.rtxscene"
+_NOT_ROOM = {
+    "scaled_normal": ("plane 0 0 0    0 1 0   1", "plane 0 0 0    0 2 0   1"),
+    "far_origin": ("plane 0 0 10   0 0 -1  1", "plane 3e20 0 10   0 0 -1  1"),
+    "reordered": ("plane 0 0 10   0 0 -1  1\n", ""),
+}
+
+
+@pytest.mark.parametrize("case", sorted(_NOT_ROOM))
+def test_not_room_planes_equal_generic_and_oracle(gpu_ctx, generic_ctx, tmp_path, case):
+    text = _BUNNY_FILE.read_text()
+    old, new = _NOT_ROOM[case]
+    assert old in text
+    text = text.replace(old, new)
+    if case == "reordered":
+        text += "plane 0 0 10   0 0 -1  1\n"
+    f = tmp_path / "scene.rtxscene"
+    f.write_text(text)
+    hs = HostScene("file:" + str(f))
+    s, cam = hs.view()
+    assert s.n_planes == 5
+    p = abi.make_params(320, 180)
+    gpu_ctx.upload(s)
+    generic_ctx.upload(s)
+    for _ in range(2):
+        apx, argb = gpu_ctx.render(cam, p)
+        bpx, brgb = generic_ctx.render(cam, p)
+        assert np.array_equal(apx, bpx) and np.array_equal(argb.view(np.uint32), brgb.view(np.uint32))
+    rpx, rrgb = oracle_bind.render(s, cam, p)
+    assert np.array_equal(apx, rpx) and np.array_equal(argb.view(np.uint32), rrgb.view(np.uint32))
