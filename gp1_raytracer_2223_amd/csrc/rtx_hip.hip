@@ -648,30 +648,36 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
 // result is the minimum of the parts' (t, triangle index) keys — left-then-right DFS
 // order is increasing triangle index (checked at upload), which makes the key minimum
 // the reference's first-found, strict-< winner — and occlusion is the OR of the parts.
-template <bool ANY, bool FAST>
-__device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, unsigned long long mask, uint32_t lane,
-                              uint4* stk, float& sc_t, uint32_t& sc_tri, unsigned long long& live, Counts& cnt,
-                              const uint32_t* occ_word = nullptr, uint32_t occ_bit = 0) {
+// SLAB = kSlabOct: `oct` is the batch's octant (batch_octant) and the part walks that copy.
+// CB: kSpecCullBack (tri_t_wave).
+template <bool ANY, int SLAB, bool CB = false>
+__device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int oct, unsigned long long mask,
+                              uint32_t lane, uint4* stk, float& sc_t, uint32_t& sc_tri, unsigned long long& live,
+                              Counts& cnt, const uint32_t* occ_word = nullptr, uint32_t occ_bit = 0) {
+    constexpr bool FAST = SLAB != kSlabExact;
     if (E.x < 0) return;   // unused entry of a device-animated mesh's reserved frontier
     const int4 M = ldcb16i(S.meshes, static_cast<uint32_t>(E.x) * 16u);
+    const float4* nb = SLAB == kSlabOct ? reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.nodes) +
+                                                                          static_cast<uint32_t>(oct) * S.oct_bytes)
+                                        : S.nodes;
     float4 b0, b1;
-    ldcb32(S.nodes, static_cast<uint32_t>(M.x), b0, b1);   // M.x: the root's byte offset
-    unsigned long long m = slab_mask<FAST ? kSlabFast : kSlabExact>(b0, b1, r) & mask;
+    ldcb32(nb, static_cast<uint32_t>(M.x), b0, b1);   // M.x: the root's byte offset
+    unsigned long long m = slab_mask<SLAB>(b0, b1, r) & mask;
     uint32_t link = __float_as_uint(b1.z), ntri = __float_as_uint(b1.w);
     const uint32_t path = static_cast<uint32_t>(E.z);
     for (int d = 0; d < E.w && m; ++d) {
         NodePair P;
-        ldcb64(S.nodes, link, P.l0, P.l1, P.r0, P.r1);
+        ldcb64(nb, link, P.l0, P.l1, P.r0, P.r1);
         const bool right = (path >> d) & 1u;
         const float4 c0 = right ? P.r0 : P.l0, c1 = right ? P.r1 : P.l1;
-        m &= slab_mask<FAST ? kSlabFast : kSlabExact>(c0, c1, r);
+        m &= slab_mask<SLAB>(c0, c1, r);
         link = __float_as_uint(c1.z);
         ntri = __float_as_uint(c1.w);
     }
     if (m == 0) return;
     if (RTX_LEAN_WALK && !RTX_STAMPS)
-        bvh_walk_lean<ANY, FAST ? kSlabFast : kSlabExact>(S, S.nodes, cull_sign(M.z, ANY), r, link, ntri, m, mask,
-                                                          lane, stk, sc_t, sc_tri, live, occ_word, occ_bit);
+        bvh_walk_lean<ANY, SLAB, CB>(S, nb, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, sc_t, sc_tri,
+                                     live, occ_word, occ_bit);
     else
         bvh_walk<ANY, FAST, false>(S, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, nullptr, sc_t, sc_tri,
                                    live, cnt, occ_word, occ_bit);
@@ -995,10 +1001,13 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
         const float sc0 = sc_t;
         uint32_t sc_tri = 0;
         unsigned long long unused = 0;
-        if (fast)
-            part_traverse<false, true>(S, E, vr, active, lane, stk, sc_t, sc_tri, unused, cnt);
+        const int oct = (RTX_OCTANT && fast && S.oct_bytes) ? batch_octant(vr, active) : -1;
+        if (oct >= 0)
+            part_traverse<false, kSlabOct, kCullBack>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri, unused, cnt);
+        else if (fast)
+            part_traverse<false, kSlabFast, kCullBack>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused, cnt);
         else
-            part_traverse<false, false>(S, E, vr, active, lane, stk, sc_t, sc_tri, unused, cnt);
+            part_traverse<false, kSlabExact, kCullBack>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused, cnt);
         if (valid && sc_t < sc0)   // accepted t >= tmin > 0: the float bits order like the values
             atomicMin(&F.hit_key[slot], (static_cast<unsigned long long>(__float_as_uint(sc_t)) << 32) | sc_tri);
         RTX_SPLIT_STAMP();
@@ -1142,12 +1151,16 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
                     const int4 E = ldc(S.parts, part);
                     float st = 0.f;
                     uint32_t stri = 0;
-                    if (sfast)
-                        part_traverse<true, true>(S, E, sr, live, lane, stk, st, stri, live, cnt, &F.occ_bits[slot],
-                                                  1u << li);
+                    const int poct2 = (RTX_OCTANT && sfast && S.oct_bytes) ? batch_octant(sr, hitmask) : -1;
+                    if (poct2 >= 0)
+                        part_traverse<true, kSlabOct, kCullBack>(S, E, sr, poct2, live, lane, stk, st, stri, live, cnt,
+                                                                 &F.occ_bits[slot], 1u << li);
+                    else if (sfast)
+                        part_traverse<true, kSlabFast, kCullBack>(S, E, sr, 0, live, lane, stk, st, stri, live, cnt,
+                                                                  &F.occ_bits[slot], 1u << li);
                     else
-                        part_traverse<true, false>(S, E, sr, live, lane, stk, st, stri, live, cnt, &F.occ_bits[slot],
-                                                   1u << li);
+                        part_traverse<true, kSlabExact, kCullBack>(S, E, sr, 0, live, lane, stk, st, stri, live, cnt,
+                                                                   &F.occ_bits[slot], 1u << li);
                     if (did && !((live >> lane) & 1ull)) atomicOr(&F.occ_bits[slot], 1u << li);
                     continue;
                 }
@@ -2186,6 +2199,18 @@ int spec_variant(int facts) {
     return -1;
 }
 
+// The split launches of a frame (PHASE 1-3) in the frame's specialised variant v (-1: generic).
+template <int P>
+void launch_phase(int v, dim3 g, hipStream_t s, const DevScene& d, const FrameArgs& F) {
+    switch (v) {
+    case 0: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[0]>), g, dim3(kBlockThreads), 0, s, d, F); break;
+    case 1: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[1]>), g, dim3(kBlockThreads), 0, s, d, F); break;
+    case 3: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[3]>), g, dim3(kBlockThreads), 0, s, d, F); break;
+    case 4: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[4]>), g, dim3(kBlockThreads), 0, s, d, F); break;
+    default: hipLaunchKernelGGL((rtx_render_kernel<false, P>), g, dim3(kBlockThreads), 0, s, d, F); break;   // (2: no mesh, never split)
+    }
+}
+
 int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
     if (grid.x == 0 || grid.y == 0) return RTX_OK;
     if (count) {
@@ -2200,6 +2225,10 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         HIP_TRY(c, hipGetLastError());
         return RTX_OK;
     }
+    // the first specialised variant whose facts the scene and frame satisfy (kSpecVariants;
+    // RTX_NO_SPEC=1 forces the generic kernel); the split launches take it too
+    const int facts = c->scene_spec | ((F.mode == RTX_MODE_COMBINED && F.shadows) ? kSpecCombShadows : 0);
+    const int v = (c->no_spec || c->deep_stack) ? -1 : spec_variant(facts);
     if (F.heavy_flag) {
         // The heavy tiles, one BVH frontier part per workgroup (see the kernel), on a
         // high-priority stream forked from the frame stream: they share no pixels with the
@@ -2208,21 +2237,16 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         hipStream_t s2 = c->split_stream;
         HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
-        hipLaunchKernelGGL((rtx_render_kernel<false, 1>), dim3(nh, np, 1), dim3(kBlockThreads), 0, s2, c->dev, F);
+        launch_phase<1>(v, dim3(nh, np, 1), s2, c->dev, F);
         HIP_TRY(c, hipGetLastError());
         if (F.shadows && c->dev.n_lights) {
-            hipLaunchKernelGGL((rtx_render_kernel<false, 2>), dim3(nh, np, c->dev.n_lights), dim3(kBlockThreads), 0,
-                               s2, c->dev, F);
+            launch_phase<2>(v, dim3(nh, np, c->dev.n_lights), s2, c->dev, F);
             HIP_TRY(c, hipGetLastError());
         }
-        hipLaunchKernelGGL((rtx_render_kernel<false, 3>), dim3(nh, 1, 1), dim3(kBlockThreads), 0, s2, c->dev, F);
+        launch_phase<3>(v, dim3(nh, 1, 1), s2, c->dev, F);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(c->ev_join, s2));
     }
-    // the first specialised variant whose facts the scene and frame satisfy (kSpecVariants;
-    // RTX_NO_SPEC=1 forces the generic kernel)
-    const int facts = c->scene_spec | ((F.mode == RTX_MODE_COMBINED && F.shadows) ? kSpecCombShadows : 0);
-    const int v = c->no_spec ? -1 : spec_variant(facts);
     if (c->deep_stack)
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
     else if (v == 0)
