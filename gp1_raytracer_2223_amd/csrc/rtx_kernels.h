@@ -118,7 +118,10 @@ struct DevScene {
     uint32_t oct_bytes;
 };
 
-constexpr size_t kOctantMaxNodeBytes = size_t(1) << 20;   // octant node copies only below this (per copy)
+#ifndef RTX_OCT_MAX_BYTES
+#define RTX_OCT_MAX_BYTES (size_t(1) << 20)
+#endif
+constexpr size_t kOctantMaxNodeBytes = RTX_OCT_MAX_BYTES;   // octant node copies only below this (per copy)
 constexpr size_t kOctantDeviceMinBytes = size_t(64) << 10;   // from this size copies 1..7 are written on the device
 constexpr int kMaxViews = 8;   // views (camera positions) rendered by one launch
 
