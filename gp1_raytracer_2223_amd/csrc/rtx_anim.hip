@@ -383,9 +383,13 @@ __device__ __forceinline__ void team_copy(const Team<G>& tm, const uint32_t* src
 }
 
 // Node classes by size: huge nodes are processed by the whole workgroup one at a time, large
-// ones by a wave, small ones by a 16-lane row, tiny ones by one lane each (every class folds
-// at most 8 positions per lane, except the huge ones' eighths).
-constexpr uint32_t kHugeNode = 512, kLargeNode = 64, kTinyNode = 8;
+// ones by a wave, small ones by a 16-lane row, tiny ones by one lane each (a large node of up
+// to 2,048 triangles folds up to 32 positions per lane: waves working on different nodes side
+// by side beat the serial whole-workgroup path there).
+#ifndef RTX_ANIM_HUGE
+#define RTX_ANIM_HUGE 2048   // above this a node takes the whole workgroup (512 measured 15 % slower)
+#endif
+constexpr uint32_t kHugeNode = RTX_ANIM_HUGE, kLargeNode = 64, kTinyNode = 8;
 __device__ __forceinline__ uint32_t node_class(uint32_t n) {
     return n > kHugeNode ? 0u : (n > kLargeNode ? 1u : (n > kTinyNode ? 2u : 3u));
 }
