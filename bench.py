@@ -7,37 +7,46 @@ state, Combined lighting, shadows on).
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-A step renders N views of the scene (`--mode views`, the default): view f is the reference
-camera moved 0.05 f along x, and every view's rows are cut into 16-row stripes dealt round
-robin over the N ranks (rank r owns view f's stripe s iff s % N == (r - f) mod N; SURVEY
-§8(e)), so every image is tiled across all the GPUs and every rank renders one frame's
-worth of pixels per step — weak scaling, the sharding rule for a path of independent
-pixels.  At N = 1 a step is exactly one reference Renderer::Render frame.  `--mode frame`
-tiles ONE frame per step over the N ranks (strong scaling: each rank renders 1/N of a
-frame, so at 8 GPUs a 1080p frame no longer fills a GPU).
+The JSON line has four parts:
 
-Two timed regions, each bracketed by barrier + stream sync and max-reduced over ranks:
-  1. `value`: K steps with inputs resident in HBM and the frames left in HBM (the
-     metric's device throughput);
-  2. `host_gather`: K steps whose frames are ALSO gathered into page-locked host frames
-     shared by all ranks (/dev/shm mapping, hipHostRegister; every rank hipMemcpy2DAsync's
-     only its own stripes over its own PCIe link) — the north star's "independent tiles
-     gathered on host".  PCIe-inclusive, so never `value`.
-No collective on the data path: the ranks' only exchange is a gloo barrier and the
-max-reduce of the timings.
+1. The headline (`value`), `--mode views` by default.  A step renders N views of the scene:
+   view f is the reference camera moved 0.05 f along x.  Every view's rows are cut into 16-row
+   stripes dealt round robin over the N ranks (rank r owns view f's stripe s iff
+   s % N == (r - f) mod N).  So every image is tiled across all the GPUs and
+   every rank renders one frame's worth of pixels per step: weak scaling.  At N = 1 a step is
+   exactly one reference Renderer::Render frame.  `--mode frame` tiles ONE frame per step over
+   the N ranks (strong scaling).
+2. `multi_gpu_configs`, at every N (N = 1 anchors the curve): the north star's multi-GPU
+   workloads, Synthetic100k 1920x1080 and Bunny + 8 lights 3840x2160, each as ONE image per
+   step tiled in 16-row stripes over the N ranks (the reference's one-frame parallel_for,
+   Renderer.cpp:79-85) — Mpix/s device-resident and gathered into the page-locked host frame,
+   each rank's HBM traffic from the PMC record of this build, and the gathered frame's parity.
+3. `parity_configs` (N = 1): every BASELINE config, plus W4_Reference and W4_Optional, rendered
+   at full size on a fresh context (4 frames, so the cost-ordered and split state is live)
+   against the reference's own frame (tests/golden/config_*.npz).
+4. `cpu_baseline`: the reference's CPU Renderer timed on this host (rank 0, N = 1).
 
-Frames in flight (--inflight, default 2): consecutive steps go round robin to that many
-render contexts on the rank's GPU (each its own stream, frame buffer and tile schedule),
-so frame k+1 starts while frame k's last waves drain.  `roofline.kernel_ms` is the
-serialized launch time of ONE context (HIP events on its stream, mean of 1000 launches), the
-figure a rocprofv3 kernel trace of `--inflight 1` shows.  It is measured first, before the W
-warm-up steps: those 1000 launches (~60 ms) also take the GPU from its idle clock to its
-steady rendering clock, which a short run's few warm-up steps do not.
+Timed regions are bracketed by barrier + stream sync and max-reduced over ranks:
+  `value`: K steps with inputs resident in HBM and the frames left in HBM;
+  `host_gather`: K steps whose frames are ALSO gathered into page-locked host frames shared by
+     all ranks (/dev/shm mapping, hipHostRegister; every rank hipMemcpy2DAsync's only its own
+     stripes over its own PCIe link) — the north star's "independent tiles gathered on host".
+     PCIe-inclusive, so never `value`.
+No data moves between ranks.  The control plane (barrier, max / sum of a few numbers) is a
+shared-memory block on the node (ShmCtl), so the bench process loads only the ROCm runtime
+librtx_hip links against, never torch's bundled copy.
 
-After timing, the gathered frame is checked against the reference: `parity` carries the
-SHA-256 comparison with tests/golden/config_<scene>_<W>x<H>.npz (the frame the reference
-built in place produced), the max-abs of the float colour on the golden's 4096 samples,
-and the frame's FNV beside `cpu_baseline.fnv` (the reference timed in this same run).
+Frames in flight (--inflight, default 2): consecutive steps go round robin to that many render
+contexts on the rank's GPU (each its own stream, frame buffer and tile schedule), so frame k+1
+starts while frame k's last waves drain.  `roofline.kernel_ms` is the serialized launch time of
+ONE context (HIP events on its stream, mean of 1000 launches), the figure a rocprofv3 kernel
+trace of `--inflight 1` shows.  It is measured first, before the W warm-up steps: those 1000
+launches (~60 ms) also take the GPU from its idle clock to its steady rendering clock, which a
+short run's few warm-up steps do not.
+
+`roofline.traffic` is the HBM bytes per launch from the PMC record (tools/pmc_configs.sh ->
+profiles/r*/pmc_configs.json) of THIS build: records carry the SHA-256 of the librtx_hip.so
+they were measured with, and a record of another build is never used (traffic null).
 """
 from __future__ import annotations
 
@@ -45,6 +54,7 @@ import argparse
 import ctypes as C
 import hashlib
 import json
+import mmap
 import os
 import struct
 import subprocess
@@ -69,10 +79,21 @@ from gp1_raytracer_2223_amd.scene import HostScene  # noqa: E402
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md, spec)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (spec)
 GOLDEN = ROOT / "tests" / "golden"
+LIB_HIP = ROOT / "gp1_raytracer_2223_amd" / "lib" / "librtx_hip.so"
 # ref_harness's FNV-1a (oracle/ref/ref_harness.cpp `bench`) starts from the decimal basis
 # 1469598103934665603; SURVEY §8(c)'s recorded hashes use the same one.
 FNV_BASIS = 1469598103934665603
 COST = [41, 19, 14, 12, 63, 9, 15, 1, 26, 6, 31, 103]   # SURVEY §8(d) FLOP per counted unit
+K_KERNEL_LAUNCHES = 1000   # launches averaged for the headline's roofline.kernel_ms
+
+# BASELINE.json's multi-GPU workloads: one image per step, tiled over the ranks (steps per run)
+MULTI_GPU_CONFIGS = [("Synthetic100k", 1920, 1080, 100), ("Bunny8Lights", 3840, 2160, 300)]
+# parity_configs: (scene, W, H, bit-exact required).  Cook-Torrance / Phong use powf, where the
+# device libm may differ from glibc by an ulp: those are held to the north star's tolerance.
+PARITY_CONFIGS = [("W1", 640, 480, True), ("W3", 1280, 720, False), ("W4_Bunny", 1920, 1080, True),
+                  ("Synthetic100k", 1920, 1080, True), ("Bunny8Lights", 3840, 2160, True),
+                  ("W4_Reference", 1920, 1080, False), ("W4_Optional", 1920, 1080, False)]
+PARITY_FRAMES = 4
 
 
 def make_views(cam: abi.Camera, n: int) -> "C.Array":
@@ -91,52 +112,128 @@ def fnv1a(px: np.ndarray) -> str:
     return f"{h:016x}"
 
 
+def sha256(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def lib_sha256() -> str:
+    return hashlib.sha256(LIB_HIP.read_bytes()).hexdigest()
+
+
+# ---------------------------------------------------------------------------- control plane
+class ShmCtl:
+    """Barrier and small reductions over the ranks of ONE node through a /dev/shm block.
+
+    Rank r owns one sequence word and two 16-value slots; it writes only those (aligned 8-byte
+    stores, which x86 never tears or reorders against each other).  barrier(): bump the own
+    sequence word to k and wait until every rank's is >= k.  Reductions write the values into
+    slot k % 2 before the barrier and read every rank's slot after it; a rank cannot come back
+    to that slot before every rank has passed the next barrier, i.e. finished reading.  The
+    block is created by rank 0 under a temporary name and renamed into place (atomic), and
+    unlinked once every rank has mapped it."""
+
+    SLOT = 16
+
+    def __init__(self, world: int, rank: int, tag: str):
+        self.world, self.rank = world, rank
+        self.k = 0
+        words = world * (1 + 2 * self.SLOT)
+        nbytes = 8 * words
+        path = os.path.join(SharedFrame._dirs()[0] if os.path.isdir("/dev/shm") else tempfile.gettempdir(),
+                            f"rtx_ctl_{tag}")
+        if rank == 0:
+            tmp = f"{path}.{os.getpid()}"
+            fd = os.open(tmp, os.O_RDWR | os.O_CREAT | os.O_EXCL, 0o600)
+            os.ftruncate(fd, nbytes)
+            os.rename(tmp, path)
+        else:
+            t0 = time.monotonic()
+            while True:
+                try:
+                    fd = os.open(path, os.O_RDWR)
+                    if os.fstat(fd).st_size >= nbytes:
+                        break
+                    os.close(fd)
+                except FileNotFoundError:
+                    pass
+                if time.monotonic() - t0 > 300:
+                    raise TimeoutError(f"rank {rank}: control block {path} never appeared")
+                time.sleep(0.005)
+        try:
+            self.mm = mmap.mmap(fd, nbytes, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        finally:
+            os.close(fd)
+        a = np.frombuffer(self.mm, dtype=np.int64)
+        self.seq = a[:world]
+        self.vals = np.frombuffer(self.mm, dtype=np.float64, offset=8 * world).reshape(2, world, self.SLOT)
+        self.path = path
+        self.barrier()
+        if rank == 0:
+            try:
+                os.unlink(path)   # every rank has it mapped
+            except FileNotFoundError:
+                pass
+
+    def barrier(self) -> None:
+        self.k += 1
+        self.seq[self.rank] = self.k
+        t0 = time.monotonic()
+        while int(self.seq.min()) < self.k:
+            if time.monotonic() - t0 > 600:
+                raise TimeoutError(f"rank {self.rank}: barrier {self.k} timed out ({self.seq.tolist()})")
+            time.sleep(0)
+
+    def allreduce(self, xs: list[float]) -> np.ndarray:
+        assert len(xs) <= self.SLOT
+        slot = self.vals[(self.k + 1) % 2]
+        slot[self.rank, :len(xs)] = xs
+        self.barrier()
+        return slot[:, :len(xs)].copy()
+
+    def close(self) -> None:
+        self.seq = self.vals = None
+        try:
+            self.mm.close()
+        except BufferError:
+            pass
+
+
 class Dist:
+    """Rank / world from the torch.distributed.run environment; the control plane is ShmCtl
+    (one node, no torch in this process)."""
+
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.ctl = None
         if self.world > 1:
-            import torch.distributed as dist   # control plane only (gloo): no data-path collective
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            # gloo prints its connection log on stdout; keep stdout for the one JSON line
-            sys.stdout.flush()
-            saved = os.dup(1)
-            os.dup2(2, 1)
-            try:
-                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
-                dist.barrier()
-            finally:
-                sys.stdout.flush()
-                os.dup2(saved, 1)
-                os.close(saved)
-            self.dist = dist
+            # every rank of one torchrun launch has the same parent (the elastic agent)
+            tag = f"{os.environ.get('MASTER_PORT', 'solo')}_{os.getuid()}_{os.getppid()}"
+            self.ctl = ShmCtl(self.world, self.rank, tag)
 
     def barrier(self):
-        if self.world > 1:
-            self.dist.barrier()
+        if self.ctl:
+            self.ctl.barrier()
 
     def max(self, x: float) -> float:
-        if self.world == 1:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
+        return x if not self.ctl else float(self.ctl.allreduce([x]).max())
 
     def sum_i64(self, xs: list[int]) -> list[int]:
-        if self.world == 1:
+        if not self.ctl:
             return xs
-        import torch
-        t = torch.tensor(xs, dtype=torch.int64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return [int(v) for v in t.tolist()]
+        # exact: float64 holds integers below 2^53 (FLOP per frame ~1e10)
+        return [int(v) for v in self.ctl.allreduce([float(x) for x in xs]).sum(axis=0)]
+
+    def gather(self, xs: list[float]) -> np.ndarray:
+        return np.array([xs], np.float64) if not self.ctl else self.ctl.allreduce(xs)
 
     def close(self):
-        if self.world > 1:
-            self.dist.destroy_process_group()
+        if self.ctl:
+            self.ctl.close()
 
 
+# ---------------------------------------------------------------------------- CPU reference
 def write_obj_from_asset(asset: Path, out_obj: Path) -> None:
     """Re-emit an .rtxmesh as OBJ text (exact float round trip, 1-based faces) so the
     reference harness can load it where /root/reference does not exist."""
@@ -168,65 +265,68 @@ def cgroup_cpu_quota() -> float | None:
         return None
 
 
-def cpu_baseline(scene: str, width: int, height: int, frames: int) -> dict | None:
-    """The reference CPU Renderer timed on this host (rank 0, N = 1 only): the
-    reference's own sources built in place by oracle/ref (kind "reference"), or the C
-    restatement in oracle/ when that build is absent (kind "port").
+class CpuReference:
+    """The reference CPU Renderer timed on this host: the reference's own sources built in
+    place by oracle/ref (kind "reference"), or the C restatement in oracle/ when that build
+    is absent (kind "port").  Test infrastructure, run only outside the timed regions."""
 
-    Threads = every CPU this process may run on (len(sched_getaffinity)), which is what
-    the reference's PPL parallel_for uses (std::thread::hardware_concurrency, Renderer.cpp:
-    79-85).  Where a cgroup CPU quota caps the process below that (the GPU box: 16 CPUs of
-    256), the quota-sized run and a single-thread run are recorded too, and
-    `full_host_upper_bound` = single-thread rate x hardware threads (perfect linear
-    scaling over every hardware thread, SMT included) bounds what the whole host could do."""
-    nthreads = len(os.sched_getaffinity(0))
-    quota = cgroup_cpu_quota()
-    harness = ROOT / "oracle" / "_ref" / "ref_harness"
-    runs = {}
-    if harness.exists():
-        with tempfile.TemporaryDirectory() as td:
-            res = Path(td) / "Resources"
+    def __init__(self):
+        self.harness = ROOT / "oracle" / "_ref" / "ref_harness"
+        self.kind = "reference" if self.harness.exists() else "port"
+        self.td = None
+        if self.kind == "reference":
+            self.td = tempfile.TemporaryDirectory()
+            res = Path(self.td.name) / "Resources"
             res.mkdir()
             for stem in ("lowpoly_bunny2", "Assignment3D1"):
                 write_obj_from_asset(abi.ASSET_DIR / f"{stem}.rtxmesh", res / f"{stem}.obj")
+            self.how = "reference sources built in place with g++ -O2 -ffp-contract=off (oracle/ref), 1024-pixel dynamic chunks"
+        else:
+            self.how = "C restatement oracle/rtx_oracle.c"
 
-            def run(threads, nframes):
-                out = subprocess.run([str(harness), "bench", scene, "-1", str(width), str(height), str(threads),
-                                      str(nframes)], cwd=td, check=True, capture_output=True, text=True, timeout=900)
-                return json.loads(out.stdout.strip().splitlines()[-1])
-            runs["all"] = run(nthreads, frames)
-            if quota is not None and int(quota) < nthreads:
-                runs["quota"] = run(max(1, int(quota)), frames)
-            runs["one"] = run(1, 1)
-        kind = "reference"
-        how = "reference sources built in place with g++ -O2 -ffp-contract=off (oracle/ref), 1024-pixel dynamic chunks"
-    else:
+    def run(self, scene: str, width: int, height: int, threads: int, frames: int) -> dict:
+        if self.kind == "reference":
+            out = subprocess.run([str(self.harness), "bench", scene, "-1", str(width), str(height), str(threads),
+                                  str(frames)], cwd=self.td.name, check=True, capture_output=True, text=True,
+                                 timeout=900)
+            return json.loads(out.stdout.strip().splitlines()[-1])
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_bind   # test infrastructure: the checker, timed here as the CPU baseline
         hs = HostScene(scene)
         s, cam = hs.view()
         p = abi.make_params(width, height)
-
-        def run(threads, nframes):
+        oracle_bind.render(s, cam, p, threads=threads, want_rgb=False)
+        ts = []
+        for _ in range(frames):
+            t0 = time.perf_counter()
             oracle_bind.render(s, cam, p, threads=threads, want_rgb=False)
-            ts = []
-            for _ in range(nframes):
-                t0 = time.perf_counter()
-                oracle_bind.render(s, cam, p, threads=threads, want_rgb=False)
-                ts.append(time.perf_counter() - t0)
-            med = float(np.median(ts))
-            return {"median_s": med, "mpix_s": width * height / med / 1e6, "fnv": None}
-        runs["all"] = run(nthreads, frames)
-        if quota is not None and int(quota) < nthreads:
-            runs["quota"] = run(max(1, int(quota)), frames)
-        runs["one"] = run(1, 1)
-        kind = "port"
-        how = "C restatement oracle/rtx_oracle.c"
+            ts.append(time.perf_counter() - t0)
+        med = float(np.median(ts))
+        return {"median_s": med, "mpix_s": width * height / med / 1e6, "fnv": None}
+
+    def close(self):
+        if self.td:
+            self.td.cleanup()
+
+
+def cpu_baseline(ref: CpuReference, scene: str, width: int, height: int, frames: int) -> dict:
+    """Threads = every CPU this process may run on (len(sched_getaffinity)), which is what the
+    reference's PPL parallel_for uses (std::thread::hardware_concurrency, Renderer.cpp:79-85).
+    Where a cgroup CPU quota caps the process below that (the GPU box: 16 CPUs of 256), the
+    quota-sized run and a single-thread run are recorded too, and `full_host_upper_bound` =
+    single-thread rate x hardware threads (perfect linear scaling over every hardware thread,
+    SMT included) bounds what the whole host could do."""
+    nthreads = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    runs = {"all": ref.run(scene, width, height, nthreads, frames)}
+    if quota is not None and int(quota) < nthreads:
+        runs["quota"] = ref.run(scene, width, height, max(1, int(quota)), frames)
+    runs["one"] = ref.run(scene, width, height, 1, 1)
     r = runs["all"]
     one = runs["one"]["mpix_s"]
-    out = {"value": round(r["mpix_s"], 4), "unit": "Mpixels/s", "cores": nthreads, "kind": kind,
+    out = {"value": round(r["mpix_s"], 4), "unit": "Mpixels/s", "cores": nthreads, "kind": ref.kind,
            "sample": f"{frames} frames of {scene} {width}x{height}, median of Renderer::Render, {nthreads} threads "
-                     f"(= sched_getaffinity, the reference's hardware_concurrency), {how}",
+                     f"(= sched_getaffinity, the reference's hardware_concurrency), {ref.how}",
            "median_s": r["median_s"], "fnv": r.get("fnv"),
            "single_thread_mpix_s": round(one, 4),
            "full_host_upper_bound_mpix_s": round(one * nthreads, 2),
@@ -239,18 +339,23 @@ def cpu_baseline(scene: str, width: int, height: int, frames: int) -> dict | Non
     return out
 
 
-def pmc_traffic(scene: str, width: int, height: int, views: int) -> tuple[int | None, str | None]:
-    """HBM bytes per launch of the render kernel from the newest committed rocprofv3 PMC
-    summary of this same configuration (tools/profile.sh -> profiles/r*/pmc_summary.json:
-    2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md).  A benchmark
-    process cannot read its own PMC counters, so this is the profiled value, not a live one."""
-    for f in sorted(ROOT.glob("profiles/r*/pmc_summary.json"), reverse=True):
+# ---------------------------------------------------------------------------- records
+def pmc_traffic(scene: str, width: int, height: int, views: int, stripe_step: int,
+                lib_hash: str) -> tuple[dict | None, str | None]:
+    """The PMC record of this configuration measured with THIS librtx_hip.so (its SHA-256),
+    from the newest profiles/r*/pmc_configs.json: HBM bytes per launch of the main render
+    kernel and per frame (every render launch of the frame), 2 x FETCH_SIZE + WRITE_SIZE per
+    the gfx950 correction of MI355X_MICROARCH.md.  A benchmark process cannot read its own
+    counters; a record of any other build is ignored (traffic null)."""
+    want = {"scene": scene, "width": width, "height": height, "views": views, "stripe_step": stripe_step}
+    for f in sorted(ROOT.glob("profiles/r*/pmc_configs.json"), reverse=True):
         try:
-            d = json.loads(f.read_text())
+            recs = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
-        if d.get("config") == {"scene": scene, "width": width, "height": height, "views": views}:
-            return int(d["hbm_bytes_per_launch"]), str(f.relative_to(ROOT))
+        for r in recs.get("records", []):
+            if r.get("config") == want and r.get("lib_sha256") == lib_hash:
+                return r, str(f.relative_to(ROOT))
     return None, None
 
 
@@ -259,32 +364,194 @@ def golden_for(scene: str, width: int, height: int):
     return (np.load(f), f) if f.exists() else (None, None)
 
 
-def parity_report(px: np.ndarray, rgb: np.ndarray, scene: str, width: int, height: int, cpu: dict | None) -> dict:
-    """Self-check of the benchmarked frame against the reference's own frame."""
+def _channels(p):
+    return np.stack([(p >> 16) & 255, (p >> 8) & 255, p & 255], -1).astype(np.int32)
+
+
+def parity_report(px: np.ndarray, rgb: np.ndarray, scene: str, width: int, height: int, cpu_fnv: str | None = None,
+                  exact: bool = True, with_fnv: bool = True) -> dict:
+    """Self-check of a rendered frame against the reference's own frame (golden)."""
     g, f = golden_for(scene, width, height)
-    out = {"frame": "the host-gathered frame of the timed contexts (cost-ordered / split state)",
-           "gpu_fnv": fnv1a(px)}
-    if cpu and cpu.get("fnv"):
-        out["cpu_fnv"] = cpu["fnv"]
-        out["fnv_match"] = out["gpu_fnv"] == cpu["fnv"]
+    out = {}
+    if with_fnv:
+        out["gpu_fnv"] = fnv1a(px)
+        if cpu_fnv:
+            out["cpu_fnv"] = cpu_fnv
+            out["fnv_match"] = out["gpu_fnv"] == cpu_fnv
     if g is None:
         out["reference"] = None
         return out
     rgb3 = rgb.reshape(-1, 3)
     idx = g["idx"]
-    ch = lambda p: np.stack([(p >> 16) & 255, (p >> 8) & 255, p & 255], -1).astype(np.int32)  # noqa: E731
-    px_ok = hashlib.sha256(px.tobytes()).hexdigest() == str(g["sha_pixels"][0])
-    rgb_ok = hashlib.sha256(rgb3.tobytes()).hexdigest() == str(g["sha_rgb"][0])
+    px_ok = sha256(px) == str(g["sha_pixels"][0])
+    rgb_ok = sha256(rgb3) == str(g["sha_rgb"][0])
     out.update({"reference": str(f.relative_to(ROOT)), "pixels_sha256_match": px_ok, "rgb_sha256_match": rgb_ok,
                 "bit_exact": bool(px_ok and rgb_ok),
                 "max_abs": float(np.abs(rgb3[idx] - g["rgb"]).max()),
-                "max_lsb": int(np.abs(ch(px[idx]) - ch(g["pixels"])).max()),
+                "max_lsb": int(np.abs(_channels(px[idx]) - _channels(g["pixels"])).max()),
                 "samples": int(idx.size), "tolerance": "max_abs <= 1e-4, <= 1 LSB (north star)"})
-    out["within_tolerance"] = bool(out["max_abs"] <= 1e-4 and out["max_lsb"] <= 1)
+    out["within_tolerance"] = bool(out["max_abs"] <= 1e-4 and out["max_lsb"] <= 1 and not np.isnan(rgb3).any())
+    out["required"] = "bit_exact" if exact else "within_tolerance (powf in the BRDF)"
+    out["ok"] = bool(out["bit_exact"] if exact else out["within_tolerance"])
     return out
 
 
-K_KERNEL_LAUNCHES = 1000   # launches averaged for roofline.kernel_ms
+# ---------------------------------------------------------------------------- one workload
+class Workload:
+    """One scene x size x mode on this rank's contexts: the timed regions, the algorithmic
+    FLOP count, and the gathered frame for the parity check."""
+
+    def __init__(self, ctxs, d: Dist, scene: str, W: int, H: int, mode: str):
+        self.ctxs, self.d = ctxs, d
+        self.scene, self.W, self.H, self.mode = scene, W, H, mode
+        N = d.world
+        self.striped = N > 1
+        self.hs = HostScene(scene)
+        s, cam = self.hs.view()
+        for c in ctxs:
+            c.upload(s)
+        self.cam = cam
+        self.nviews = 1 if mode == "frame" else N
+        self.views = make_views(cam, self.nviews)
+        self.params = abi.make_params(W, H, stripe_rows=16 if self.striped else 0, stripe_first=d.rank,
+                                      stripe_step=N)
+        self.frame_pixels = self.nviews * W * H   # per step, all ranks together
+        self.lib = ctxs[0].lib
+
+    def step(self, i, gather_to=None):
+        c = self.ctxs[i % len(self.ctxs)]
+        rc = self.lib.rtx_render_views_async(c.h, self.views, self.nviews, C.byref(self.params), 0)
+        if rc != abi.RTX_OK:
+            abi.check(rc, "rtx_render_views_async", c.h)
+        if gather_to is not None:
+            c.gather_async(gather_to)
+
+    def sync_all(self):
+        for c in self.ctxs:
+            c.synchronize()
+
+    def timed(self, fn, k):
+        self.d.barrier()
+        self.sync_all()
+        t0 = time.perf_counter()
+        for i in range(k):
+            fn(i)
+        self.sync_all()
+        self.d.barrier()
+        return self.d.max(time.perf_counter() - t0)
+
+    def kernel_ms(self, launches: int) -> float:
+        """Mean launch time of ONE context's serialized launches (HIP events on its stream)."""
+        ms = C.c_float()
+        ctx = self.ctxs[0]
+        abi.check(self.lib.rtx_time_views(ctx.h, self.views, self.nviews, C.byref(self.params), launches,
+                                          C.byref(ms)), "rtx_time_views", ctx.h)
+        return ms.value
+
+    def flop(self) -> tuple[int, int, int, int]:
+        """Algorithmic work (SURVEY §8(d) FLOP model, instrumented kernel) of this rank's
+        launch and of the whole step over all ranks: (flop, pixels, step flop, step pixels)."""
+        N, r = self.d.world, self.d.rank
+        counts = np.zeros(12, np.uint64)
+        for f in range(self.nviews):
+            pv = abi.make_params(self.W, self.H, stripe_rows=16 if self.striped else 0,
+                                 stripe_first=(r - f) % N if self.mode == "views" else r, stripe_step=N)
+            counts += self.ctxs[0].count_work(self.views[f], pv)
+        flop = int(sum(int(c) * w for c, w in zip(counts, COST)))
+        pixels = int(counts[0])
+        step_flop, step_pixels = self.d.sum_i64([flop, pixels])
+        return flop, pixels, step_flop, step_pixels
+
+    def run(self, steps: int, warmup: int, launches: int, gather: bool, tag: str) -> dict:
+        d, W, H = self.d, self.W, self.H
+        kernel_ms = self.kernel_ms(launches)
+        for i in range(warmup):
+            self.step(i)
+        self.sync_all()
+        elapsed = self.timed(self.step, steps)          # device-resident frames (`value`)
+
+        # the same frames gathered into host frames shared by the ranks
+        nbytes = self.nviews * W * H * 16   # uint32 pixels + float RGB plane per view (parity)
+        shared = None
+        if d.rank == 0:
+            shared = SharedFrame.create(tag, nbytes)
+        d.barrier()
+        if d.rank != 0:
+            shared = SharedFrame.attach(tag, nbytes)
+        d.barrier()
+        if d.rank == 0:
+            shared.unlink()   # every rank has it mapped: nothing stays behind in /dev/shm
+        pinned = shared.pin(self.ctxs[0])
+        host_px = shared.view(np.uint32, self.nviews * W * H)
+        host_rgb = shared.view(np.float32, 3 * self.nviews * W * H, offset=4 * self.nviews * W * H)
+        gathered = None
+        if gather:
+            for i in range(min(warmup, 10)):
+                self.step(i, host_px)
+            self.sync_all()
+            g_elapsed = self.timed(lambda i: self.step(i, host_px), steps)
+            gathered = {"mpix_s": round(self.frame_pixels * steps / g_elapsed / 1e6, 3),
+                        "ms_per_step": round(g_elapsed / steps * 1e3, 5), "pinned": bool(pinned),
+                        "target": "page-locked host frames (one per view) shared by all ranks (/dev/shm mapping)",
+                        "copy": "hipMemcpy2DAsync of the rank's own 16-row stripes (rtx_gather_async)"}
+        flop, pixels, step_flop, step_pixels = self.flop()
+        # Parity: every rank renders its stripes once more on the timed context (same schedule
+        # state), with colours, gathered into the shared host frame; rank 0 checks view 0.
+        ctx = self.ctxs[0]
+        abi.check(self.lib.rtx_render_views_async(ctx.h, self.views, self.nviews, C.byref(self.params), 1),
+                  "rtx_render_views_async", ctx.h)
+        ctx.gather_async(host_px, host_rgb)
+        ctx.synchronize()
+        d.barrier()
+        px0 = np.array(host_px[:W * H]) if d.rank == 0 else None
+        rgb0 = np.array(host_rgb[:3 * W * H]) if d.rank == 0 else None
+        d.barrier()   # nobody unmaps before rank 0 has copied the frame
+        del host_px, host_rgb
+        shared.close()
+        return {"kernel_ms": kernel_ms, "elapsed": elapsed, "gathered": gathered, "flop": flop, "pixels": pixels,
+                "step_flop": step_flop, "step_pixels": step_pixels, "px0": px0, "rgb0": rgb0,
+                "value": self.frame_pixels * steps / elapsed / 1e6, "ms_per_step": elapsed / steps * 1e3}
+
+
+def roofline(flop: int, kernel_ms: float, rec: dict | None, src: str | None) -> dict:
+    achieved = flop / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
+    out = {"bound": "valu", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": round(achieved / FP32_PEAK_TFLOPS, 5)}
+    traffic = rec["hbm_bytes_per_launch"] if rec else None
+    frame_traffic = rec.get("hbm_bytes_per_frame") if rec else None
+    out.update({"traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC, main render kernel)",
+                "traffic_source": src,
+                "traffic_note": None if rec else "no PMC record of this librtx_hip.so build for this configuration",
+                "hbm_bytes_per_frame": frame_traffic,
+                "hbm_gbs": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic and kernel_ms > 0 else None,
+                # north star: the HBM roofline fraction, reported beside the VALU one
+                "hbm_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                if traffic and kernel_ms > 0 else None,
+                "kernel_ms": round(kernel_ms, 5)})
+    return out
+
+
+def parity_configs(dev: int) -> list[dict]:
+    """Every BASELINE config (+ W4_Reference, W4_Optional) at full size on a fresh context:
+    PARITY_FRAMES frames (frame 1 measures tile costs, later ones run cost-ordered and split),
+    the last one checked against the reference's frame."""
+    out = []
+    for scene, W, H, exact in PARITY_CONFIGS:
+        ctx = DeviceContext(dev)
+        try:
+            hs = HostScene(scene)
+            s, cam = hs.view()
+            ctx.upload(s)
+            p = abi.make_params(W, H)
+            for _ in range(PARITY_FRAMES - 1):
+                ctx.render_async(cam, p)
+            px, rgb = ctx.render(cam, p)
+            heavy = ctx.split_info()[0]
+            rep = parity_report(px, rgb, scene, W, H, exact=exact, with_fnv=False)
+            out.append({"config": f"{scene} {W}x{H}", "frames": PARITY_FRAMES, "heavy_tiles_split": heavy, **rep})
+        finally:
+            ctx.close()
+    return out
 
 
 def main() -> int:
@@ -300,122 +567,25 @@ def main() -> int:
     ap.add_argument("--cpu-frames", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the host-gather timed region")
+    ap.add_argument("--no-extra", action="store_true", help="headline only: no multi_gpu_configs / parity_configs")
     ap.add_argument("--inflight", type=int, default=2, help="frames in flight (render contexts per GPU)")
     args = ap.parse_args()
 
-    # The render contexts come up BEFORE the gloo process group: torch's gloo barrier
-    # initialises torch's own bundled HIP runtime, after which this process's ROCm runtime
-    # (librtx_hip) no longer detects the device ("no ROCm-capable device", seen at N = 2).
-    # RTX_BENCH_DEVICE pins every rank to one device: rehearsing the N-rank path on a
-    # one-GPU machine (the driver's multi-GPU runs leave it unset: rank r -> device LOCAL_RANK)
+    # RTX_BENCH_DEVICE pins every rank to one device: rehearsing the N-rank path on a one-GPU
+    # machine (the driver's multi-GPU runs leave it unset: rank r -> device LOCAL_RANK)
     dev = int(os.environ.get("RTX_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     ctxs = [DeviceContext(dev) for _ in range(max(1, args.inflight))]
     d = Dist()
     N = d.world
     if args.gpus != N and d.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={N}; using {N}", file=sys.stderr)
-    hs = HostScene(args.scene)
-    scene, cam = hs.view()
-    for c in ctxs:
-        c.upload(scene)
-    ctx = ctxs[0]
-    lib = ctx.lib
-    W, H = args.width, args.height
-    striped = N > 1
-    if args.mode == "frame":
-        nviews = 1
-        views = make_views(cam, 1)
-        params = abi.make_params(W, H, stripe_rows=16 if striped else 0, stripe_first=d.rank, stripe_step=N)
-        frame_pixels = W * H                       # one frame per step, all ranks together
-    else:
-        nviews = N
-        views = make_views(cam, N)
-        params = abi.make_params(W, H, stripe_rows=16 if striped else 0, stripe_first=d.rank, stripe_step=N)
-        frame_pixels = N * W * H                   # N frames per step, one frame's worth per rank
-
-    def step(i, gather_to=None):
-        c = ctxs[i % len(ctxs)]
-        rc = lib.rtx_render_views_async(c.h, views, nviews, C.byref(params), 0)
-        if rc != abi.RTX_OK:
-            abi.check(rc, "rtx_render_views_async", c.h)
-        if gather_to is not None:
-            c.gather_async(gather_to)
-
-    def sync_all():
-        for c in ctxs:
-            c.synchronize()
-
-    def timed(fn, k):
-        d.barrier()
-        sync_all()
-        t0 = time.perf_counter()
-        for i in range(k):
-            fn(i)
-        sync_all()
-        d.barrier()
-        return d.max(time.perf_counter() - t0)
-
-    # Kernel-only time of the same launches (HIP events on the launch stream), the roofline's
-    # denominator: the mean of kKernelLaunches serialized launches, taken first — it also brings
-    # the GPU from its idle clock to the steady rendering clock (profiles/r02/warmup_probe.txt),
-    # which the requested W warm-up steps alone (the driver uses 5) do not.
-    kernel_ms = C.c_float()
-    abi.check(lib.rtx_time_views(ctx.h, views, nviews, C.byref(params), K_KERNEL_LAUNCHES,
-                                 C.byref(kernel_ms)), "rtx_time_views", ctx.h)
-    kernel_ms = kernel_ms.value
-
-    for i in range(args.warmup):
-        step(i)
-    sync_all()
-
-    # ---- timed region 1: device-resident frames (`value`)
-    elapsed = timed(step, args.steps)
-
-    # ---- timed region 2: the same frames gathered into host frames shared by the ranks
-    shared = None
-    gathered = None
-    nbytes = nviews * W * H * 16    # uint32 pixels + float RGB plane per view (parity check)
+    lib_hash = lib_sha256()
     tag = f"{os.environ.get('MASTER_PORT', 'solo')}_{os.getuid()}_{os.getppid() if N > 1 else os.getpid()}"
-    if d.rank == 0:
-        shared = SharedFrame.create(tag, nbytes)
-    d.barrier()
-    if d.rank != 0:
-        shared = SharedFrame.attach(tag, nbytes)
-    d.barrier()
-    if d.rank == 0:
-        shared.unlink()   # every rank has it mapped: nothing stays behind in /dev/shm
-    pinned = shared.pin(ctx)
-    host_px = shared.view(np.uint32, nviews * W * H)
-    host_rgb = shared.view(np.float32, 3 * nviews * W * H, offset=4 * nviews * W * H)
-    if not args.no_gather:
-        for i in range(min(args.warmup, 10)):
-            step(i, host_px)
-        sync_all()
-        g_elapsed = timed(lambda i: step(i, host_px), args.steps)
-        gathered = {"mpix_s": round(frame_pixels * args.steps / g_elapsed / 1e6, 3),
-                    "ms_per_step": round(g_elapsed / args.steps * 1e3, 5), "pinned": bool(pinned),
-                    "target": "page-locked host frames (one per view) shared by all ranks (/dev/shm mapping)",
-                    "copy": "hipMemcpy2DAsync of the rank's own 16-row stripes (rtx_gather_async)"}
+    W, H = args.width, args.height
 
-    # Algorithmic work of one launch (SURVEY §8(d) FLOP model) from the instrumented kernel.
-    counts_total = np.zeros(12, np.uint64)
-    for f in range(nviews):
-        pv = abi.make_params(W, H, stripe_rows=16 if striped else 0,
-                             stripe_first=(d.rank - f) % N if args.mode == "views" else d.rank, stripe_step=N)
-        counts_total += ctx.count_work(views[f], pv)
-    flop = int(sum(int(c) * w for c, w in zip(counts_total, COST)))
-    pixels_per_rank = int(counts_total[0])
-    frame_flop, frame_counted = d.sum_i64([flop, pixels_per_rank])
-
-    # Parity of the benchmarked frame: every rank renders its stripes once more on the timed
-    # context (same schedule state), with colours, gathered into the shared host frame.
-    parity = None
-    if shared is not None:
-        abi.check(lib.rtx_render_views_async(ctx.h, views, nviews, C.byref(params), 1), "rtx_render_views_async",
-                  ctx.h)
-        ctx.gather_async(host_px, host_rgb)
-        ctx.synchronize()
-        d.barrier()
+    # ---- 1. headline
+    hw = Workload(ctxs, d, args.scene, W, H, args.mode)
+    hr = hw.run(args.steps, args.warmup, K_KERNEL_LAUNCHES, not args.no_gather, tag + "_h")
 
     # End-to-end single frame through the blocking C-ABI entry into pageable memory (N = 1).
     e2e = None
@@ -425,34 +595,90 @@ def main() -> int:
         ts = []
         for _ in range(10):
             t1 = time.perf_counter()
-            abi.check(lib.rtx_render(ctx.h, C.byref(cam), C.byref(p1), host.ctypes.data_as(C.POINTER(C.c_uint32)),
-                                     None), "rtx_render", ctx.h)
+            abi.check(hw.lib.rtx_render(ctxs[0].h, C.byref(hw.cam), C.byref(p1),
+                                        host.ctypes.data_as(C.POINTER(C.c_uint32)), None), "rtx_render", ctxs[0].h)
             ts.append(time.perf_counter() - t1)
         e2e = W * H / float(np.median(ts)) / 1e6
 
+    # ---- 2. the north star's multi-GPU workloads, one image per step tiled over the N ranks
+    multi = []
+    if not args.no_extra:
+        for scene, mw, mh, msteps in MULTI_GPU_CONFIGS:
+            wl = Workload(ctxs, d, scene, mw, mh, "frame")
+            r = wl.run(msteps, 10, 100, not args.no_gather, f"{tag}_{scene}")
+            rec, src = pmc_traffic(scene, mw, mh, 1, N, lib_hash)
+            # every rank's HBM rate over its own launches (the PMC record is rank 0's stripes)
+            per_rank = d.gather([r["kernel_ms"], r["flop"]])
+            entry = {"config": f"{scene} {mw}x{mh}, one frame per step tiled over {N} rank(s) in 16-row stripes",
+                     "scene": scene, "width": mw, "height": mh, "n_gpus": N, "steps": msteps,
+                     "mpix_s": round(r["value"], 3), "ms_per_step": round(r["ms_per_step"], 5),
+                     "gathered_mpix_s": r["gathered"]["mpix_s"] if r["gathered"] else None,
+                     "roofline_rank0": roofline(r["flop"], r["kernel_ms"], rec, src),
+                     "per_rank_kernel_ms": [round(float(x), 5) for x in per_rank[:, 0]],
+                     "per_rank_tflops": [round(float(f) / (float(k) * 1e-3) / 1e12, 3) if k > 0 else None
+                                         for k, f in per_rank],
+                     "hbm_per_rank": None, "frame_flop_all_ranks": r["step_flop"],
+                     "frame_pixels_counted": r["step_pixels"]}
+            if rec:
+                entry["hbm_per_rank"] = [
+                    {"gbs": round(rec["hbm_bytes_per_launch"] / (float(k) * 1e-3) / 1e9, 2),
+                     "frac": round(rec["hbm_bytes_per_launch"] / (float(k) * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+                    for k in per_rank[:, 0]]
+                entry["hbm_note"] = ("rank 0's PMC bytes per launch over each rank's own launch time (ranks render "
+                                     "equal shares of 16-row stripes)")
+            if d.rank == 0:
+                entry["parity"] = parity_report(r["px0"], r["rgb0"], scene, mw, mh, with_fnv=False)
+            multi.append(entry)
+
+    # ---- 3. parity of every config at full size (N = 1; one rank per GPU renders stripes at N > 1)
+    pconf = parity_configs(dev) if (N == 1 and not args.no_extra) else None
+
+    # ---- 4. CPU reference on this host, same run (rank 0, N = 1)
     cpu = None
     if d.rank == 0 and N == 1 and not args.no_cpu_baseline:
+        ref = CpuReference()
         try:
-            cpu = cpu_baseline(args.scene, W, H, args.cpu_frames)
+            cpu = cpu_baseline(ref, args.scene, W, H, args.cpu_frames)
+            nthreads = len(os.sched_getaffinity(0))
+            for entry in multi:   # one frame of each multi-GPU workload, all threads
+                try:
+                    cr = ref.run(entry["scene"], entry["width"], entry["height"], nthreads, 1)
+                    entry["cpu_reference_mpix_s"] = round(cr["mpix_s"], 4)
+                    entry["speedup_vs_cpu"] = round(entry["mpix_s"] / cr["mpix_s"], 1)
+                except Exception as e:   # noqa: BLE001
+                    entry["cpu_reference_mpix_s"] = f"failed: {e}"
         except Exception as e:   # the baseline must not take the headline down
-            cpu = {"value": None, "unit": "Mpixels/s", "cores": 0, "kind": "reference", "sample": f"failed: {e}"}
-    if d.rank == 0 and shared is not None:
-        # view 0 is the reference camera: the frame the goldens were made from
-        parity = parity_report(np.array(host_px[:W * H]), np.array(host_rgb[:3 * W * H]), args.scene, W, H, cpu)
+            cpu = {"value": None, "unit": "Mpixels/s", "cores": 0, "kind": ref.kind, "sample": f"failed: {e}"}
+        finally:
+            ref.close()
 
-    ms_per_step = elapsed / args.steps * 1e3
-    value = frame_pixels * args.steps / elapsed / 1e6
-    achieved = flop / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(args.scene, W, H, nviews) if not striped else (None, None)
+    parity = None
+    if d.rank == 0:
+        # view 0 is the reference camera: the frame the goldens were made from
+        parity = {"frame": "the host-gathered frame of the timed contexts (cost-ordered / split state)",
+                  **parity_report(hr["px0"], hr["rgb0"], args.scene, W, H, cpu.get("fnv") if cpu else None)}
+
+    rec, src = pmc_traffic(args.scene, W, H, hw.nviews, N, lib_hash)
+    roof = roofline(hr["flop"], hr["kernel_ms"], rec, src)
+    roof.update({"kernel": "rtx_render_kernel<false, 0, false, SPEC> (the specialised variant the scene's facts "
+                           "select; + split phases 1-3 when tiles are heavy)",
+                 "kernel_launches": K_KERNEL_LAUNCHES, "flop_per_launch": hr["flop"],
+                 "pixels_per_launch": hr["pixels"], "flop_per_pixel": round(hr["flop"] / max(hr["pixels"], 1), 2),
+                 "frame_flop_all_ranks": hr["step_flop"], "frame_pixels_counted": hr["step_pixels"],
+                 "lib_sha256": lib_hash,
+                 "note": "FP32 VALU-bound path (no dense contraction, 4 B/pixel of HBM output); "
+                         "FLOP = SURVEY §8(d) algorithmic model counted by the instrumented kernel; "
+                         "kernel_ms/achieved are rank 0's launches (mean of kernel_launches serialized launches, "
+                         "timed before the warm-up)"})
     strong = args.mode == "frame"
     out = {
         "metric": "Mpixels/s (primary+shadow rays) at 1920x1080; per-channel max-abs vs CPU ref",
-        "value": round(value, 3),
+        "value": round(hr["value"], 3),
         "unit": "Mpixels/s",
         "n_gpus": N,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 5),
+        "ms_per_step": round(hr["ms_per_step"], 5),
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
@@ -465,39 +691,25 @@ def main() -> int:
                                 f"over {N} ranks in 16-row stripes" if strong else
                                 f"{args.scene} {W}x{H}, Combined lighting, shadows on, {N} views per step, each "
                                 f"tiled over the {N} ranks in 16-row stripes"),
-                   "scene": args.scene, "width": W, "height": H, "views_per_step": nviews,
-                   "stripe_rows": 16 if striped else 0,
+                   "scene": args.scene, "width": W, "height": H, "views_per_step": hw.nviews,
+                   "stripe_rows": 16 if N > 1 else 0,
                    "parallelism": f"image stripes x{N} (no collective)", "frames_in_flight": len(ctxs)},
-        "roofline": {"bound": "valu", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP32_PEAK_TFLOPS, 5), "traffic": traffic,
-                     "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
-                     "hbm_gbs": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic and kernel_ms > 0 else None,
-                     # north star: the HBM roofline fraction, reported beside the VALU one
-                     "hbm_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
-                     if traffic and kernel_ms > 0 else None,
-                     "kernel": "rtx_render_kernel<false, 0, false, SPEC> (the specialised variant the scene's "
-                               "facts select; + split phases 1-3 when tiles are heavy)",
-                     "kernel_ms": round(kernel_ms, 5), "kernel_launches": K_KERNEL_LAUNCHES,
-                     "flop_per_launch": flop, "pixels_per_launch": pixels_per_rank,
-                     "flop_per_pixel": round(flop / max(pixels_per_rank, 1), 2),
-                     "frame_flop_all_ranks": frame_flop, "frame_pixels_counted": frame_counted,
-                     "note": "FP32 VALU-bound path (no dense contraction, 4 B/pixel of HBM output); "
-                             "FLOP = SURVEY §8(d) algorithmic model counted by the instrumented kernel; "
-                             "kernel_ms/achieved are rank 0's launches (mean of kernel_launches serialized launches, "
-                             "timed before the warm-up)"},
+        "roofline": roof,
         "cpu_baseline": cpu,
         "parity": parity,
-        "host_gather": gathered,
+        "host_gather": hr["gathered"],
         "end_to_end_mpix_s": round(e2e, 3) if e2e else None,
+        "multi_gpu_configs": multi,
+        "parity_configs": pconf,
     }
+    if pconf is not None:
+        out["parity_configs_all_ok"] = all(p.get("ok", False) for p in pconf)
     if cpu and cpu.get("value"):
-        out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        out["speedup_vs_cpu"] = round(hr["value"] / cpu["value"], 1)
         if cpu.get("full_host_upper_bound_mpix_s"):
-            out["speedup_vs_cpu_full_host_upper_bound"] = round(value / cpu["full_host_upper_bound_mpix_s"], 1)
+            out["speedup_vs_cpu_full_host_upper_bound"] = round(hr["value"] / cpu["full_host_upper_bound_mpix_s"], 1)
     if d.rank == 0:
         print(json.dumps(out), flush=True)
-    if shared is not None:
-        shared.close()
     for c in ctxs:
         c.close()
     d.close()

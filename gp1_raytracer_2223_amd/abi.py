@@ -138,7 +138,7 @@ def load_host() -> C.CDLL:
         lib.rtx_host_scene_spinning.restype = C.c_int
         lib.rtx_host_scene_mesh_source.argtypes = [VP, C.c_uint32, C.POINTER(MeshSource)]
         lib.rtx_host_scene_mesh_source.restype = C.c_int
-        lib.rtx_host_scene_transforms.argtypes = [VP, C.c_float, C.POINTER(C.c_float)]
+        lib.rtx_host_scene_transforms.argtypes = [VP, C.c_float, C.POINTER(C.c_float), C.c_uint32]
         lib.rtx_host_scene_transforms.restype = C.c_int
         _host = lib
     return _host

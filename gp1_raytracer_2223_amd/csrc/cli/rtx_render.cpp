@@ -104,9 +104,27 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
     // device-side Update: register the scene's turning meshes on the first context
     rtx_anim* anim = nullptr;
     std::vector<float> mats;
+    int n_anim = 0;
+    // every registered mesh's device Update status (NaN vertex, a tree too deep to render)
+    auto anim_ok = [&]() {
+        for (int i = 0; i < n_anim; ++i) {
+            uint32_t st[4];
+            if (rtx_anim_status(anim, static_cast<uint32_t>(i), st) != RTX_OK) {
+                std::fprintf(stderr, "device Update failed (registered mesh %d): %s\n", i, rtx_anim_last_error(anim));
+                return false;
+            }
+        }
+        return true;
+    };
     if (device_update && animated) {
         std::vector<int32_t> ids(64);
-        const int ns = rtx_host_scene_spinning(hs, ids.data(), 64);
+        const int ns = rtx_host_scene_spinning(hs, ids.data(), static_cast<uint32_t>(ids.size()));
+        if (ns > static_cast<int>(ids.size())) {   // rtx_anim_create takes at most 8 anyway
+            std::fprintf(stderr, "--device-update: %d turning meshes, more than %zu\n", ns, ids.size());
+            for (size_t i = 1; i < ctx.size(); ++i) rtx_destroy(ctx[i]);
+            return 1;
+        }
+        n_anim = ns;
         std::vector<rtx_mesh_source> src(ns > 0 ? ns : 0);
         for (int i = 0; i < ns; ++i) rtx_host_scene_mesh_source(hs, static_cast<uint32_t>(ids[i]), &src[i]);
         rtx_host_scene_view(hs, &s, &cam);
@@ -129,6 +147,7 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
             const float elapsed = static_cast<float>(secs(prev, w1));                  // Timer::Update
             prev = w1;
             if (seq) {
+                if (anim && !anim_ok()) { rc = 1; break; }   // never write a frame of a failed Update
                 r.Pixels() = buf[f];
                 if (!r.SaveBufferToImage(stem + "_" + std::to_string(frames - 1) + ".bmp")) { rc = 1; break; }
                 if (frames == static_cast<long>(seq->size())) break;
@@ -142,7 +161,7 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
         }
         const Clock::time_point f0 = Clock::now();
         const float tnow = seq ? (*seq)[queued] : static_cast<float>(secs(start, f0));
-        if (anim) rtx_host_scene_transforms(hs, tnow, mats.data());   // the turn Update(t) applies
+        if (anim) rtx_host_scene_transforms(hs, tnow, mats.data(), static_cast<uint32_t>(n_anim));   // Update(t)'s turn
         else if (animated) rtx_host_scene_update(hs, tnow);                // Scene::Update
         const Clock::time_point f1 = Clock::now();
         if (!ok(rtx_host_scene_view(hs, &s, &cam), "rtx_host_scene_view", nullptr)) break;
@@ -166,11 +185,7 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
     }
     for (int f = 0; f < inflight; ++f) rtx_synchronize(ctx[f]);
     if (anim) {
-        uint32_t st[4];
-        if (rtx_anim_status(anim, 0, st) != RTX_OK) {
-            std::fprintf(stderr, "device Update failed: %s\n", rtx_anim_last_error(anim));
-            rc = 1;
-        }
+        if (!anim_ok()) rc = 1;
         rtx_anim_destroy(anim);
     }
     if (last >= 0) r.Pixels() = buf[last];   // the last completed frame (SaveBufferToImage)

@@ -97,18 +97,20 @@ extern "C" int rtx_host_scene_mesh_source(rtx_host_scene* s, uint32_t mesh, rtx_
     return RTX_OK;
 }
 
-extern "C" int rtx_host_scene_transforms(rtx_host_scene* s, float total_time, float* out) {
-    if (!s || !out) return RTX_E_INVALID;
+extern "C" int rtx_host_scene_transforms(rtx_host_scene* s, float total_time, float* out, uint32_t capacity) {
+    if (!s || (!out && capacity)) return RTX_E_INVALID;
     const float yaw = rtx::Scene::SpinYaw(total_time);
-    int i = 0;
+    uint32_t i = 0;
     for (rtx::TriangleMesh* m : s->scene->Spinning()) {
-        m->RotateY(yaw);
-        const rtx::Mat4 f = m->scaleTransform * m->rotationTransform * m->translationTransform;   // DataTypes.h:213
-        for (int r = 0; r < 4; ++r)
-            for (int c = 0; c < 4; ++c) out[16 * i + 4 * r + c] = f.d[r].at(c);
+        m->RotateY(yaw);   // every turning mesh turns; only the first `capacity` are written
+        if (i < capacity) {
+            const rtx::Mat4 f = m->scaleTransform * m->rotationTransform * m->translationTransform;   // DataTypes.h:213
+            for (int r = 0; r < 4; ++r)
+                for (int c = 0; c < 4; ++c) out[16 * i + 4 * r + c] = f.d[r].at(c);
+        }
         ++i;
     }
-    return i;
+    return static_cast<int>(i);
 }
 
 extern "C" int rtx_host_camera_set(rtx_host_scene* s, const float origin[3], float fov_degrees, float pitch,

@@ -8,6 +8,7 @@
 #include <fstream>
 #include <random>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -101,6 +102,7 @@ private:
         unsigned n = std::thread::hardware_concurrency();
         if (const char* e = std::getenv("RTX_HOST_THREADS")) n = static_cast<unsigned>(std::atoi(e));
         n = n > 8 ? 8 : n;
+        if (const char* e = std::getenv("RTX_HOST_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
         for (unsigned k = 1; k < n; ++k) threads_.emplace_back([this] { Loop(); });
         for (auto& th : threads_) th.detach();
     }
@@ -118,12 +120,21 @@ private:
         return true;
     }
     // Workers spin a while on the queue counter before sleeping: during a build the next
-    // subtree task is picked up within a microsecond instead of a futex wake-up.
+    // subtree task is picked up within a microsecond instead of a futex wake-up.  The spin is
+    // bounded in TIME (spin_us_ after the last task, RTX_HOST_SPIN_US, default 200 us: well
+    // inside one build, shorter than the gap between two animated frames), so idle workers
+    // sleep instead of burning the CPU quota the render thread and other ranks share.
     void Loop() {
+        using Clock = std::chrono::steady_clock;
         for (;;) {
-            for (int spin = 0; spin < kSpin; ++spin) {
-                if (queued_.load(std::memory_order_acquire) > 0 && RunOne()) spin = 0;
-                else _mm_pause();
+            Clock::time_point last = Clock::now();
+            for (unsigned it = 1;; ++it) {
+                if (queued_.load(std::memory_order_acquire) > 0 && RunOne()) {
+                    last = Clock::now();
+                    continue;
+                }
+                _mm_pause();
+                if ((it & 63u) == 0 && Clock::now() - last > std::chrono::microseconds(spin_us_)) break;
             }
             std::unique_lock<std::mutex> g(mu_);
             sleeping_.fetch_add(1, std::memory_order_acq_rel);
@@ -131,7 +142,7 @@ private:
             sleeping_.fetch_sub(1, std::memory_order_acq_rel);
         }
     }
-    static constexpr int kSpin = 1 << 16;   // ~1-2 ms of _mm_pause
+    int spin_us_ = 200;
     std::atomic<int> queued_{0}, sleeping_{0};
     std::vector<std::thread> threads_;
     std::mutex mu_;

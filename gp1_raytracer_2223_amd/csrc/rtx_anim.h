@@ -77,6 +77,10 @@ struct Launch {
     float m[kMaxAnimMeshes][12]; // finalTransform: rows data[0..3], xyz each (Matrix.cpp:35-56)
     Image img;
     uint32_t lds_bytes;          // dynamic LDS per workgroup (meshes that fit build from it)
+    // A rebuilt tree this many levels deep or deeper would overflow the render kernel's
+    // kStackDepth-entry DFS stack: the build then disables the mesh in the image (node count
+    // 0, no frontier parts) and reports kErrDepth.  rtxd::kStackDepth; lower only in tests.
+    uint32_t depth_limit;
 };
 
 enum : uint32_t { kErrNaN = 1u, kErrDepth = 2u };

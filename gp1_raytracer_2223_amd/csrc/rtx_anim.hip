@@ -882,19 +882,24 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
             __builtin_amdgcn_wave_barrier();
         }
         const uint32_t nf = s_nfr;
+        // A tree deeper than the render kernel's DFS stack must never reach it (its pushes are
+        // unchecked): the mesh is disabled in this image — no frontier parts, node count 0, so
+        // mesh_traverse / part_traverse skip it — and the update reports kErrDepth.
+        const bool too_deep = maxd >= L.depth_limit;
         for (uint32_t k = lane; k < M.part_cap; k += 64u) {
-            I.parts[M.part0 + k] = k < nf ? make_int4(static_cast<int>(M.mesh),
+            I.parts[M.part0 + k] = (k < nf && !too_deep) ? make_int4(static_cast<int>(M.mesh),
                                                       static_cast<int>(M.root + M.tmp[s_fr[k][0]].ref),
                                                       static_cast<int>(s_fr[k][1]), static_cast<int>(s_fr[k][2]))
                                           : make_int4(-1, 0, 0, 0);
         }
         if (lane == 0) {
             uint32_t err = Ls.err;
-            if (maxd >= static_cast<uint32_t>(rtxd::kStackDepth)) err |= kErrDepth;
+            if (too_deep) err |= kErrDepth;
             M.status[0] = err;
             M.status[1] = maxd;
             M.status[2] = 1u + 2u * M.tmp[0].splits;   // nodesUsed
-            I.meshes[M.mesh].y = static_cast<int>(M.status[2]);   // the mesh record's node count
+            // the mesh record's node count (0: disabled, see too_deep)
+            I.meshes[M.mesh].y = too_deep ? 0 : static_cast<int>(M.status[2]);
             M.status[3] = nf;
             M.status[62] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
         }

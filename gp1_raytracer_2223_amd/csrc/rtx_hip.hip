@@ -2553,6 +2553,11 @@ struct rtx_anim {
     bool lds_big = false;                 // a mesh exceeds kLdsTris: the launch builds in HBM
     bool built = false;
     uint32_t cur = 0;                     // state buffer of the current order
+    // rebuilt trees this deep or deeper are disabled in the image (rtxa::Launch::depth_limit);
+    // RTX_ANIM_DEPTH_LIMIT lowers it for the tests of that guard
+    uint32_t depth_limit = kStackDepth;
+    bool reg_fast = false;                // DevScene::tri_fast condition at registration
+    std::vector<double> obj_radius;       // per registered mesh: max |object-space position|
 };
 
 namespace {
@@ -2643,6 +2648,10 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
     rtx_anim* a = new (std::nothrow) rtx_anim;
     if (!a) return RTX_E_NOMEM;
     a->device = c->device;
+    if (const char* e = std::getenv("RTX_ANIM_DEPTH_LIMIT")) {
+        const int v = std::atoi(e);
+        if (v >= 1 && v < kStackDepth) a->depth_limit = static_cast<uint32_t>(v);
+    }
     auto bail = [&](int code) { g_anim_err = a->err; rtx_anim_destroy(a); return code; };
 #define ANIM_CREATE_TRY(call)                                                                \
     do {                                                                                     \
@@ -2664,6 +2673,7 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
     // every animated triangle keeps |e1| |e2| within a rounding of its registration value
     // (a rotation): FAST Moller-Trumbore only with a factor-2 margin below its 2^56 bound
     a->dev.tri_fast = lay.max_ee <= 0x1p55 ? 1u : 0u;
+    a->reg_fast = a->dev.tri_fast != 0;
     a->split_ok = c->split_ok;
     a->spec = c->scene_spec;
     std::memcpy(a->room_p0, c->room_p0, sizeof a->room_p0);
@@ -2698,6 +2708,13 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
         ANIM_CREATE_TRY(anim_alloc(a, &d.tmp, 2 * T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.ref, 3 * T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.status, 128));
+        double rad = 0.0;
+        for (size_t k = 0; k < V; ++k) {
+            const double x = q.positions[3 * k], y = q.positions[3 * k + 1], z = q.positions[3 * k + 2];
+            const double r = std::sqrt(x * x + y * y + z * z);
+            rad = (r > rad || r != r) ? r : rad;   // NaN positions are refused above; inf sticks
+        }
+        a->obj_radius.push_back(rad);
         std::vector<float4> pos(V), nrm(T);
         std::vector<int4> idx(T);
         for (size_t k = 0; k < V; ++k) pos[k] = f4(q.positions[3 * k], q.positions[3 * k + 1], q.positions[3 * k + 2], 0.f);
@@ -2768,6 +2785,7 @@ extern "C" int rtx_anim_update(rtx_anim* a, rtx_ctx* c, const float* transforms)
     L.img.parts = reinterpret_cast<int4*>(B.d + a->part_off);
     L.img.oct_bytes = a->oct_bytes;
     L.lds_bytes = a->lds_big ? 0u : a->lds_bytes;
+    L.depth_limit = a->depth_limit;
     ANIM_TRY(a, rtxa::launch_build(L, c->stream));
     ANIM_TRY(a, hipEventRecord(a->ev, c->stream));
     a->built = true;
@@ -2781,6 +2799,22 @@ extern "C" int rtx_anim_update(rtx_anim* a, rtx_ctx* c, const float* transforms)
     c->sb_cur = k;
     c->scene_bytes = a->total;
     c->dev = rebase(a->dev, nullptr, B.d);
+    // FAST Moller-Trumbore needs |e1| |e2| <= 2^56 for every triangle (DevScene::tri_fast).  The
+    // caller's transform is arbitrary (a scale can grow the edges), so bound the rebuilt edges
+    // from this transform: |e| <= |v0'| + |v1'| <= 2 (||M||_F R + |t|) for object radius R,
+    // 3x3 part M and translation t (1 % for the rounding of the transformed positions),
+    // with a factor-2 margin, as at registration.
+    bool fast = a->reg_fast;
+    for (size_t i = 0; fast && i < a->mesh.size(); ++i) {
+        const float* m = transforms + 16 * i;
+        double fro = 0.0, tr = 0.0;
+        for (int r = 0; r < 3; ++r)
+            for (int q = 0; q < 3; ++q) fro += double(m[4 * r + q]) * m[4 * r + q];
+        for (int q = 0; q < 3; ++q) tr += double(m[12 + q]) * m[12 + q];
+        const double e = 2.0 * (std::sqrt(fro) * a->obj_radius[i] + std::sqrt(tr)) * 1.01;
+        fast = e * e <= 0x1p55;   // false for NaN / inf too
+    }
+    c->dev.tri_fast = fast ? 1u : 0u;
     c->deep_stack = false;
     c->split_ok = a->split_ok;
     c->scene_spec = a->spec;

@@ -74,10 +74,14 @@ class HostScene:
 
     def transforms(self, total_time: float) -> np.ndarray:
         """Update(t)'s finalTransform per turning mesh (16 floats each) without rebuilding."""
-        out = np.zeros(16 * 64, np.float32)
-        n = self._lib.rtx_host_scene_transforms(self._h, float(total_time), out.ctypes.data_as(C.POINTER(C.c_float)))
+        cap = 64
+        out = np.zeros(16 * cap, np.float32)
+        n = self._lib.rtx_host_scene_transforms(self._h, float(total_time), out.ctypes.data_as(C.POINTER(C.c_float)),
+                                                cap)
         if n < 0:
             abi.check(n, "rtx_host_scene_transforms")
+        if n > cap:
+            raise RuntimeError(f"{n} turning meshes, more than the {cap} this wrapper holds")
         return out[: 16 * n].copy()
 
     def set_camera(self, origin, fov_degrees: float = 45.0, pitch: float = 0.0, yaw: float = 0.0) -> None:

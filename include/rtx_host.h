@@ -42,12 +42,12 @@ int rtx_host_camera_set(rtx_host_scene* s, const float origin[3], float fov_degr
 /* Device-side Update (rtx_anim_*, rtx.h).  The meshes Update(t) turns (count returned,
  * ids written up to `capacity`), one mesh's object-space state, and the final transforms
  * Update(t) applies: sets each turning mesh's rotation as Update(t) does and writes
- * scale * rotation * translation (16 floats per turning mesh, Matrix data[4] row-major)
- * WITHOUT rebuilding — the host scene's own geometry is then stale until the next
- * rtx_host_scene_update. */
+ * scale * rotation * translation (16 floats per turning mesh, Matrix data[4] row-major, at
+ * most `capacity` meshes written; the count of turning meshes is returned) WITHOUT rebuilding
+ * — the host scene's own geometry is then stale until the next rtx_host_scene_update. */
 int rtx_host_scene_spinning(rtx_host_scene* s, int32_t* mesh_ids, uint32_t capacity);
 int rtx_host_scene_mesh_source(rtx_host_scene* s, uint32_t mesh, rtx_mesh_source* out);
-int rtx_host_scene_transforms(rtx_host_scene* s, float total_time, float* out);
+int rtx_host_scene_transforms(rtx_host_scene* s, float total_time, float* out, uint32_t capacity);
 
 /* Utils::ParseOBJ (source/Utils.h:377-451).  Fills caller buffers when non-NULL and
  * always reports the counts; returns RTX_OK or RTX_E_INVALID (unreadable file). */

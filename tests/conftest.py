@@ -15,6 +15,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+# Under `pytest -x` the first failure ends the run, so the full-size BASELINE configs and the
+# oracle parity suite run before everything else (the driver's round-end `-m gpu` check).
+_FIRST = ("test_gpu_configs.py", "test_gpu_parity.py")
+
+
+def pytest_collection_modifyitems(config, items):
+    def rank(item):
+        name = Path(str(item.fspath)).name
+        return _FIRST.index(name) if name in _FIRST else len(_FIRST)
+    items.sort(key=rank)   # stable: the order inside each file is kept
+
+
 @pytest.fixture(scope="session", autouse=True)
 def _built():
     """Make sure the native libraries exist (builds in-tree if missing)."""

@@ -106,3 +106,47 @@ def test_bench_multi_rank_hip_gloo(mode, tmp_path):
     views = world if mode == "views" else 1
     assert r["roofline"]["frame_pixels_counted"] == views * 1920 * 1080   # every pixel exactly once
     assert r["host_gather"]["mpix_s"] > 0
+
+
+def _ctl_worker(rank, world, port, q):
+    import sys
+    import time
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "tests")]
+    os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank), MASTER_PORT=str(port))
+    import bench
+    d = bench.Dist()
+    out = []
+    for k in range(50):   # back-to-back reductions reuse the two value slots
+        if rank == k % world:
+            time.sleep(0.002)   # a late rank: nobody may leave the barrier before it arrives
+        out.append((d.max(float(rank * 10 + k)), d.sum_i64([rank + 1, k])))
+    g = d.gather([float(rank), 2.0 * rank])
+    d.barrier()
+    d.close()
+    q.put((rank, out, g.tolist()))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_control_plane_shm(world):
+    """bench.py's control plane between rank processes (ShmCtl: barrier, max, sum, gather
+    through one /dev/shm block, no torch in the bench process): every rank sees every
+    reduction's result over all ranks, for 50 reductions in a row with a late rank each time."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31000 + world + os.getpid() % 1000
+    procs = [ctx.Process(target=_ctl_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (o, g)) for r, o, g in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        out, g = res[r]
+        for k, (mx, sm) in enumerate(out):
+            assert mx == float((world - 1) * 10 + k)
+            assert sm == [world * (world + 1) // 2, world * k]
+        assert g == [[float(i), 2.0 * i] for i in range(world)]
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith(f"rtx_ctl_{port}_")]

@@ -192,3 +192,30 @@ def test_anim_create_rejects_bad_input(gpu_ctx):
     ok = (C.c_int32 * 1)(0)
     assert lib.rtx_anim_create(C.byref(h), gpu_ctx.h, C.byref(s), ok, src, 0) == abi.RTX_E_INVALID
     assert lib.rtx_anim_create(C.byref(h), gpu_ctx.h, C.byref(s), ok, src, 9) != abi.RTX_OK
+
+
+def test_device_update_too_deep_tree_is_disabled_not_rendered(monkeypatch):
+    """A rebuilt BVH at or beyond the render kernel's DFS stack depth must never reach the
+    kernel (its stack pushes are unchecked).  The build then disables the mesh in the image
+    (node count 0, no frontier parts) and the update reports the error.  Forced here by
+    lowering the limit to 4 levels (RTX_ANIM_DEPTH_LIMIT, read at rtx_anim_create): the frames,
+    cost-ordered and split, equal a host upload of the same Update with the mesh's BVH absent."""
+    monkeypatch.setenv("RTX_ANIM_DEPTH_LIMIT", "4")
+    dev_scene, host_scene = _scene("W4_Bunny"), _scene("W4_Bunny")
+    a, b = DeviceContext(0), DeviceContext(0)
+    anim = DeviceAnimation(dev_scene, a)
+    anim.update(1.3, a)
+    host_scene.update(1.3)
+    with pytest.raises(RuntimeError, match="too deep"):
+        anim.status(0)
+    s, cam = host_scene.view()
+    s.meshes[0].n_nodes = 0   # the disabled mesh: triangles present, no tree to walk
+    b.upload(s)
+    p = abi.make_params(480, 270)
+    for _ in range(3):
+        apx, _ = a.render(cam, p)
+        bpx, _ = b.render(cam, p)
+        assert np.array_equal(apx, bpx)
+    anim.close()
+    a.close()
+    b.close()

@@ -11,7 +11,8 @@ Bar (BASELINE.json north_star): per-channel max-abs <= 1e-4 on the float colour 
 uint32 within 1 LSB; the powf-free configs (W1, W4_Bunny, Synthetic100k, Bunny8Lights)
 bit-exact, i.e. both SHA-256 equal.  W3 uses Cook-Torrance (powf in Fresnel): the device
 libm's powf may differ by an ulp, so it is checked on the 4096 samples within tolerance and
-its SHA is reported, not required."""
+its SHA is reported, not required; so are W4_Reference and W4_Optional (Cook-Torrance
+spheres / mesh), whose 1080p frames the reference also produced (tests/golden/make_goldens.py)."""
 import hashlib
 import os
 from pathlib import Path
@@ -27,7 +28,9 @@ pytestmark = pytest.mark.gpu
 G = Path(__file__).resolve().parent / "golden"
 TOL = 1e-4
 CONFIGS = [("W1", 640, 480, True), ("W3", 1280, 720, False), ("W4_Bunny", 1920, 1080, True),
-           ("Synthetic100k", 1920, 1080, True), ("Bunny8Lights", 3840, 2160, True)]
+           ("Synthetic100k", 1920, 1080, True), ("Bunny8Lights", 3840, 2160, True),
+           # the other two animated catalogue scenes (Initialize state) at 1080p: Cook-Torrance powf
+           ("W4_Reference", 1920, 1080, False), ("W4_Optional", 1920, 1080, False)]
 FRAMES = 4
 
 

@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Render one configuration F times for a rocprofv3 PMC pass (tools/pmc_configs.sh).
+
+    python3 tools/pmc_driver.py <scene> <W> <H> <stripe_step> <frames>
+
+Rank 0's stripes of a `stripe_step`-way tiled frame (16-row stripes; step 1 = the whole frame),
+one frame at a time (synchronised), exactly the launches bench.py times: the first frame
+measures tile costs, later ones run cost-ordered and split the heavy tiles."""
+import ctypes as C
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+from gp1_raytracer_2223_amd import abi  # noqa: E402
+
+abi.load_hip()
+from gp1_raytracer_2223_amd.renderer import DeviceContext  # noqa: E402
+from gp1_raytracer_2223_amd.scene import HostScene  # noqa: E402
+
+
+def main() -> int:
+    scene, W, H, step, frames = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+    ctx = DeviceContext(0)
+    s, cam = HostScene(scene).view()
+    ctx.upload(s)
+    p = abi.make_params(W, H, stripe_rows=16 if step > 1 else 0, stripe_first=0, stripe_step=step)
+    for _ in range(frames):
+        abi.check(ctx.lib.rtx_render_views_async(ctx.h, C.byref(cam), 1, C.byref(p), 0), "render", ctx.h)
+        ctx.synchronize()
+    ctx.close()
+    print(f"rendered {frames} frames of {scene} {W}x{H} stripe_step {step}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
