@@ -22,7 +22,8 @@ from gp1_raytracer_2223_amd.scene import HostScene  # noqa: E402
 def main() -> int:
     scene, W, H, step, frames = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
     ctx = DeviceContext(0)
-    s, cam = HostScene(scene).view()
+    hs = HostScene(scene)   # owns the arrays the view points into: keep it alive
+    s, cam = hs.view()
     ctx.upload(s)
     p = abi.make_params(W, H, stripe_rows=16 if step > 1 else 0, stripe_first=0, stripe_step=step)
     for _ in range(frames):
