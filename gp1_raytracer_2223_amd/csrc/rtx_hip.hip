@@ -39,6 +39,12 @@ using namespace rtxd;
 #ifndef RTX_STAMPS
 #define RTX_STAMPS 0
 #endif
+// RTX_STAMPS_LEAN: stamps with the product walk (timeline only; the step counters stay 0)
+#if RTX_STAMPS && !defined(RTX_STAMPS_LEAN)
+#define RTX_STAMPS_WALK 1
+#else
+#define RTX_STAMPS_WALK 0
+#endif
 [[maybe_unused]] constexpr int kStampWords = 6;
 #if RTX_STAMPS
 #define RTX_SPLIT_STAMP()                                                                          \
@@ -520,6 +526,23 @@ constexpr int kPlaneCache = 8;   // planes whose shadow-ray numerators are kept 
 #ifndef RTX_PPLANE_SKIP
 #define RTX_PPLANE_SKIP 0
 #endif
+#ifndef RTX_PREFETCH
+#define RTX_PREFETCH 0
+#endif
+// Prefetch touch (experiment): one wave-uniform vector load of the first dword of each child's
+// record (node pair or first triangle) as soon as the pair arrives, so that the line is in
+// the L2 by the time the walk's scalar load asks for it.  Issued in asm (the compiler does
+// not track it), so every touch is drained with touch_wait (s_waitcnt vmcnt(0), the walk has
+// no other vector loads) before its destination register can be reused.
+__device__ __forceinline__ uint32_t touch_ld(const void* base, uint32_t off) {
+    const char* p = static_cast<const char*>(base) + off;
+    uint32_t v;
+    asm volatile("global_load_dword %0, %1, %2" : "=&v"(v) : "v"(0u), "s"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ void touch_wait(uint32_t a, uint32_t b) {
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(a), "v"(b) : "memory");
+}
 // bvh_walk without counters, shaped for the scalar unit: one inner loop descends through
 // inner nodes with scalar selects (no i1 value crosses a block, so nothing is carried as a
 // VGPR boolean or a lane-mask flow variable), a dead end leaves it as an empty "leaf", and
@@ -532,10 +555,19 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                               uint32_t occ_bit) {
     constexpr bool FAST = SLAB != kSlabExact;
     uint32_t sp = 0;
+    [[maybe_unused]] uint32_t pf0 = 0, pf1 = 0;
     for (;;) {
         while (ntri == 0) {
             NodePair P;
             ldcb64(nb, link, P.l0, P.l1, P.r0, P.r1);
+#if RTX_PREFETCH
+            touch_wait(pf0, pf1);
+            {
+                const uint32_t nl = __float_as_uint(P.l1.w), nr = __float_as_uint(P.r1.w);
+                pf0 = touch_ld(nl ? static_cast<const void*>(S.tris) : nb, __float_as_uint(P.l1.z));
+                pf1 = touch_ld(nr ? static_cast<const void*>(S.tris) : nb, __float_as_uint(P.r1.z));
+            }
+#endif
             const unsigned long long ml = slab_mask<SLAB>(P.l0, P.l1, r) & m;
             const unsigned long long mr = slab_mask<SLAB>(P.r0, P.r1, r) & m;
 #if RTX_ASM_SELECT
@@ -575,6 +607,9 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
             // opaque: a 32-bit s_cmp for the loop test (else it becomes a 64-bit v_cmp on nx)
             ntri = RTX_ASM_SELECT ? opaque(static_cast<uint32_t>(nx >> 32)) : static_cast<uint32_t>(nx >> 32);
         }
+#if RTX_PREFETCH
+        touch_wait(pf0, pf1);
+#endif
         if (m) {
             const bool in = (m >> lane) & 1ull;
             for (uint32_t k = 0; k < ntri; ++k) {
@@ -622,7 +657,7 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
                               unsigned long long& live, Counts& cnt) {
     constexpr bool FAST = SLAB != kSlabExact;
     if (M.y == 0) return;
-    const bool OCT = SLAB == kSlabOct && !COUNT && !RTX_STAMPS;
+    const bool OCT = SLAB == kSlabOct && !COUNT && !RTX_STAMPS_WALK;
     const float4* nb = OCT ? reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.nodes) +
                                                              static_cast<uint32_t>(oct) * S.oct_bytes)
                            : S.nodes;
@@ -633,7 +668,7 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
     const unsigned long long m =
         (OCT ? slab_mask<kSlabOct>(b0, b1, r) : slab_mask<FAST ? kSlabFast : kSlabExact>(b0, b1, r)) & mask;
     if (m == 0) return;
-    if (RTX_LEAN_WALK && !COUNT && !RTX_STAMPS)
+    if (RTX_LEAN_WALK && !COUNT && !RTX_STAMPS_WALK)
         bvh_walk_lean<ANY, OCT ? kSlabOct : (FAST ? kSlabFast : kSlabExact), CB>(
             S, nb, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask, lane, stk, sc_t,
             sc_tri, live, nullptr, 0u);
@@ -675,7 +710,7 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int
         ntri = __float_as_uint(c1.w);
     }
     if (m == 0) return;
-    if (RTX_LEAN_WALK && !RTX_STAMPS)
+    if (RTX_LEAN_WALK && !RTX_STAMPS_WALK)
         bvh_walk_lean<ANY, SLAB, CB>(S, nb, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, sc_t, sc_tri,
                                      live, occ_word, occ_bit);
     else

@@ -14,7 +14,7 @@ for L in $LIBS; do
   for grp in "${GRPS[@]}"; do
     i=$((i+1))
     timeout -s KILL 90 rocprofv3 --pmc $grp -d $OUT/$L/g$i -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --inflight 1 \
-      --no-cpu-baseline --no-gather ${BENCH_ARGS:-} > $OUT/$L.g$i.log 2>&1 || { echo "$L group $i failed"; tail -5 $OUT/$L.g$i.log; exit 1; }
+      --no-cpu-baseline --no-gather --no-extra ${BENCH_ARGS:-} > $OUT/$L.g$i.log 2>&1 || { echo "$L group $i failed"; tail -5 $OUT/$L.g$i.log; exit 1; }
   done
   python3 - "$OUT/$L" "$L" <<'PY'
 import csv, collections, glob, sys

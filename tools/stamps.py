@@ -51,6 +51,11 @@ for q in (10, 25, 50, 75, 90, 99, 100):
 tt = np.linspace(0, end.max(), 21)
 conc = [int(((start <= x) & (end > x)).sum()) for x in tt]
 print("  concurrency over time:", conc)
+dq = np.percentile(dur, [50, 90, 99, 99.9])
+print("  wave duration p50/p90/p99/p99.9 (us):", " / ".join(f"{x:.1f}" for x in dq))
+late = end > 0.9 * end.max()
+print(f"  waves still running in the last 10% of the span: {int(late.sum())}, of them started in the first 10%: "
+      f"{int((late & (start < 0.1 * end.max())).sum())}")
 for x in range(8):
     sel = xcc == x
     if sel.any():
@@ -63,14 +68,14 @@ print(f"  wave node-pair steps: mean {nodes.mean():.0f} p50 {np.median(nodes):.0
       f"tri steps: mean {tris.mean():.0f} max {tris.max()}")
 tiles_x = (W + 7) // 8
 order = np.argsort(-dur)[:12]
-print("  slowest waves: dur_us  node_steps  tri_steps  slab_eff  tri_eff  (px0, py0)")
+print("  slowest waves: dur_us  start_us  node_steps  tri_steps  slab_eff  tri_eff  (px0, py0)")
 for w in order:
     ty, tx = divmod(int(wave_id[w]), tiles_x)
     x0 = tx * 8
     y0 = ty * 8
     se = lane_slab[w] / max(1, 128 * nodes[w])
     te = lane_tri[w] / max(1, 64 * tris[w])
-    print(f"    {dur[w]:9.1f} {nodes[w]:10d} {tris[w]:10d} {se:9.3f} {te:8.3f}  ({x0}, {y0})")
+    print(f"    {dur[w]:9.1f} {start[w]:9.1f} {nodes[w]:10d} {tris[w]:10d} {se:9.3f} {te:8.3f}  ({x0}, {y0})")
 us_per_step = dur / np.maximum(1, nodes + tris)
 print(f"  us per (node+tri) step: p50 {np.median(us_per_step):.3f}  slowest-wave {us_per_step[order[0]]:.3f}")
 for ph in range(2):
