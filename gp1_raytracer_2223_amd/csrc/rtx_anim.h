@@ -1,14 +1,22 @@
 // rtx_anim.h — Scene::Update on the device for animated meshes: the
-// interface between the C-ABI (rtx_anim_* in rtx_hip.hip) and the build kernel
+// interface between the C-ABI (rtx_anim_* in rtx_hip.hip) and the build kernels
 // (rtx_anim.hip).  Internal; not part of the installed headers.
 //
-// One workgroup per animated mesh restates, in HBM and bit for bit,
+// Two launches restate, in HBM and bit for bit,
 //   TriangleMesh::UpdateTransforms   (source/DataTypes.h:210-236)
 //   TriangleMesh::BuildBVH / Subdivide / FindBestSplitPlane / UpdateNodeBounds (:294-483)
 // including the in-place swap partition's permutation of indices, normals and
-// transformedNormals, which the next Update starts from — and writes the result straight
+// transformedNormals, which the next Update starts from — and write the result straight
 // into a scene image in the render layout of rtx_upload_scene (triangle records, the node
-// pairs with their 8 octant copies, the split-rendering frontier).
+// pairs with their 8 octant copies, the split-rendering frontier):
+//   1 rtx_anim_build  workgroup (mesh, 0): transforms, per-triangle build records, the top
+//                     levels of the tree (whole-workgroup teams) until a level holds
+//                     kSubTarget nodes; those become independent subtrees, built by
+//                     workgroups (mesh, 1 + f) once the top phase is published: their levels,
+//                     then their split counts and DFS ranks
+//   2 rtx_anim_out    kOutGroups workgroups per mesh: the reference's numbering, the node
+//                   array, node records, triangle records and permuted state; workgroup 0
+//                   also the split-rendering frontier and the status words
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,12 +25,14 @@
 
 namespace rtxa {
 
-constexpr int kAnimThreads = 512;                // one workgroup per mesh
+constexpr int kAnimThreads = 1024;               // threads of every build workgroup
 constexpr int kAnimWaves = kAnimThreads / 64;
 constexpr int kMaxAnimMeshes = 8;                // animated meshes per launch
 constexpr int kMaxAnimParts = 128;               // frontier entries per mesh (kPartsPerMesh)
-constexpr int kLdsBytesPerTri = 50;              // 9 build floats, 2 permutation words, 3 16-bit ranks
-constexpr int kLdsTris = 3136;                   // meshes up to this size build from LDS (153 KB + 3.6 KB static)
+constexpr int kSubTarget = 16;                   // the top phase stops at a level this wide
+constexpr int kMaxSub = 2 * kSubTarget;          // subtrees per mesh (a level of < 16 nodes doubles at most)
+constexpr int kMaxTop = 4 * kSubTarget;          // top-phase nodes per mesh (< 2 x 16 per level, few levels)
+constexpr int kOutGroups = 16;                   // workgroups per mesh of the output launch
 
 // A node of the build tree before the reference's numbering (64 B).
 struct alignas(16) TmpNode {
@@ -31,9 +41,18 @@ struct alignas(16) TmpNode {
     int32_t l;                   // left child's temp id (right = l + 1); -1: leaf
     uint32_t depth;
     uint32_t splits;             // split nodes in the subtree, itself included
-    uint32_t rank;               // DFS preorder rank among the split nodes
-    uint32_t ref;                // index in the reference's node array
-    uint32_t pad[3];
+    uint32_t rank;               // DFS preorder rank among the split nodes (relative to its subtree root)
+    int32_t parent;              // -1 for the root
+    uint32_t sub;                // subtree index (kMaxSub: a top-phase node)
+    uint32_t pad[2];
+};
+
+// Per-subtree record written by the top phase and completed by the subtree build.
+struct SubRec {
+    uint32_t root;               // temp id of the subtree root (a node of the top phase's last level)
+    uint32_t base;               // first temp id of its descendants (2 n - 2 slots reserved)
+    uint32_t nalloc;             // descendants allocated
+    uint32_t maxd;               // deepest level reached (absolute depth)
 };
 
 struct MeshDev {
@@ -43,17 +62,16 @@ struct MeshDev {
     float4* nrm[2];              // object-space normals in that order (state), T
     float4* tnrm;                // transformedNormals in the input order, T
     float4* tnrm_out;            // transformedNormals in the built order, T
-    // Build arrays by triangle id (input order) and the two permutation buffers; used in
-    // place of the workgroup's LDS copy when the mesh is too large for it (kLdsTris)
-    float* soa;                  // 9 T floats: centroid x, y, z, box lo x, y, z, box hi x, y, z
+    float* soa;                  // build records by triangle id: 9 T floats (centroid xyz, box lo xyz, box hi xyz)
     uint32_t* perm[2];           // build position -> triangle id, T each
     uint32_t* lb;                // partition scratch: left-stream wrong-side positions by rank, T
     uint32_t* rs;                // right-stream ones by rank, T
     uint32_t* rk;                // rank of each position, T
     TmpNode* tmp;                // 2T
-    uint32_t* lvl[8];            // node lists per size class (rtx_anim.hip) x current / next level, T each
+    uint32_t* lvl[2];            // level lists (current / next), T each; a subtree uses [first, first + n)
+    SubRec* sub;                 // kMaxSub
     rtx_bvh_node* ref;           // the reference's node array (3T entries, persistent)
-    uint32_t* status;            // {error bits, deepest level, nodesUsed, frontier parts}
+    uint32_t* status;            // {error bits, deepest level, nodesUsed, frontier parts, ...} + stamps
     uint32_t V, T;
     uint32_t mat_bits;           // material index (the triangle record's 4th float4)
     uint32_t mesh;               // mesh index in the scene
@@ -61,6 +79,13 @@ struct MeshDev {
     uint32_t root;               // root node slot (odd) in the scene image
     uint32_t part0, part_cap;    // frontier entries of the mesh in the scene image
 };
+
+// status words: 0 error bits, 1 deepest level, 2 nodesUsed, 3 frontier parts, 4 subtrees,
+// 5 top-phase nodes, 6 top-phase levels, 7 the epoch of the last published top phase; 8.. phase stamps (s_memrealtime, 100 MHz, low 32 bits):
+// 8 top start, 9 set-up done, 10 top levels done, 11 first subtree start, 12 last subtree end,
+// 13 output start, 14 numbering known (workgroup 0), 15 frontier done, 16 last output end
+enum : uint32_t { kStTop0 = 8, kStSetup = 9, kStTopDone = 10, kStSub0 = 11, kStSubEnd = 12, kStOut0 = 13,
+                  kStRanks = 14, kStFrontier = 15, kStOutEnd = 16 };
 
 struct Image {                   // sections of the destination scene image
     int4* meshes;                // mesh records {root byte offset, nodesUsed, cull, material}
@@ -76,14 +101,17 @@ struct Launch {
     uint32_t cur;                // state buffer (idx / nrm) holding the current order
     float m[kMaxAnimMeshes][12]; // finalTransform: rows data[0..3], xyz each (Matrix.cpp:35-56)
     Image img;
-    uint32_t lds_bytes;          // dynamic LDS per workgroup (meshes that fit build from it)
     // A rebuilt tree this many levels deep or deeper would overflow the render kernel's
     // kStackDepth-entry DFS stack: the build then disables the mesh in the image (node count
     // 0, no frontier parts) and reports kErrDepth.  rtxd::kStackDepth; lower only in tests.
     uint32_t depth_limit;
+    uint32_t top_lds;            // meshes up to this many triangles run the top phase from LDS (0: none)
+    uint32_t sub_lds;            // subtrees build from LDS when they fit (0: always from HBM)
+    uint32_t epoch;              // this update's number (> 0): the top phase publishes it in status[7]
 };
+constexpr uint32_t kTopLdsTris = 3136;   // the largest top_lds (rtx_anim.hip's LDS budget)
 
-enum : uint32_t { kErrNaN = 1u, kErrDepth = 2u };
+enum : uint32_t { kErrNaN = 1u, kErrDepth = 2u, kErrTimeout = 4u };
 
 hipError_t launch_build(const Launch& L, hipStream_t stream);
 

@@ -1,23 +1,33 @@
 // rtx_anim.hip — Scene::Update for animated meshes on the device (see rtx_anim.h).
 //
-// One 1024-thread workgroup per mesh.  The build tree is grown level by level (one barrier
-// per level); each node of a level is handled by one wave:
-//   * FindBestSplitPlane (DataTypes.h:398-483): centroid bounds, 8 bins per live axis, the
-//     7-plane SAH sweep with the reference's float expressions and quirks (0.3333f
-//     centroids, centroid max starting at FLT_MIN, 0 * inf = NaN costs for empty sides);
-//   * the partition (DataTypes.h:343-363) as a parallel scatter that lands every triangle
-//     exactly where the serial swap loop leaves it (derivation below);
-//   * UpdateNodeBounds (:310-321) of both children.
-// Every min/max is a fold in the reference's order: each lane folds a contiguous chunk
-// in order and lanes are combined left to right, so std::min / std::max's "first
-// occurrence wins a tie" is kept (only a signed zero can observe it).  The tree is then
-// numbered as the reference's recursion allocates it (children pairs in DFS preorder of the
-// splits), and the mesh is written into the scene image in rtx_upload_scene's layout.
+// The reference rebuilds each turning mesh's BVH top-down by binned SAH (DataTypes.h:294-483):
+// per node, the centroid bounds, 8 bins per live axis, the 7-plane sweep, the in-place swap
+// partition and UpdateNodeBounds of both children.  Here the tree is grown level by level by
+// TEAMS of waves (a node per team; 16, 8, 4, 2 waves while a level is narrow, one wave per node
+// once it is wide), first for the top levels of every mesh (launch 1, one workgroup per mesh),
+// then for each of the top phase's last-level nodes as an independent subtree (launch 2, one
+// workgroup per subtree, so the build spreads over as many CUs as there are subtrees).
+//
+// Exactness of the folds.  The reference folds with std::min / std::max from FLT_MAX /
+// FLT_MIN, keeping the first of equal values; only a signed zero can observe that order.
+//   * Bins and centroid bounds feed only the SAH decision: bin boxes enter through
+//     AABB::Area = products of (max - min) with max >= FLT_MIN > 0, where (max - (+0)) and
+//     (max - (-0)) are the same number, and the centroid minimum through (c - min) and
+//     min + step (i + 1), equally blind to the zero's sign.  So they are folded in any order
+//     (LDS float atomics, wave reductions): the same VALUES, hence the same decisions.
+//   * Node bounds are written to the node array, so their minima keep the reference's first
+//     occurrence exactly: an LDS atomic minimum over 64-bit keys (value order with -0 read as
+//     +0, then the fold position, the sign riding in the low bit).  Maxima start at FLT_MIN
+//     and can never be a zero: any order.
+//   * The partition is the swap loop's closed form (derivation at team_ranks), a scatter.
+// Launch 3 numbers the tree as the reference's recursion allocates it (children pairs in DFS
+// preorder of the splits) and writes the node array, the render layout and the state.
 // Built with the render library's flags (-ffp-contract=off, correctly rounded div/sqrt).
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
 #include <cstdint>
+#include <algorithm>
 #include <type_traits>
 
 #include "rtx_anim.h"
@@ -29,6 +39,7 @@ namespace {
 __device__ __forceinline__ float rmin(float m, float x) { return (x < m) ? x : m; }   // std::min(m, x)
 __device__ __forceinline__ float rmax(float m, float x) { return (m < x) ? x : m; }   // std::max(m, x)
 __device__ __forceinline__ float fbits(uint32_t u) { return __uint_as_float(u); }
+__device__ __forceinline__ uint32_t stamp() { return static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()); }
 
 // Matrix::TransformPoint / TransformVector (Matrix.cpp:35-56), m = rows data[0..3] (xyz):
 // left-to-right sums of products, no contraction.
@@ -44,252 +55,143 @@ __device__ __forceinline__ float3 normalized(float3 v) {   // Vector3::Normalize
     const float m = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
     return make_float3(v.x / m, v.y / m, v.z / m);
 }
-__device__ __forceinline__ float area(const float lo[3], const float hi[3]) {   // AABB::Area
-    const float ex = hi[0] - lo[0], ey = hi[1] - lo[1], ez = hi[2] - lo[2];
+__device__ __forceinline__ float area(float lx, float ly, float lz, float hx, float hy, float hz) {   // AABB::Area
+    const float ex = hx - lx, ey = hy - ly, ez = hz - lz;
     return ex * ey + ey * ez + ez * ex;
 }
 
-// The build arrays by triangle id and the two permutation buffers, in the workgroup's LDS
-// (meshes up to kLdsTris triangles) or in HBM (MeshDev::soa / perm): generic pointers.
-template <class S>   // S: the partition scratch type (16-bit in LDS, 32-bit in HBM)
-struct Arr {
-    float *cx, *cy, *cz;         // centroid (v0 + v1 + v2) * 0.3333f
-    float *lx, *ly, *lz;         // triangle box min(min(v0, v1), v2)
-    float *hx, *hy, *hz;         //              max(max(v0, v1), v2)
-    uint32_t* perm[2];           // build position -> triangle id
-    S *lb, *rs, *rk;             // partition scratch: left bigs / right smalls by rank, rank by position
-    __device__ float c(int ax, uint32_t id) const { return ax == 0 ? cx[id] : (ax == 1 ? cy[id] : cz[id]); }
-};
-
-struct Bounds {
-    float l0 = FLT_MAX, l1 = FLT_MAX, l2 = FLT_MAX, h0 = FLT_MIN, h1 = FLT_MIN, h2 = FLT_MIN;
-    template <class AR>
-    __device__ void grow(const AR& A, uint32_t id) {   // UpdateNodeBounds over one triangle
-        l0 = rmin(l0, A.lx[id]); l1 = rmin(l1, A.ly[id]); l2 = rmin(l2, A.lz[id]);
-        h0 = rmax(h0, A.hx[id]); h1 = rmax(h1, A.hy[id]); h2 = rmax(h2, A.hz[id]);
-    }
-    __device__ void store(float mn[3], float mx[3]) const {
-        mn[0] = l0; mn[1] = l1; mn[2] = l2; mx[0] = h0; mx[1] = h1; mx[2] = h2;
-    }
-};
-
-// A team: G consecutive lanes of one wave handle one node (G = 64: the whole wave; G = 16:
-// one DPP row, four nodes per wave).  Control flow is uniform within a team (trip counts
-// depend only on the node), so team reductions and ballots see every lane of the team.
-template <int G>
-struct Team {
-    static_assert(G == 16 || G == 64, "teams are DPP rows or whole waves");
-    uint32_t tl, tb;   // lane within the team, the team's first lane in the wave
-    __device__ explicit Team(uint32_t lane) : tl(lane % G), tb(lane - lane % G) {}
-    __device__ unsigned long long ballot(bool p) const {
-        const unsigned long long b = __ballot(p);
-        return G == 64 ? b : (b >> tb) & ((1ull << G) - 1ull);
-    }
-    __device__ uint32_t below(unsigned long long m) const { return __popcll(m & ((1ull << tl) - 1ull)); }
-    // contiguous chunk [s, e) of positions [a, a + n) for this lane: folds stay in order
-    __device__ void chunk(uint32_t a, uint32_t n, uint32_t& s, uint32_t& e) const {
-        const uint32_t c = (n + G - 1u) / G;
-        s = a + min(n, tl * c);
-        e = a + min(n, tl * c + c);
-    }
-};
-
-// In-order team folds without LDS round trips: DPP row_shl:n (lane i reads lane i + n of its
-// row; a source beyond the row yields the fold identity) halves the row in four steps, lane 16r
-// ending with the in-order fold of row r; rows are combined in order from v_readlane values
-// (G = 64) or the row fold is broadcast with row_newbcast:0 (G = 16).  Every result is the
-// team's fold, in every lane of the team.
-template <int N>
-__device__ __forceinline__ uint32_t dpp_shl(uint32_t v, uint32_t identity) {
-    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(identity), static_cast<int>(v),
-                                                             0x100 + N, 0xf, 0xf, false));
-}
-__device__ __forceinline__ uint32_t dpp_row_bcast0(uint32_t v) {
-    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x150, 0xf, 0xf, false));
-}
-struct OpMin {
-    static constexpr float kId = FLT_MAX;
-    __device__ static float f(float m, float x) { return rmin(m, x); }
-};
-struct OpMax {
-    static constexpr float kId = FLT_MIN;
-    __device__ static float f(float m, float x) { return rmax(m, x); }
-};
-template <int G, class Op>
-__device__ __forceinline__ float team_fold(float v) {
-    const uint32_t id = __float_as_uint(Op::kId);
-    v = Op::f(v, __uint_as_float(dpp_shl<1>(__float_as_uint(v), id)));
-    v = Op::f(v, __uint_as_float(dpp_shl<2>(__float_as_uint(v), id)));
-    v = Op::f(v, __uint_as_float(dpp_shl<4>(__float_as_uint(v), id)));
-    v = Op::f(v, __uint_as_float(dpp_shl<8>(__float_as_uint(v), id)));
-    if (G == 16) return __uint_as_float(dpp_row_bcast0(__float_as_uint(v)));
+// ---- keys of the first-occurrence minimum (node bounds)
+__device__ __forceinline__ uint32_t ord(float v) {   // order-preserving bits of a non-NaN float
     const uint32_t u = __float_as_uint(v);
-    const float r0 = __uint_as_float(__builtin_amdgcn_readlane(u, 0)), r1 = __uint_as_float(__builtin_amdgcn_readlane(u, 16));
-    const float r2 = __uint_as_float(__builtin_amdgcn_readlane(u, 32)), r3 = __uint_as_float(__builtin_amdgcn_readlane(u, 48));
-    return Op::f(Op::f(Op::f(r0, r1), r2), r3);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
-template <int G>
-__device__ __forceinline__ uint32_t team_sum(uint32_t v) {
-    v += dpp_shl<1>(v, 0u);
-    v += dpp_shl<2>(v, 0u);
-    v += dpp_shl<4>(v, 0u);
-    v += dpp_shl<8>(v, 0u);
-    if (G == 16) return dpp_row_bcast0(v);
-    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
-           __builtin_amdgcn_readlane(v, 48);
+__device__ __forceinline__ float unord(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
-template <int G>
-__device__ __forceinline__ Bounds team_fold(const Bounds& B) {
-    Bounds R;
-    R.l0 = team_fold<G, OpMin>(B.l0); R.l1 = team_fold<G, OpMin>(B.l1); R.l2 = team_fold<G, OpMin>(B.l2);
-    R.h0 = team_fold<G, OpMax>(B.h0); R.h1 = team_fold<G, OpMax>(B.h1); R.h2 = team_fold<G, OpMax>(B.h2);
-    return R;
+// value (zeros as +0) | fold position | sign: the minimum key is the reference's std::min fold
+// result from FLT_MAX (position 0 = the initial value, element p at 1 + p)
+__device__ __forceinline__ unsigned long long min_key(float v, uint32_t pos) {
+    const float c = (v == 0.f) ? 0.f : v;
+    return (static_cast<unsigned long long>(ord(c)) << 32) | (pos << 1) | (__float_as_uint(v) >> 31);
+}
+__device__ __forceinline__ float min_key_value(unsigned long long k) {
+    const float v = unord(static_cast<uint32_t>(k >> 32));
+    return (v == 0.f && (k & 1ull)) ? -0.f : v;
+}
+__device__ __forceinline__ unsigned long long min_key_init() { return min_key(FLT_MAX, 0u); }
+
+// ---- order-free wave reductions (values only, see the header)
+__device__ __forceinline__ float wave_minf(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_min64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t lo = __shfl_xor(static_cast<uint32_t>(v), o), hi = __shfl_xor(static_cast<uint32_t>(v >> 32), o);
+        const unsigned long long w = (static_cast<unsigned long long>(hi) << 32) | lo;
+        v = w < v ? w : v;
+    }
+    return v;
 }
 
-// Bounds of the triangle boxes at build positions [a, b) (UpdateNodeBounds: a triangle's box
-// min(min(v0, v1), v2) grows a node exactly as its three vertices in order do), every lane.
-template <int G, class AR>
-__device__ __forceinline__ Bounds team_bounds(const Team<G>& tm, const AR& A, const uint32_t* perm, uint32_t a,
-                                              uint32_t b) {
-    Bounds B;
-    uint32_t s, e;
-    tm.chunk(a, b - a, s, e);
-#pragma unroll 4
-    for (uint32_t k = s; k < e; ++k) B.grow(A, perm[k]);
-    return team_fold<G>(B);
+// Order-free wave reductions through DPP row shifts (lanes outside the row keep the identity)
+// and the four row results read back in order: about 11 instructions per value.
+template <int N>
+__device__ __forceinline__ uint32_t dpp_shr(uint32_t v, uint32_t identity) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(identity), static_cast<int>(v),
+                                                             0x110 + N, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_minf(float v) {
+    const uint32_t id = __float_as_uint(FLT_MAX);
+    v = fminf(v, __uint_as_float(dpp_shr<1>(__float_as_uint(v), id)));
+    v = fminf(v, __uint_as_float(dpp_shr<2>(__float_as_uint(v), id)));
+    v = fminf(v, __uint_as_float(dpp_shr<4>(__float_as_uint(v), id)));
+    v = fminf(v, __uint_as_float(dpp_shr<8>(__float_as_uint(v), id)));
+    const uint32_t u = __float_as_uint(v);
+    return fminf(fminf(__uint_as_float(__builtin_amdgcn_readlane(u, 15)), __uint_as_float(__builtin_amdgcn_readlane(u, 31))),
+                 fminf(__uint_as_float(__builtin_amdgcn_readlane(u, 47)), __uint_as_float(__builtin_amdgcn_readlane(u, 63))));
+}
+__device__ __forceinline__ float dpp_maxf(float v) {
+    const uint32_t id = __float_as_uint(FLT_MIN);
+    v = fmaxf(v, __uint_as_float(dpp_shr<1>(__float_as_uint(v), id)));
+    v = fmaxf(v, __uint_as_float(dpp_shr<2>(__float_as_uint(v), id)));
+    v = fmaxf(v, __uint_as_float(dpp_shr<4>(__float_as_uint(v), id)));
+    v = fmaxf(v, __uint_as_float(dpp_shr<8>(__float_as_uint(v), id)));
+    const uint32_t u = __float_as_uint(v);
+    return fmaxf(fmaxf(__uint_as_float(__builtin_amdgcn_readlane(u, 15)), __uint_as_float(__builtin_amdgcn_readlane(u, 31))),
+                 fmaxf(__uint_as_float(__builtin_amdgcn_readlane(u, 47)), __uint_as_float(__builtin_amdgcn_readlane(u, 63))));
+}
+__device__ __forceinline__ uint32_t dpp_sum(uint32_t v) {
+    v += dpp_shr<1>(v, 0u);
+    v += dpp_shr<2>(v, 0u);
+    v += dpp_shr<4>(v, 0u);
+    v += dpp_shr<8>(v, 0u);
+    return __builtin_amdgcn_readlane(v, 15) + __builtin_amdgcn_readlane(v, 31) + __builtin_amdgcn_readlane(v, 47) +
+           __builtin_amdgcn_readlane(v, 63);
 }
 
+// The build records and permutation of a build region.  Records: centroid (v0 + v1 + v2) *
+// 0.3333f and the triangle box min(min(v0, v1), v2) / max(max(v0, v1), v2) — growing a node or
+// bin by the box equals growing it by the three vertices in order (first occurrence
+// included) — as 9 arrays of `stride` floats by element index.  LDS = true: the region's
+// records, permutation buffers and partition scratch are staged in the workgroup's LDS
+// (16-bit indices, element = local index, positions relative to pos0); false: HBM
+// (MeshDev::soa / perm / lb / rs / rk, element = triangle id, absolute positions).
+template <bool LDS>
+struct Store {
+    using P = std::conditional_t<LDS, uint16_t, uint32_t>;
+    P* perm[2];
+    P *lb, *rs, *rk;
+    const float* rec;
+    uint32_t stride, pos0;
+    __device__ float c(int ax, uint32_t e) const { return rec[ax * stride + e]; }
+    __device__ float lo(int ax, uint32_t e) const { return rec[(3 + ax) * stride + e]; }
+    __device__ float hi(int ax, uint32_t e) const { return rec[(6 + ax) * stride + e]; }
+};
+constexpr uint32_t kLdsBytesTop = 46;    // per element: 9 record floats, 2 + 3 16-bit words
+constexpr uint32_t kLdsBytesSub = 50;    // + the element's triangle id
+constexpr uint32_t kTopLdsMax = kTopLdsTris;   // meshes up to this size run the top phase from LDS
+constexpr uint32_t kSubLdsMax = 2816;    // subtrees up to this size build from LDS
+
+#ifndef RTX_ANIM_STEP_STAMPS
+#define RTX_ANIM_STEP_STAMPS 0   // diagnostics: the root node's step times in status[64..72]
+#endif
 constexpr int kBins = 8, kPlanes = kBins - 1;
 
-// One axis's 8 bins: idxCount and the box of the triangles' vertices, folded in order.
-struct Bins {
-    float bl[kBins][3], bh[kBins][3];
-    uint32_t bc[kBins];
-    __device__ void clear() {
-#pragma unroll
-        for (int q = 0; q < kBins; ++q) {
-            bl[q][0] = bl[q][1] = bl[q][2] = FLT_MAX;
-            bh[q][0] = bh[q][1] = bh[q][2] = FLT_MIN;
-            bc[q] = 0u;
-        }
-    }
-    template <class AR>
-    __device__ void add(const AR& A, uint32_t id, int ax, float minBounds, float scale) {
-        const float x = (A.c(ax, id) - minBounds) * scale;
-        // static_cast<int> of x >= 0 (a NaN x only comes from a NaN vertex: flagged, bin 0)
-        int bi = x >= 0.f ? static_cast<int>(fminf(x, 2147483520.f)) : 0;
-        bi = kPlanes < bi ? kPlanes : bi;   // std::min(amountOfPlaneBins, binIdx)
-        const float lx = A.lx[id], ly = A.ly[id], lz = A.lz[id], hx = A.hx[id], hy = A.hy[id], hz = A.hz[id];
-        // branch-free: the other bins see their fold identity (FLT_MAX for a min that starts at
-        // FLT_MAX, FLT_MIN for a max that starts at FLT_MIN), which leaves them bit-unchanged;
-        // per-bin branches get merged into a pointer select and the bins into scratch memory
-#pragma unroll
-        for (int q = 0; q < kBins; ++q) {
-            const bool h = bi == q;
-            bc[q] += h ? 3u : 0u;
-            bl[q][0] = rmin(bl[q][0], h ? lx : FLT_MAX);
-            bl[q][1] = rmin(bl[q][1], h ? ly : FLT_MAX);
-            bl[q][2] = rmin(bl[q][2], h ? lz : FLT_MAX);
-            bh[q][0] = rmax(bh[q][0], h ? hx : FLT_MIN);
-            bh[q][1] = rmax(bh[q][1], h ? hy : FLT_MIN);
-            bh[q][2] = rmax(bh[q][2], h ? hz : FLT_MIN);
-        }
-    }
-    // the plane sweep (DataTypes.h:444-480), AABBs starting at {MaxVector, MinVector}
-    __device__ void sweep(int ax, float minBounds, float boundsDifference, float& bestCost, int& axis,
-                          float& pos) const {
-        float leftArea[kPlanes], rightArea[kPlanes];
-        int leftCount[kPlanes], rightCount[kPlanes];
-        int leftSum = 0, rightSum = 0;
-        float llo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, lhi[3] = {FLT_MIN, FLT_MIN, FLT_MIN};
-        float rlo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, rhi[3] = {FLT_MIN, FLT_MIN, FLT_MIN};
-#pragma unroll
-        for (int i = 0; i < kPlanes; ++i) {
-            leftSum += static_cast<int>(bc[i]);
-            leftCount[i] = leftSum;
-            #pragma unroll
-            for (int c = 0; c < 3; ++c) { llo[c] = rmin(llo[c], bl[i][c]); lhi[c] = rmax(lhi[c], bh[i][c]); }
-            leftArea[i] = area(llo, lhi);
-            rightSum += static_cast<int>(bc[kPlanes - i]);
-            rightCount[kPlanes - i - 1] = rightSum;
-            #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                rlo[c] = rmin(rlo[c], bl[kPlanes - i][c]);
-                rhi[c] = rmax(rhi[c], bh[kPlanes - i][c]);
-            }
-            rightArea[kPlanes - i - 1] = area(rlo, rhi);
-        }
-        const float step = boundsDifference / kBins;
-#pragma unroll
-        for (int i = 0; i < kPlanes; ++i) {
-            const float planeCost = static_cast<float>(leftCount[i]) * leftArea[i] +
-                                    static_cast<float>(rightCount[i]) * rightArea[i];
-            if (planeCost < bestCost) {
-                axis = ax;
-                pos = minBounds + step * static_cast<float>(i + 1);
-                bestCost = planeCost;
-            }
-        }
-    }
+// Per-team LDS scratch (one node at a time per team).
+struct Slot {
+    float cb[6];                         // centroid bounds: min xyz, max xyz
+    uint32_t bc[3][kBins];               // idxCount per axis and bin
+    float bl[3][kBins][3], bh[3][kBins][3];
+    unsigned long long cmin[2][3];       // children's node bounds (keys) and maxima
+    float cmax[2][3];
+    uint32_t wc[kAnimWaves][3];          // per-wave partition counts: smalls, left bigs, right smalls
 };
 
-// Centroid bounds of positions [a, b): min from FLT_MAX, max from FLT_MIN (the reference's
-// minBounds / maxBounds, DataTypes.h:404-419), the three axes in one fold, every lane.
-template <int G, class AR>
-__device__ __forceinline__ Bounds team_centroid_bounds(const Team<G>& tm, const AR& A, const uint32_t* perm,
-                                                       uint32_t a, uint32_t b) {
-    Bounds C;
-    uint32_t s, e;
-    tm.chunk(a, b - a, s, e);
-#pragma unroll 4
-    for (uint32_t k = s; k < e; ++k) {
-        const uint32_t id = perm[k];
-        const float x = A.cx[id], y = A.cy[id], z = A.cz[id];
-        C.l0 = rmin(C.l0, x); C.l1 = rmin(C.l1, y); C.l2 = rmin(C.l2, z);
-        C.h0 = rmax(C.h0, x); C.h1 = rmax(C.h1, y); C.h2 = rmax(C.h2, z);
-    }
-    return team_fold<G>(C);
-}
+// Shared state of one workgroup's level loop.
+struct Level {
+    uint32_t K, next, take, maxn, nmaxn;   // nodes this level, appended next-level nodes, wave-task counter, max counts
+    uint32_t ids;                          // next temp id
+    uint32_t err;
+};
 
-// One axis's bins over positions [a, b), every lane.
-template <int G, class AR>
-__device__ __forceinline__ void team_bins(const Team<G>& tm, const AR& A, const uint32_t* perm, uint32_t a,
-                                          uint32_t b, int ax, float minBounds, float scale, Bins& bins) {
-    bins.clear();
-    uint32_t s, e;
-    tm.chunk(a, b - a, s, e);
-#pragma unroll 2
-    for (uint32_t k = s; k < e; ++k) bins.add(A, perm[k], ax, minBounds, scale);
-#pragma unroll
-    for (int q = 0; q < kBins; ++q) {
-        bins.bc[q] = team_sum<G>(bins.bc[q]);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            bins.bl[q][c] = team_fold<G, OpMin>(bins.bl[q][c]);
-            bins.bh[q][c] = team_fold<G, OpMax>(bins.bh[q][c]);
-        }
-    }
-}
+// The level lists of a build region (a mesh for the top phase, a subtree's range for launch 2).
+struct Region {
+    uint32_t* cur;
+    uint32_t* nxt;
+};
 
-// FindBestSplitPlane (DataTypes.h:398-483) for the node at [a, a + n) by one team: the best
-// cost (FLT_MAX when no axis is live) with axis / pos, uniform over the team.
-template <int G, class AR>
-__device__ __forceinline__ float team_best_split(const Team<G>& tm, const AR& A, const uint32_t* perm, uint32_t a,
-                                                 uint32_t n, int& axis, float& pos) {
-    const Bounds C = team_centroid_bounds(tm, A, perm, a, a + n);
-    const float cl[3] = {C.l0, C.l1, C.l2}, ch[3] = {C.h0, C.h1, C.h2};
-    float bestCost = FLT_MAX;
-#pragma unroll
-    for (int ax = 0; ax < 3; ++ax) {
-        const float minBounds = cl[ax];
-        const float boundsDifference = ch[ax] - minBounds;
-        if (fabsf(boundsDifference) < FLT_EPSILON) continue;
-        Bins bins;
-        team_bins(tm, A, perm, a, a + n, ax, minBounds, kBins / boundsDifference, bins);
-        bins.sweep(ax, minBounds, boundsDifference, bestCost, axis, pos);   // the same in every lane
-    }
-    return bestCost;
-}
+// A team: waves [w0, w0 + k) of the workgroup; lanes tl in [0, 64 k).
+struct Team {
+    uint32_t k, w0, wt, tl, lane;
+};
 
 // The serial swap loop (DataTypes.h:343-363, in triangle units) on a node of n triangles
 // with flags big(q) = !(centroid[axis] < splitPos) examines the left stream q = 0, 1, ...
@@ -301,396 +203,452 @@ __device__ __forceinline__ float team_best_split(const Team<G>& tm, const AR& A,
 //   m-th big q < pL         -> n-1 (m = 0) or (position of the (m-1)-th right small) - 1
 //   m-th small p >= pL      -> position of the m-th left big   (right smalls counted from the end)
 //   big p >= pL             -> p - 1
-// The ranks of positions [lo, hi) are assigned with the rank bases lbase / rbase (the counts
-// of left bigs before lo / right smalls after hi): one team, or one wave of a workgroup.
-template <int G, class AR>
-__device__ __forceinline__ void team_ranks(const Team<G>& tm, const AR& A, const uint32_t* src, const MeshDev& M,
-                                           uint32_t first, uint32_t lo, uint32_t hi, uint32_t pL, int axis,
-                                           float pos, uint32_t lbase, uint32_t rbase) {
-    auto small = [&](uint32_t q) { return A.c(axis, src[first + q]) < pos; };
+// One wave assigns the ranks of positions [lo, hi) (relative to the node's local first f0),
+// given the rank bases lbase / rbase (the counts of left bigs before lo / right smalls after hi).
+template <bool LDS>
+__device__ __forceinline__ void wave_ranks(const Store<LDS>& St, const typename Store<LDS>::P* src, uint32_t lane,
+                                           uint32_t f0, uint32_t lo, uint32_t hi, uint32_t pL, int axis, float pos,
+                                           uint32_t lbase, uint32_t rbase) {
+    using P = typename Store<LDS>::P;
+    auto small = [&](uint32_t q) { return St.c(axis, src[f0 + q]) < pos; };
+    const unsigned long long below = (1ull << lane) - 1ull;
     uint32_t carry = lbase;
     const uint32_t lhi = min(hi, pL);
-    for (uint32_t base = lo; base < lhi; base += G) {   // left-stream bigs, in order
-        const uint32_t q = base + tm.tl;
+    for (uint32_t base = lo; base < lhi; base += 64u) {   // left-stream bigs, in order
+        const uint32_t q = base + lane;
         const bool b = q < lhi && !small(q);
-        const unsigned long long m = tm.ballot(b);
+        const unsigned long long m = __ballot(b);
         if (b) {
-            const uint32_t r = carry + tm.below(m);
-            A.lb[first + r] = q;
-            A.rk[first + q] = r;
+            const uint32_t r = carry + __popcll(m & below);
+            St.lb[f0 + r] = static_cast<P>(q);
+            St.rk[f0 + q] = static_cast<P>(r);
         }
         carry += __popcll(m);
     }
     carry = rbase;
     const uint32_t rlo = max(lo, pL);
     for (uint32_t top = hi; top > rlo;) {   // right-stream smalls, from the end
-        const uint32_t cnt = min(static_cast<uint32_t>(G), top - rlo);
-        const bool in = tm.tl < cnt;
-        const uint32_t p = in ? top - 1u - tm.tl : 0u;
+        const uint32_t cnt = min(64u, top - rlo);
+        const bool in = lane < cnt;
+        const uint32_t p = in ? top - 1u - lane : 0u;
         const bool sm = in && small(p);
-        const unsigned long long m = tm.ballot(sm);
+        const unsigned long long m = __ballot(sm);
         if (sm) {
-            const uint32_t r = carry + tm.below(m);
-            A.rs[first + r] = p;
-            A.rk[first + p] = r;
+            const uint32_t r = carry + __popcll(m & below);
+            St.rs[f0 + r] = static_cast<P>(p);
+            St.rk[f0 + p] = static_cast<P>(r);
         }
         carry += __popcll(m);
         top -= cnt;
     }
 }
 // Destination of position q once every rank is known.
-template <class AR>
-__device__ __forceinline__ uint32_t part_dest(const AR& A, uint32_t first, uint32_t n, uint32_t q, uint32_t pL,
+template <bool LDS>
+__device__ __forceinline__ uint32_t part_dest(const Store<LDS>& St, uint32_t f0, uint32_t n, uint32_t q, uint32_t pL,
                                               bool big) {
     if (q < pL) {
         if (!big) return q;
-        const uint32_t m = A.rk[first + q];
-        return m == 0u ? n - 1u : static_cast<uint32_t>(A.rs[first + m - 1u]) - 1u;
+        const uint32_t m = St.rk[f0 + q];
+        return m == 0u ? n - 1u : static_cast<uint32_t>(St.rs[f0 + m - 1u]) - 1u;
     }
-    return big ? q - 1u : static_cast<uint32_t>(A.lb[first + A.rk[first + q]]);
-}
-template <int G, class AR>
-__device__ __forceinline__ uint32_t team_count_small(const Team<G>& tm, const AR& A, const uint32_t* src,
-                                                     uint32_t first, uint32_t lo, uint32_t hi, int axis, float pos) {
-    uint32_t S = 0;
-    for (uint32_t base = lo; base < hi; base += G) {
-        const uint32_t q = base + tm.tl;
-        S += __popcll(tm.ballot(q < hi && A.c(axis, src[first + q]) < pos));
-    }
-    return S;
-}
-template <int G, class AR>
-__device__ __forceinline__ void team_partition(const Team<G>& tm, const AR& A, const uint32_t* src, uint32_t* dst,
-                                               const MeshDev& M, uint32_t first, uint32_t n, int axis, float pos,
-                                               uint32_t& S_out) {
-    const uint32_t S = team_count_small(tm, A, src, first, 0u, n, axis, pos);
-    const uint32_t pL = S + ((S < n && !(A.c(axis, src[first + S]) < pos)) ? 1u : 0u);
-    team_ranks(tm, A, src, M, first, 0u, n, pL, axis, pos, 0u, 0u);
-    __threadfence_block();
-    for (uint32_t q = tm.tl; q < n; q += G) {
-        const uint32_t id = src[first + q];
-        dst[first + part_dest(A, first, n, q, pL, !(A.c(axis, id) < pos))] = id;
-    }
-    __threadfence_block();
-    S_out = S;
+    return big ? q - 1u : static_cast<uint32_t>(St.lb[f0 + St.rk[f0 + q]]);
 }
 
-template <int G>
-__device__ __forceinline__ void team_copy(const Team<G>& tm, const uint32_t* src, uint32_t* dst, uint32_t first,
-                                          uint32_t n) {
-    for (uint32_t q = tm.tl; q < n; q += G) dst[first + q] = src[first + q];
-    __threadfence_block();
+// Team synchronisation: a workgroup barrier for multi-wave teams (every wave of the workgroup
+// runs the same sequence of barriers), else the wave's own memory ordering.
+template <bool MULTI>
+__device__ __forceinline__ void tsync() {
+    if (MULTI) {
+        __syncthreads();
+    } else {
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
-// Node classes by size: huge nodes are processed by the whole workgroup one at a time, large
-// ones by a wave, small ones by a 16-lane row, tiny ones by one lane each (a large node of up
-// to 2,048 triangles folds up to 32 positions per lane: waves working on different nodes side
-// by side beat the serial whole-workgroup path there).
-#ifndef RTX_ANIM_HUGE
-#define RTX_ANIM_HUGE 2048   // above this a node takes the whole workgroup (512 measured 15 % slower)
-#endif
-constexpr uint32_t kHugeNode = RTX_ANIM_HUGE, kLargeNode = 64, kTinyNode = 8;
-__device__ __forceinline__ uint32_t node_class(uint32_t n) {
-    return n > kHugeNode ? 0u : (n > kLargeNode ? 1u : (n > kTinyNode ? 2u : 3u));
-}
-
-// Shared state of one build (LDS): per class the node count of the current level and the
-// append counter of the next one.
-struct Lists {
-    uint32_t n[4], next[4], ntmp, depth, err;
+// Node bounds over elements in fold order: a lane's private keys / maxima, then the wave's.
+struct BoundAcc {
+    unsigned long long k0 = ~0ull, k1 = ~0ull, k2 = ~0ull;
+    float m0 = FLT_MIN, m1 = FLT_MIN, m2 = FLT_MIN;
+    template <class ST>
+    __device__ void add(const ST& St, uint32_t e, uint32_t r) {   // element e at fold position r (>= 1)
+        const float a0 = St.lo(0, e), a1 = St.lo(1, e), a2 = St.lo(2, e);
+        if (a0 == a0) { const unsigned long long k = min_key(a0, r); k0 = k < k0 ? k : k0; }
+        if (a1 == a1) { const unsigned long long k = min_key(a1, r); k1 = k < k1 ? k : k1; }
+        if (a2 == a2) { const unsigned long long k = min_key(a2, r); k2 = k < k2 ? k : k2; }
+        m0 = fmaxf(m0, St.hi(0, e)); m1 = fmaxf(m1, St.hi(1, e)); m2 = fmaxf(m2, St.hi(2, e));
+    }
+    __device__ void wave() {
+        k0 = wave_min64(k0); k1 = wave_min64(k1); k2 = wave_min64(k2);
+        m0 = wave_maxf(m0); m1 = wave_maxf(m1); m2 = wave_maxf(m2);
+    }
+    // into the slot's child c: atomics (several waves) or a plain store (one wave)
+    __device__ void put(Slot& sl, int c, bool atomic) const {
+        if (atomic) {
+            atomicMin(&sl.cmin[c][0], k0); atomicMin(&sl.cmin[c][1], k1); atomicMin(&sl.cmin[c][2], k2);
+            atomicMax(&sl.cmax[c][0], m0); atomicMax(&sl.cmax[c][1], m1); atomicMax(&sl.cmax[c][2], m2);
+        } else {
+            const unsigned long long i = min_key_init();
+            sl.cmin[c][0] = k0 < i ? k0 : i; sl.cmin[c][1] = k1 < i ? k1 : i; sl.cmin[c][2] = k2 < i ? k2 : i;
+            sl.cmax[c][0] = m0; sl.cmax[c][1] = m1; sl.cmax[c][2] = m2;
+        }
+    }
 };
 
-// Children of a split node: temp ids, and entries in the next level's list of their class.
-__device__ __forceinline__ void add_children(const MeshDev& M, Lists& Ls, uint32_t cl, uint32_t t, uint32_t first,
-                                             uint32_t n, uint32_t S, uint32_t depth, const float lmn[3],
-                                             const float lmx[3], const float rmn[3], const float rmx[3]) {
-    const uint32_t c = atomicAdd(&Ls.ntmp, 2u);
-    TmpNode a{}, b{};
-    for (int q = 0; q < 3; ++q) { a.mn[q] = lmn[q]; a.mx[q] = lmx[q]; b.mn[q] = rmn[q]; b.mx[q] = rmx[q]; }
-    a.first = first; a.count = S; a.l = -1; a.depth = depth + 1;
-    b.first = first + S; b.count = n - S; b.l = -1; b.depth = depth + 1;
-    M.tmp[c] = a;
-    M.tmp[c + 1] = b;
-    M.tmp[t].l = static_cast<int32_t>(c);
-    for (uint32_t h = 0; h < 2; ++h) {
-        const uint32_t k = node_class(h ? n - S : S);
-        const uint32_t w = atomicAdd(&Ls.next[k], 1u);
-        M.lvl[2 * k + (cl ^ 1u)][w] = c + h;
-    }
-}
-
-// One node by one team of G lanes (a wave, or a 16-lane row).
-template <int G, class AR>
-__device__ __forceinline__ void team_node(const Team<G>& tm, const AR& A, uint32_t* src, uint32_t* dst,
-                                          const MeshDev& M, Lists& Ls, uint32_t cl, uint32_t t, uint32_t depth) {
-    const TmpNode X = M.tmp[t];
-    const uint32_t n = X.count;
-    int axis = 0;
-    float pos = 0.f;
-    const float splitCost = team_best_split(tm, A, src, X.first, n, axis, pos);
-    const float noSplitCost = static_cast<float>(3u * n) * area(X.mn, X.mx);   // CalculateNodeCost
-    if (splitCost >= noSplitCost) {
-        team_copy(tm, src, dst, X.first, n);
-        return;
-    }
-    uint32_t S = 0;
-    team_partition(tm, A, src, dst, M, X.first, n, axis, pos, S);
-    if (S == 0u || S == n) {   // leftCount 0 or all: a leaf, with the permutation applied
-        team_copy(tm, dst, src, X.first, n);
-        return;
-    }
-    const Bounds Lb = team_bounds(tm, A, dst, X.first, X.first + S);
-    const Bounds Rb = team_bounds(tm, A, dst, X.first + S, X.first + n);
-    if (tm.tl == 0) {
-        float lmn[3], lmx[3], rmn[3], rmx[3];
-        Lb.store(lmn, lmx);
-        Rb.store(rmn, rmx);
-        add_children(M, Ls, cl, t, X.first, n, S, depth, lmn, lmx, rmn, rmx);
-    }
-}
-
-// Workgroup scratch for a node processed by every wave (huge nodes): per-wave partial folds,
-// combined in wave order.
-struct WgScratch {
-    float b[kAnimWaves][6];                    // bounds / centroid bounds
-    float bins[kAnimWaves][kBins * 7];         // one axis's bins: count, lo xyz, hi xyz
-    uint32_t cnt[kAnimWaves][2];
-};
-
-__device__ __forceinline__ void wg_store_bounds(WgScratch& W, uint32_t wave, const Bounds& B) {
-    W.b[wave][0] = B.l0; W.b[wave][1] = B.l1; W.b[wave][2] = B.l2;
-    W.b[wave][3] = B.h0; W.b[wave][4] = B.h1; W.b[wave][5] = B.h2;
-}
-__device__ __forceinline__ Bounds wg_fold_bounds(const WgScratch& W) {   // waves in order
-    Bounds B;
+// One axis's bins over the positions [0, n) a lane visits (tl, tl + nl, ...), folded in
+// registers (branch-free: the other bins see their fold identity), then over the wave (DPP),
+// then into the slot: atomics (several waves) or plain stores (one wave).  Order-free (see
+// the header); used where lanes hold several elements, LDS atomics per element otherwise.
+template <class ST, class PT>
+__device__ __forceinline__ void bins_private(const ST& St, const PT* src, uint32_t f0, uint32_t n, uint32_t tl,
+                                             uint32_t nl, uint32_t lane, int ax, float minB, float scale, Slot& sl,
+                                             bool atomic) {
+    uint32_t bc[kBins];
+    float bl[kBins][3], bh[kBins][3];
 #pragma unroll
-    for (int w = 0; w < kAnimWaves; ++w) {
-        B.l0 = rmin(B.l0, W.b[w][0]); B.l1 = rmin(B.l1, W.b[w][1]); B.l2 = rmin(B.l2, W.b[w][2]);
-        B.h0 = rmax(B.h0, W.b[w][3]); B.h1 = rmax(B.h1, W.b[w][4]); B.h2 = rmax(B.h2, W.b[w][5]);
+    for (int q = 0; q < kBins; ++q) {
+        bc[q] = 0u;
+        bl[q][0] = bl[q][1] = bl[q][2] = FLT_MAX;
+        bh[q][0] = bh[q][1] = bh[q][2] = FLT_MIN;
     }
-    return B;
-}
-
-// One huge node by the whole workgroup: wave w takes the w-th contiguous eighth of the range.
-template <class AR>
-__device__ void wg_node(const AR& A, uint32_t* src, uint32_t* dst, const MeshDev& M, Lists& Ls, WgScratch& W,
-                        uint32_t cl, uint32_t t, uint32_t depth, uint32_t tid) {
-    const uint32_t lane = tid & 63u, wave = tid >> 6;
-    const Team<64> tm(lane);
-    const TmpNode X = M.tmp[t];
-    const uint32_t n = X.count, first = X.first;
-    const uint32_t per = (n + kAnimWaves - 1u) / kAnimWaves;
-    const uint32_t lo = min(n, wave * per), hi = min(n, wave * per + per);   // this wave's eighth
-    // centroid bounds
-    {
-        const Bounds C = team_centroid_bounds(tm, A, src, first + lo, first + hi);
-        if (lane == 0) wg_store_bounds(W, wave, C);
-    }
-    __syncthreads();
-    const Bounds C = wg_fold_bounds(W);
-    const float cl3[3] = {C.l0, C.l1, C.l2}, ch3[3] = {C.h0, C.h1, C.h2};
-    float bestCost = FLT_MAX, pos = 0.f;
-    int axis = 0;
+    for (uint32_t p = tl; p < n; p += nl) {
+        const uint32_t e = src[f0 + p];
+        const float x = (St.c(ax, e) - minB) * scale;
+        int bi = x >= 0.f ? static_cast<int>(fminf(x, 2147483520.f)) : 0;
+        bi = kPlanes < bi ? kPlanes : bi;
+        const float l0 = St.lo(0, e), l1 = St.lo(1, e), l2 = St.lo(2, e);
+        const float h0 = St.hi(0, e), h1 = St.hi(1, e), h2 = St.hi(2, e);
 #pragma unroll
-    for (int ax = 0; ax < 3; ++ax) {
-        const float minBounds = cl3[ax];
-        const float boundsDifference = ch3[ax] - minBounds;
-        if (fabsf(boundsDifference) < FLT_EPSILON) continue;   // uniform
-        Bins bins;
-        team_bins(tm, A, src, first + lo, first + hi, ax, minBounds, kBins / boundsDifference, bins);
-        __syncthreads();   // the previous axis's partials are consumed
+        for (int q = 0; q < kBins; ++q) {
+            const bool h = bi == q;
+            bc[q] += h ? 3u : 0u;
+            bl[q][0] = fminf(bl[q][0], h ? l0 : FLT_MAX);
+            bl[q][1] = fminf(bl[q][1], h ? l1 : FLT_MAX);
+            bl[q][2] = fminf(bl[q][2], h ? l2 : FLT_MAX);
+            bh[q][0] = fmaxf(bh[q][0], h ? h0 : FLT_MIN);
+            bh[q][1] = fmaxf(bh[q][1], h ? h1 : FLT_MIN);
+            bh[q][2] = fmaxf(bh[q][2], h ? h2 : FLT_MIN);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < kBins; ++q) {
+        const uint32_t c = dpp_sum(bc[q]);
+        const float a0 = dpp_minf(bl[q][0]), a1 = dpp_minf(bl[q][1]), a2 = dpp_minf(bl[q][2]);
+        const float b0 = dpp_maxf(bh[q][0]), b1 = dpp_maxf(bh[q][1]), b2 = dpp_maxf(bh[q][2]);
         if (lane == 0) {
-#pragma unroll
-            for (int q = 0; q < kBins; ++q) {
-                W.bins[wave][7 * q] = __uint_as_float(bins.bc[q]);
-#pragma unroll
-                for (int c = 0; c < 3; ++c) { W.bins[wave][7 * q + 1 + c] = bins.bl[q][c]; W.bins[wave][7 * q + 4 + c] = bins.bh[q][c]; }
+            if (atomic) {
+                atomicAdd(&sl.bc[ax][q], c);
+                atomicMin(&sl.bl[ax][q][0], a0); atomicMin(&sl.bl[ax][q][1], a1); atomicMin(&sl.bl[ax][q][2], a2);
+                atomicMax(&sl.bh[ax][q][0], b0); atomicMax(&sl.bh[ax][q][1], b1); atomicMax(&sl.bh[ax][q][2], b2);
+            } else {
+                sl.bc[ax][q] = c;
+                sl.bl[ax][q][0] = a0; sl.bl[ax][q][1] = a1; sl.bl[ax][q][2] = a2;
+                sl.bh[ax][q][0] = b0; sl.bh[ax][q][1] = b1; sl.bh[ax][q][2] = b2;
             }
         }
-        __syncthreads();
-        Bins all;
-        all.clear();
-#pragma unroll
-        for (int w = 0; w < kAnimWaves; ++w) {
-#pragma unroll
-            for (int q = 0; q < kBins; ++q) {
-                all.bc[q] += __float_as_uint(W.bins[w][7 * q]);
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    all.bl[q][c] = rmin(all.bl[q][c], W.bins[w][7 * q + 1 + c]);
-                    all.bh[q][c] = rmax(all.bh[q][c], W.bins[w][7 * q + 4 + c]);
-                }
-            }
-        }
-        all.sweep(ax, minBounds, boundsDifference, bestCost, axis, pos);
     }
-    const float noSplitCost = static_cast<float>(3u * n) * area(X.mn, X.mx);
-    if (bestCost >= noSplitCost) {   // uniform: every thread folded the same partials
-        for (uint32_t q = tid; q < n; q += kAnimThreads) dst[first + q] = src[first + q];
-        return;   // the caller's barrier publishes dst
-    }
-    // partition: S, then each wave's left bigs / right smalls, rank bases, ranks, scatter
-    {
-        const uint32_t s = team_count_small(tm, A, src, first, lo, hi, axis, pos);
-        if (lane == 0) W.cnt[wave][0] = s;
-    }
-    __syncthreads();
-    uint32_t S = 0;
-#pragma unroll
-    for (int w = 0; w < kAnimWaves; ++w) S += W.cnt[w][0];
-    const uint32_t pL = S + ((S < n && !(A.c(axis, src[first + S]) < pos)) ? 1u : 0u);
-    __syncthreads();   // cnt is reused
-    {
-        uint32_t nl = 0, nr = 0;
-        for (uint32_t base = lo; base < hi; base += 64u) {
-            const uint32_t q = base + lane;
-            const bool in = q < hi;
-            const bool sm = in && A.c(axis, src[first + q]) < pos;
-            nl += __popcll(tm.ballot(in && q < pL && !sm));
-            nr += __popcll(tm.ballot(in && q >= pL && sm));
-        }
-        if (lane == 0) { W.cnt[wave][0] = nl; W.cnt[wave][1] = nr; }
-    }
-    __syncthreads();
-    uint32_t lbase = 0, rbase = 0;
-#pragma unroll
-    for (int w = 0; w < kAnimWaves; ++w) {
-        if (static_cast<uint32_t>(w) < wave) lbase += W.cnt[w][0];
-        if (static_cast<uint32_t>(w) > wave) rbase += W.cnt[w][1];
-    }
-    team_ranks(tm, A, src, M, first, lo, hi, pL, axis, pos, lbase, rbase);
-    __syncthreads();
-    for (uint32_t q = tid; q < n; q += kAnimThreads) {
-        const uint32_t id = src[first + q];
-        dst[first + part_dest(A, first, n, q, pL, !(A.c(axis, id) < pos))] = id;
-    }
-    __syncthreads();
-    if (S == 0u || S == n) {
-        for (uint32_t q = tid; q < n; q += kAnimThreads) src[first + q] = dst[first + q];
-        return;
-    }
-    // children's bounds: each wave's part of [first, first + S) and of [first + S, first + n)
-    float mn[2][3], mx[2][3];
-    for (int h = 0; h < 2; ++h) {
-        const uint32_t a0 = h ? S : 0u, a1 = h ? n : S;
-        const uint32_t pw = (a1 - a0 + kAnimWaves - 1u) / kAnimWaves;
-        const uint32_t l0 = min(a1, a0 + wave * pw), l1 = min(a1, a0 + wave * pw + pw);
-        const Bounds B = team_bounds(tm, A, dst, first + l0, first + l1);
-        __syncthreads();
-        if (lane == 0) wg_store_bounds(W, wave, B);
-        __syncthreads();
-        wg_fold_bounds(W).store(mn[h], mx[h]);
-    }
-    if (tid == 0) add_children(M, Ls, cl, t, first, n, S, depth, mn[0], mx[0], mn[1], mx[1]);
 }
 
-// One node of at most kTinyNode triangles by ONE lane: the reference's own serial passes
-// (bounds folds, bins, sweep, the swap loop itself), in place on `src`, then copied to `dst`
-// so that both permutation buffers hold the range.
-template <class AR>
-__device__ __forceinline__ void lane_node(const AR& A, uint32_t* src, uint32_t* dst, const MeshDev& M, Lists& Ls, uint32_t cl,
-                          uint32_t t, uint32_t depth) {
-    const TmpNode X = M.tmp[t];
-    const uint32_t first = X.first, n = X.count;
-    bool leaf = 3u * n <= 8u;
-    int axis = 0;
-    float pos = 0.f;
-    if (!leaf) {
-        float cl3[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, ch3[3] = {FLT_MIN, FLT_MIN, FLT_MIN};
-#pragma unroll 4
-        for (uint32_t k = 0; k < n; ++k) {
-            const uint32_t id = src[first + k];
-            const float x = A.cx[id], y = A.cy[id], z = A.cz[id];
-            cl3[0] = rmin(cl3[0], x); cl3[1] = rmin(cl3[1], y); cl3[2] = rmin(cl3[2], z);
-            ch3[0] = rmax(ch3[0], x); ch3[1] = rmax(ch3[1], y); ch3[2] = rmax(ch3[2], z);
+// One node (temp id t, or none: `act` false) by one team.  b: the permutation buffer of this
+// level (depth parity); the next level's is b ^ 1.  Children are appended to rg.nxt.
+template <bool MULTI, bool LDS>
+__device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>& St, const Team& tm, Slot& sl, Level& Lv,
+                             const Region& rg, bool act, uint32_t t, uint32_t b, uint32_t sub) {
+    using P = typename Store<LDS>::P;
+    P* src = b ? St.perm[1] : St.perm[0];   // (selects: a dynamic index would put St in scratch)
+    P* dst = b ? St.perm[0] : St.perm[1];
+    const uint32_t nl = 64u * tm.k;
+    TmpNode X{};
+    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[63] = stamp();
+    if (act) X = M.tmp[t];
+    const uint32_t n = act ? X.count : 0u, first = X.first, f0 = first - St.pos0;
+    // Subdivide's termination (idxCount <= 8) and the teams with no node: nothing but the copy
+    const bool work = act && 3u * n > 8u;
+    // 1. slot init
+    if (work) {
+        if (tm.tl < 6) sl.cb[tm.tl] = tm.tl < 3 ? FLT_MAX : FLT_MIN;
+        if (tm.tl < 3 * kBins) (&sl.bc[0][0])[tm.tl] = 0u;
+        for (uint32_t i = tm.tl; i < 3 * kBins * 3; i += nl) {
+            (&sl.bl[0][0][0])[i] = FLT_MAX;
+            (&sl.bh[0][0][0])[i] = FLT_MIN;
         }
-        float bestCost = FLT_MAX;
+        if (MULTI && tm.tl < 6) {
+            (&sl.cmin[0][0])[tm.tl] = min_key_init();
+            (&sl.cmax[0][0])[tm.tl] = FLT_MIN;
+        }
+    }
+    tsync<MULTI>();
+    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[64] = stamp();
+    // 2. centroid bounds (FindBestSplitPlane's minBounds / maxBounds, DataTypes.h:404-419)
+    if (work) {
+        float a0 = FLT_MAX, a1 = FLT_MAX, a2 = FLT_MAX, b0 = FLT_MIN, b1 = FLT_MIN, b2 = FLT_MIN;
+        for (uint32_t q = tm.tl; q < n; q += nl) {
+            const uint32_t e = src[f0 + q];
+            const float x = St.c(0, e), y = St.c(1, e), z = St.c(2, e);
+            a0 = fminf(a0, x); a1 = fminf(a1, y); a2 = fminf(a2, z);
+            b0 = fmaxf(b0, x); b1 = fmaxf(b1, y); b2 = fmaxf(b2, z);
+        }
+        a0 = wave_minf(a0); a1 = wave_minf(a1); a2 = wave_minf(a2);
+        b0 = wave_maxf(b0); b1 = wave_maxf(b1); b2 = wave_maxf(b2);
+        if (tm.lane == 0) {
+            if (MULTI) {
+                atomicMin(&sl.cb[0], a0); atomicMin(&sl.cb[1], a1); atomicMin(&sl.cb[2], a2);
+                atomicMax(&sl.cb[3], b0); atomicMax(&sl.cb[4], b1); atomicMax(&sl.cb[5], b2);
+            } else {
+                sl.cb[0] = a0; sl.cb[1] = a1; sl.cb[2] = a2; sl.cb[3] = b0; sl.cb[4] = b1; sl.cb[5] = b2;
+            }
+        }
+    }
+    tsync<MULTI>();
+    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[65] = stamp();
+    float minB[3] = {0.f, 0.f, 0.f}, bd[3] = {0.f, 0.f, 0.f}, scale[3] = {0.f, 0.f, 0.f};
+    bool live[3] = {false, false, false};
+    if (work) {
 #pragma unroll
         for (int ax = 0; ax < 3; ++ax) {
-            const float minBounds = cl3[ax];
-            const float boundsDifference = ch3[ax] - minBounds;
-            if (fabsf(boundsDifference) < FLT_EPSILON) continue;
-            const float scale = kBins / boundsDifference;
-            Bins bins;
-            bins.clear();
-#pragma unroll 2
-            for (uint32_t k = 0; k < n; ++k) bins.add(A, src[first + k], ax, minBounds, scale);
-            bins.sweep(ax, minBounds, boundsDifference, bestCost, axis, pos);
+            minB[ax] = sl.cb[ax];
+            bd[ax] = sl.cb[3 + ax] - minB[ax];                 // boundsDifference
+            live[ax] = !(fabsf(bd[ax]) < FLT_EPSILON);          // else `continue`
+            scale[ax] = kBins / bd[ax];
         }
-        const float noSplitCost = static_cast<float>(3u * n) * area(X.mn, X.mx);   // CalculateNodeCost
-        leaf = bestCost >= noSplitCost;
-    }
-    uint32_t S = n;
-    if (!leaf) {   // DataTypes.h:343-363 on this node's range
-        int i = 0, j = static_cast<int>(n) - 1;
-        while (i <= j) {
-            const uint32_t id = src[first + i];
-            if (A.c(axis, id) < pos) {
-                ++i;
-            } else {
-                src[first + i] = src[first + j];
-                src[first + j] = id;
-                --j;
+        // 3. bins (DataTypes.h:424-440): idxCount += 3 and the box of the three vertices;
+        //    in registers when lanes hold several elements, else LDS atomics per element
+        if (n > 2u * nl) {
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax)
+                if (live[ax]) bins_private(St, src, f0, n, tm.tl, nl, tm.lane, ax, minB[ax], scale[ax], sl, MULTI);
+        } else for (uint32_t q = tm.tl; q < n; q += nl) {
+            const uint32_t e = src[f0 + q];
+            const float l0 = St.lo(0, e), l1 = St.lo(1, e), l2 = St.lo(2, e);
+            const float h0 = St.hi(0, e), h1 = St.hi(1, e), h2 = St.hi(2, e);
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+                if (!live[ax]) continue;
+                const float x = (St.c(ax, e) - minB[ax]) * scale[ax];
+                // static_cast<int> of x >= 0 (a NaN x only comes from a NaN vertex: flagged, bin 0)
+                int bi = x >= 0.f ? static_cast<int>(fminf(x, 2147483520.f)) : 0;
+                bi = kPlanes < bi ? kPlanes : bi;   // std::min(amountOfPlaneBins, binIdx)
+                atomicAdd(&sl.bc[ax][bi], 3u);
+                atomicMin(&sl.bl[ax][bi][0], l0); atomicMin(&sl.bl[ax][bi][1], l1); atomicMin(&sl.bl[ax][bi][2], l2);
+                atomicMax(&sl.bh[ax][bi][0], h0); atomicMax(&sl.bh[ax][bi][1], h1); atomicMax(&sl.bh[ax][bi][2], h2);
             }
         }
-        S = static_cast<uint32_t>(i);
     }
-#pragma unroll 4
-    for (uint32_t k = 0; k < n; ++k) dst[first + k] = src[first + k];
-    if (leaf || S == 0u || S == n) return;
-    Bounds L, R;
-#pragma unroll 4
-    for (uint32_t k = 0; k < S; ++k) L.grow(A, src[first + k]);
-#pragma unroll 4
-    for (uint32_t k = S; k < n; ++k) R.grow(A, src[first + k]);
-    float lmn[3], lmx[3], rmn[3], rmx[3];
-    L.store(lmn, lmx);
-    R.store(rmn, rmx);
-    add_children(M, Ls, cl, t, first, n, S, depth, lmn, lmx, rmn, rmx);
+    tsync<MULTI>();
+    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[66] = stamp();
+    // 4. the plane sweep (DataTypes.h:443-480): lane j < 21 evaluates plane j % 7 of axis j / 7;
+    //    the reference takes the first strictly smaller cost in (axis, plane) order from FLT_MAX
+    int axis = 0;
+    float pos = 0.f;
+    bool split = false;
+    if (work) {
+        unsigned long long key = ~0ull;
+        const uint32_t j = tm.lane;
+        if (j < 3u * kPlanes) {
+            const int ax = static_cast<int>(j / kPlanes), i = static_cast<int>(j % kPlanes);
+            if (live[ax]) {
+                int lc = 0, rc = 0;
+                float l0 = FLT_MAX, l1 = FLT_MAX, l2 = FLT_MAX, h0 = FLT_MIN, h1 = FLT_MIN, h2 = FLT_MIN;
+                for (int q = 0; q <= i; ++q) {   // leftBox.Grow(bins[q].bounds), q = 0..i
+                    lc += static_cast<int>(sl.bc[ax][q]);
+                    l0 = rmin(l0, sl.bl[ax][q][0]); l1 = rmin(l1, sl.bl[ax][q][1]); l2 = rmin(l2, sl.bl[ax][q][2]);
+                    h0 = rmax(h0, sl.bh[ax][q][0]); h1 = rmax(h1, sl.bh[ax][q][1]); h2 = rmax(h2, sl.bh[ax][q][2]);
+                }
+                const float la = area(l0, l1, l2, h0, h1, h2);
+                l0 = l1 = l2 = FLT_MAX;
+                h0 = h1 = h2 = FLT_MIN;
+                for (int q = kPlanes; q > i; --q) {   // rightBox.Grow(bins[q].bounds), q = 7..i+1
+                    rc += static_cast<int>(sl.bc[ax][q]);
+                    l0 = rmin(l0, sl.bl[ax][q][0]); l1 = rmin(l1, sl.bl[ax][q][1]); l2 = rmin(l2, sl.bl[ax][q][2]);
+                    h0 = rmax(h0, sl.bh[ax][q][0]); h1 = rmax(h1, sl.bh[ax][q][1]); h2 = rmax(h2, sl.bh[ax][q][2]);
+                }
+                const float ra = area(l0, l1, l2, h0, h1, h2);
+                const float cost = static_cast<float>(lc) * la + static_cast<float>(rc) * ra;
+                // candidates: cost < FLT_MAX (NaN never is); ties keep the earlier (axis, plane)
+                if (cost < FLT_MAX) key = min_key(cost, j) & ~1ull;
+            }
+        }
+        key = wave_min64(key);
+        float bestCost = FLT_MAX;
+        if (key != ~0ull) {
+            const uint32_t jb = static_cast<uint32_t>(key) >> 1;
+            axis = static_cast<int>(jb / kPlanes);
+            const int i = static_cast<int>(jb % kPlanes);
+            const float step = bd[axis] / kBins;
+            pos = minB[axis] + step * static_cast<float>(i + 1);
+            bestCost = min_key_value(key);
+        }
+        const float noSplitCost = static_cast<float>(3u * n) * area(X.mn[0], X.mn[1], X.mn[2], X.mx[0], X.mx[1], X.mx[2]);
+        split = !(bestCost >= noSplitCost);   // Subdivide: `if (splitCost >= noSplitCost) return;`
+    }
+    // 5. the partition: per-wave blocks of positions in order
+    const uint32_t per = (n + tm.k - 1u) / tm.k;
+    const uint32_t lo = min(n, tm.wt * per), hi = min(n, tm.wt * per + per);
+    auto small = [&](uint32_t q) { return St.c(axis, src[f0 + q]) < pos; };
+    uint32_t S = 0, pL = 0;
+    if (split) {
+        uint32_t s = 0;
+        for (uint32_t base = lo; base < hi; base += 64u) {
+            const uint32_t q = base + tm.lane;
+            s += __popcll(__ballot(q < hi && small(q)));
+        }
+        if (MULTI && tm.lane == 0) sl.wc[tm.wt][0] = s;
+        S = s;
+    }
+    if (MULTI) {
+        tsync<true>();
+        if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[67] = stamp();
+        if (split) {
+            S = 0;
+            for (uint32_t w = 0; w < tm.k; ++w) S += sl.wc[w][0];
+        }
+    }
+    if (split) pL = S + ((S < n && !small(S)) ? 1u : 0u);
+    uint32_t lbase = 0, rbase = 0;
+    if (split && MULTI) {
+        uint32_t cl = 0, cr = 0;
+        for (uint32_t base = lo; base < hi; base += 64u) {
+            const uint32_t q = base + tm.lane;
+            const bool in = q < hi;
+            const bool sm = in && small(q);
+            cl += __popcll(__ballot(in && q < pL && !sm));
+            cr += __popcll(__ballot(in && q >= pL && sm));
+        }
+        if (tm.lane == 0) { sl.wc[tm.wt][1] = cl; sl.wc[tm.wt][2] = cr; }
+    }
+    if (MULTI) {
+        tsync<true>();
+        if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[68] = stamp();
+        if (split)
+            for (uint32_t w = 0; w < tm.k; ++w) {
+                if (w < tm.wt) lbase += sl.wc[w][1];
+                if (w > tm.wt) rbase += sl.wc[w][2];
+            }
+    }
+    if (split) wave_ranks(St, src, tm.lane, f0, lo, hi, pL, axis, pos, lbase, rbase);
+    tsync<MULTI>();
+    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[69] = stamp();
+    if (split) {
+        for (uint32_t q = tm.tl; q < n; q += nl) {
+            const uint32_t e = src[f0 + q];
+            dst[f0 + part_dest(St, f0, n, q, pL, !(St.c(axis, e) < pos))] = static_cast<P>(e);
+        }
+    } else if (act) {
+        for (uint32_t q = tm.tl; q < n; q += nl) dst[f0 + q] = src[f0 + q];   // a leaf: both buffers
+    }
+    tsync<MULTI>();
+    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[70] = stamp();
+    // leftCount 0 or all: a leaf with the permutation applied (both buffers)
+    const bool kids = split && S != 0u && S != n;
+    if (split && !kids)
+        for (uint32_t q = tm.tl; q < n; q += nl) src[f0 + q] = dst[f0 + q];
+    // 6. UpdateNodeBounds of both children (DataTypes.h:310-321), positions in the new order
+    if (kids) {
+        for (int c = 0; c < 2; ++c) {   // one child at a time (registers)
+            BoundAcc A;
+            const uint32_t a = c ? S : 0u, z = c ? n : S;
+            for (uint32_t q = a + tm.tl; q < z; q += nl) A.add(St, dst[f0 + q], 1u + (q - a));
+            A.wave();
+            if (tm.lane == 0) A.put(sl, c, MULTI);
+        }
+    }
+    tsync<MULTI>();
+    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[71] = stamp();
+    if (kids && tm.wt == 0 && tm.lane == 0) {
+        const uint32_t c = atomicAdd(&Lv.ids, 2u);
+        TmpNode a{}, bb{};
+        for (int q = 0; q < 3; ++q) {
+            a.mn[q] = min_key_value(sl.cmin[0][q]); a.mx[q] = sl.cmax[0][q];
+            bb.mn[q] = min_key_value(sl.cmin[1][q]); bb.mx[q] = sl.cmax[1][q];
+        }
+        a.first = first; a.count = S; a.l = -1; a.depth = X.depth + 1; a.parent = static_cast<int32_t>(t); a.sub = sub;
+        bb.first = first + S; bb.count = n - S; bb.l = -1; bb.depth = X.depth + 1; bb.parent = static_cast<int32_t>(t);
+        bb.sub = sub;
+        M.tmp[c] = a;
+        M.tmp[c + 1] = bb;
+        M.tmp[t].l = static_cast<int32_t>(c);
+        const uint32_t w = atomicAdd(&Lv.next, 2u);
+        rg.nxt[w] = c;
+        rg.nxt[w + 1] = c + 1;
+        atomicMax(&Lv.nmaxn, max(S, n - S));
+    }
+    if (MULTI) tsync<true>();   // the slot is free for the next level
+    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[72] = stamp();
 }
 
-// LDS = true: the build arrays live in the workgroup's LDS (every mesh of the launch fits),
-// so the compiler sees LDS pointers and emits ds_read / ds_write instead of flat accesses.
+// The level loop over a region's list (Lv.K nodes in rg.cur) until no level remains or, with
+// stop_wide, the level is kSubTarget wide or would take the top phase past kMaxTop nodes.
+// depth: the level of the list's nodes.  lvl_base (optional): the first temp id created while
+// processing each level (relative to the first).
 template <bool LDS>
-__global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
-    const MeshDev& M = L.meshes[blockIdx.x];
-    const float* mat = L.m[blockIdx.x];
+__device__ __forceinline__ uint32_t build_levels(const MeshDev& M, const Store<LDS>& St, Level& Lv, Slot* slots, Region& rg,
+                                 uint32_t depth, bool stop_wide, uint32_t sub, uint32_t* lvl_base, uint32_t lvl_cap,
+                                 uint32_t* stamps = nullptr, uint32_t nstamps = 0) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t depth0 = depth;
+    for (;; ++depth) {
+        const uint32_t K = Lv.K;
+        if (K == 0) break;
+        if (stop_wide && (K >= static_cast<uint32_t>(kSubTarget) || Lv.ids + 2u * K > static_cast<uint32_t>(kMaxTop)))
+            break;
+        if (lvl_base && tid == 0 && depth - depth0 < lvl_cap) lvl_base[depth - depth0] = Lv.ids;
+        const uint32_t b = depth & 1u;
+        // team size: 16 / K waves (a power of two), fewer while the nodes are small
+        uint32_t k = 1;
+        while (2u * k * K <= static_cast<uint32_t>(kAnimWaves)) k *= 2u;
+        while (k > 1u && Lv.maxn < 96u * k) k /= 2u;
+        if (k > 1u) {
+            const Team tm{k, (wave / k) * k, wave % k, (wave % k) * 64u + lane, lane};
+            const uint32_t j = wave / k;
+            node_process<true, LDS>(M, St, tm, slots[j], Lv, rg, j < K, j < K ? rg.cur[j] : 0u, b, sub);
+        } else {
+            const Team tm{1u, wave, 0u, lane, lane};
+            for (;;) {
+                uint32_t j = 0;
+                if (lane == 0) j = atomicAdd(&Lv.take, 1u);
+                j = __shfl(j, 0);
+                if (j >= K) break;
+                node_process<false, LDS>(M, St, tm, slots[wave], Lv, rg, true, rg.cur[j], b, sub);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            if (stamps && depth - depth0 < nstamps) stamps[depth - depth0] = stamp();   // diagnostics: level end
+            Lv.K = Lv.next;
+            Lv.next = 0;
+            Lv.take = 0;
+            Lv.maxn = Lv.nmaxn;
+            Lv.nmaxn = 0;
+        }
+        uint32_t* tsw = rg.cur;
+        rg.cur = rg.nxt;
+        rg.nxt = tsw;
+        __syncthreads();
+    }
+    return depth;
+}
+
+// ============================================================ launch 1: set-up + top levels
+template <bool LDS>
+__device__ __forceinline__ void top_phase(const Launch& L, const MeshDev& M, Level& Lv, Slot* slots, float* dyn) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const float* mat = L.m[blockIdx.x];
     const uint32_t T = M.T, V = M.V;
     const int4* idx = M.idx[L.cur];
     const float4* nrm = M.nrm[L.cur];
-    extern __shared__ float s_dyn[];
-    __shared__ Lists Ls;
-    __shared__ uint32_t s_fr[kMaxAnimParts][3];
-    __shared__ uint32_t s_nfr;
-    // build arrays: in LDS when every mesh of the launch fits (LDS), else in HBM
-    using Scratch = std::conditional_t<LDS, uint16_t, uint32_t>;
-    Arr<Scratch> A;
-    {
-        float* base = LDS ? s_dyn : M.soa;
-        A.cx = base; A.cy = base + T; A.cz = base + 2 * T;
-        A.lx = base + 3 * T; A.ly = base + 4 * T; A.lz = base + 5 * T;
-        A.hx = base + 6 * T; A.hy = base + 7 * T; A.hz = base + 8 * T;
-        A.perm[0] = LDS ? reinterpret_cast<uint32_t*>(s_dyn + 9 * T) : M.perm[0];
-        A.perm[1] = LDS ? reinterpret_cast<uint32_t*>(s_dyn + 10 * T) : M.perm[1];
-        uint16_t* s16 = reinterpret_cast<uint16_t*>(s_dyn + 11 * T);
-        A.lb = LDS ? reinterpret_cast<Scratch*>(s16) : reinterpret_cast<Scratch*>(M.lb);
-        A.rs = LDS ? reinterpret_cast<Scratch*>(s16 + T) : reinterpret_cast<Scratch*>(M.rs);
-        A.rk = LDS ? reinterpret_cast<Scratch*>(s16 + 2 * T) : reinterpret_cast<Scratch*>(M.rk);
+    float* soa = M.soa;
+    Store<LDS> St;
+    if (LDS) {
+        using P = typename Store<LDS>::P;
+        P* p16 = reinterpret_cast<P*>(dyn + 9 * T);
+        St = Store<LDS>{{p16, p16 + T}, p16 + 2 * T, p16 + 3 * T, p16 + 4 * T, dyn, T, 0u};
+    } else {
+        St = Store<LDS>{{reinterpret_cast<typename Store<LDS>::P*>(M.perm[0]),
+                         reinterpret_cast<typename Store<LDS>::P*>(M.perm[1])},
+                        reinterpret_cast<typename Store<LDS>::P*>(M.lb), reinterpret_cast<typename Store<LDS>::P*>(M.rs),
+                        reinterpret_cast<typename Store<LDS>::P*>(M.rk), soa, T, 0u};
     }
-    // diagnostic phase stamps (s_memrealtime, 100 MHz): status[8] start, [9] set-up done,
-    // [10 + d] level d done, [60] numbered, [61] written, [62] frontier done
-    auto stamp = [&](int slot) {
-        if (tid == 0) M.status[slot] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
-    };
-    stamp(8);
-    __shared__ WgScratch W;
-    if (tid == 0) {
-        for (int q = 0; q < 4; ++q) { Ls.n[q] = 0; Ls.next[q] = 0; }
-        Ls.n[node_class(T)] = 1;
-        Ls.ntmp = 1; Ls.depth = 0; Ls.err = 0;
-    }
-
+    float* rec = const_cast<float*>(St.rec);
     // ---- UpdateTransforms (DataTypes.h:210-230)
     for (uint32_t v = tid; v < V; v += kAnimThreads) {
         const float4 p = M.pos[v];
@@ -698,7 +656,9 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
         M.tpos[v] = make_float4(t.x, t.y, t.z, 0.f);
     }
     __syncthreads();
-    // per triangle: transformed normal (input order), centroid, box
+    // per triangle: transformed normal (input order), centroid, box; the identity permutation;
+    // the root's bounds over the input order (BuildBVH, DataTypes.h:294-308)
+    BoundAcc A;
     for (uint32_t k = tid; k < T; k += kAnimThreads) {
         const float4 n = nrm[k];
         const float3 tn = normalized(xform_vector(mat, n.x, n.y, n.z));
@@ -707,114 +667,302 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
         const float4 v0 = M.tpos[i.x], v1 = M.tpos[i.y], v2 = M.tpos[i.z];
         if (v0.x != v0.x || v0.y != v0.y || v0.z != v0.z || v1.x != v1.x || v1.y != v1.y || v1.z != v1.z ||
             v2.x != v2.x || v2.y != v2.y || v2.z != v2.z)
-            atomicOr(&Ls.err, kErrNaN);
+            atomicOr(&Lv.err, kErrNaN);
         // (v0 + v1 + v2) * 0.3333f, the reference's centroid (DataTypes.h:348, 411-415, 435)
-        A.cx[k] = ((v0.x + v1.x) + v2.x) * 0.3333f;
-        A.cy[k] = ((v0.y + v1.y) + v2.y) * 0.3333f;
-        A.cz[k] = ((v0.z + v1.z) + v2.z) * 0.3333f;
-        A.lx[k] = rmin(rmin(v0.x, v1.x), v2.x); A.ly[k] = rmin(rmin(v0.y, v1.y), v2.y); A.lz[k] = rmin(rmin(v0.z, v1.z), v2.z);
-        A.hx[k] = rmax(rmax(v0.x, v1.x), v2.x); A.hy[k] = rmax(rmax(v0.y, v1.y), v2.y); A.hz[k] = rmax(rmax(v0.z, v1.z), v2.z);
-        A.perm[0][k] = k;
+        const float r9[9] = {((v0.x + v1.x) + v2.x) * 0.3333f, ((v0.y + v1.y) + v2.y) * 0.3333f,
+                             ((v0.z + v1.z) + v2.z) * 0.3333f,
+                             rmin(rmin(v0.x, v1.x), v2.x), rmin(rmin(v0.y, v1.y), v2.y), rmin(rmin(v0.z, v1.z), v2.z),
+                             rmax(rmax(v0.x, v1.x), v2.x), rmax(rmax(v0.y, v1.y), v2.y), rmax(rmax(v0.z, v1.z), v2.z)};
+#pragma unroll
+        for (int c = 0; c < 9; ++c) {
+            soa[c * T + k] = r9[c];
+            if (LDS) rec[c * T + k] = r9[c];
+        }
+        St.perm[0][k] = static_cast<typename Store<LDS>::P>(k);
+        A.add(St, k, 1u + k);
     }
+    A.wave();
+    Slot& s0 = slots[0];
+    if (tid < 3) { s0.cmin[0][tid] = min_key_init(); s0.cmax[0][tid] = FLT_MIN; }
     __syncthreads();
-    // ---- BuildBVH (DataTypes.h:294-308): the root covers every triangle (its bounds: each
-    // wave folds its eighth, the eighths are folded in order)
-    {
-        const Team<64> tm(lane);
-        const uint32_t per = (T + kAnimWaves - 1u) / kAnimWaves;
-        const Bounds B = team_bounds(tm, A, A.perm[0], min(T, wave * per), min(T, wave * per + per));
-        if (lane == 0) wg_store_bounds(W, wave, B);
-    }
+    if (lane == 0) A.put(s0, 0, true);
     __syncthreads();
     if (tid == 0) {
         TmpNode r{};
-        wg_fold_bounds(W).store(r.mn, r.mx);
-        r.first = 0; r.count = T; r.l = -1; r.depth = 0;
+        for (int q = 0; q < 3; ++q) { r.mn[q] = min_key_value(s0.cmin[0][q]); r.mx[q] = s0.cmax[0][q]; }
+        r.first = 0; r.count = T; r.l = -1; r.depth = 0; r.parent = -1; r.sub = kMaxSub;
         M.tmp[0] = r;
-        M.lvl[2 * node_class(T)][0] = 0;
+        M.lvl[0][0] = 0;
+        M.status[kStSetup] = stamp();
     }
     __syncthreads();
-    stamp(9);
-    // ---- Subdivide (DataTypes.h:323-389), one level per iteration, each node by a team
-    // sized to it (node_class)
-    uint32_t cr = 0, cl = 0;
-    for (uint32_t depth = 0;; ++depth) {
-        const uint32_t n0 = Ls.n[0], n1 = Ls.n[1], n2 = Ls.n[2], n3 = Ls.n[3];
-        if (n0 + n1 + n2 + n3 == 0) break;
-        uint32_t* src = cr ? A.perm[1] : A.perm[0];   // (selects: a dynamic index would put A in scratch)
-        uint32_t* dst = cr ? A.perm[0] : A.perm[1];
-        if (tid == 0 && depth < 12) {   // diagnostics: node count per class at this level
-            M.status[64 + 4 * depth] = n0; M.status[65 + 4 * depth] = n1;
-            M.status[66 + 4 * depth] = n2; M.status[67 + 4 * depth] = n3;
+    // ---- Subdivide (DataTypes.h:323-389), the top levels
+    Region rg{M.lvl[0], M.lvl[1]};
+    const uint32_t D = build_levels<LDS>(M, St, Lv, slots, rg, 0u, true, kMaxSub, nullptr, 0u, M.status + 20, 8u);
+    if (LDS) {   // both permutation buffers back to HBM (subtrees stage from them, the output reads them)
+        for (uint32_t k = tid; k < T; k += kAnimThreads) {
+            M.perm[0][k] = St.perm[0][k];
+            M.perm[1][k] = St.perm[1][k];
         }
-        for (uint32_t j = 0; j < n0; ++j) {
-            wg_node(A, src, dst, M, Ls, W, cl, M.lvl[0 + cl][j], depth, tid);
+    }
+    // the last level's nodes become subtrees: descendants' temp ids in disjoint ranges
+    if (wave == 0) {
+        const uint32_t K = Lv.K;
+        uint32_t base = Lv.ids;
+        for (uint32_t j0 = 0; j0 < K; j0 += 64u) {
+            const uint32_t j = j0 + lane;
+            uint32_t t = 0, need = 0;
+            if (j < K) {
+                t = rg.cur[j];
+                const uint32_t n = M.tmp[t].count;
+                need = n > 1u ? 2u * n - 2u : 0u;
+            }
+            // inclusive prefix of `need` over the wave (in j order)
+            uint32_t incl = need;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = __shfl_up(incl, o);
+                if (lane >= static_cast<uint32_t>(o)) incl += v;
+            }
+            if (j < K) {
+                M.sub[j] = SubRec{t, base + incl - need, 0u, D};
+                M.tmp[t].sub = j;
+            }
+            base += __shfl(incl, 63);
+        }
+        if (lane == 0) {
+            M.status[0] = Lv.err;
+            M.status[1] = K ? D : (D ? D - 1u : 0u);   // deepest level so far
+            M.status[4] = K;
+            M.status[5] = Lv.ids;
+            M.status[6] = D;
+            M.status[kStTopDone] = stamp();
+            M.status[59] = static_cast<uint32_t>(__builtin_amdgcn_s_memtime());
+            M.status[kStSub0] = 0xffffffffu;
+            M.status[kStSubEnd] = 0u;
+        }
+    }
+}
+
+// ============================================================ launch 2: one subtree per workgroup
+constexpr uint32_t kSubLevels = 256;
+template <bool LDS>
+__device__ __forceinline__ void sub_phase(const Launch& L, const MeshDev& M, uint32_t f, Level& Lv, Slot* slots, uint32_t* lvl_base,
+                          float* dyn) {
+    const uint32_t tid = threadIdx.x;
+    const SubRec S0 = M.sub[f];
+    const TmpNode X0 = M.tmp[S0.root];
+    const uint32_t D = M.status[6], n = X0.count, b = D & 1u;
+    const uint32_t t_sub0 = stamp();
+    Store<LDS> St;
+    uint32_t* gmap = nullptr;
+    if (LDS) {   // stage the subtree's records by local element index
+        using P = typename Store<LDS>::P;
+        gmap = reinterpret_cast<uint32_t*>(dyn + 9 * n);
+        P* p16 = reinterpret_cast<P*>(gmap + n);
+        St = Store<LDS>{{p16, p16 + n}, p16 + 2 * n, p16 + 3 * n, p16 + 4 * n, dyn, n, X0.first};
+        for (uint32_t q = tid; q < n; q += kAnimThreads) {
+            const uint32_t g = M.perm[b][X0.first + q];
+            gmap[q] = g;
+#pragma unroll
+            for (int c = 0; c < 9; ++c) dyn[c * n + q] = M.soa[c * M.T + g];
+            (b ? St.perm[1] : St.perm[0])[q] = static_cast<P>(q);
+        }
+    } else {
+        St = Store<LDS>{{reinterpret_cast<typename Store<LDS>::P*>(M.perm[0]),
+                         reinterpret_cast<typename Store<LDS>::P*>(M.perm[1])},
+                        reinterpret_cast<typename Store<LDS>::P*>(M.lb), reinterpret_cast<typename Store<LDS>::P*>(M.rs),
+                        reinterpret_cast<typename Store<LDS>::P*>(M.rk), M.soa, M.T, 0u};
+    }
+    if (tid == 0) {
+        if (f == 0) M.status[29] = stamp();   // subtree 0: staged
+        atomicMin(&M.status[kStSub0], stamp());
+        Lv.K = 1; Lv.next = 0; Lv.take = 0; Lv.maxn = n; Lv.nmaxn = 0; Lv.ids = S0.base; Lv.err = 0;
+        M.lvl[0][X0.first] = S0.root;
+    }
+    __syncthreads();
+    Region rg{M.lvl[0] + X0.first, M.lvl[1] + X0.first};
+    const uint32_t Dend = build_levels<LDS>(M, St, Lv, slots, rg, D, false, f, lvl_base, kSubLevels,
+                                            f == 0 ? M.status + 32 : nullptr, 24u);
+    if (f == 0 && tid == 0) M.status[30] = stamp();   // subtree 0: levels done
+    if (LDS)   // the final order (every leaf range is current in both buffers) as triangle ids
+        for (uint32_t q = tid; q < n; q += kAnimThreads) M.perm[0][X0.first + q] = gmap[St.perm[0][q]];
+    // levels D .. Dend - 1 hold nodes: level D the root, level D + r (r >= 1) the ids
+    // [lvl_base[r - 1], lvl_base[r])
+    const uint32_t nlev = Dend - D, idend = Lv.ids;
+    const bool ranks_ok = nlev < kSubLevels;
+    if (tid == 0 && ranks_ok) lvl_base[nlev] = idend;
+    __syncthreads();
+    auto lvl_lo = [&](uint32_t r) { return r == 0 ? S0.root : lvl_base[r - 1]; };
+    auto lvl_hi = [&](uint32_t r) { return r == 0 ? S0.root + 1u : lvl_base[r]; };
+    // split counts bottom-up, then the DFS preorder ranks of the split nodes top-down
+    // (relative to the subtree root: its descendants' ranks follow its own)
+    if (ranks_ok) {
+        for (int r = static_cast<int>(nlev) - 1; r >= 0; --r) {
+            for (uint32_t t = lvl_lo(r) + tid; t < lvl_hi(r); t += kAnimThreads) {
+                const int32_t l = M.tmp[t].l;
+                M.tmp[t].splits = l >= 0 ? 1u + M.tmp[l].splits + M.tmp[l + 1].splits : 0u;
+            }
             __syncthreads();
         }
-        if (tid == 0 && depth < 12) M.status[112 + depth] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
-        {
-            const Team<64> tm(lane);
-            for (uint32_t j = wave; j < n1; j += kAnimWaves) team_node(tm, A, src, dst, M, Ls, cl, M.lvl[2 + cl][j], depth);
-        }
-        {
-            const Team<16> tm(lane);
-            constexpr uint32_t kTeams = kAnimThreads / 16;
-            for (uint32_t j = tid / 16u; j < n2; j += kTeams) team_node(tm, A, src, dst, M, Ls, cl, M.lvl[4 + cl][j], depth);
-        }
-        for (uint32_t j = tid; j < n3; j += kAnimThreads) lane_node(A, src, dst, M, Ls, cl, M.lvl[6 + cl][j], depth);
+        if (tid == 0) M.tmp[S0.root].rank = 0u;
         __syncthreads();
+        for (uint32_t r = 0; r < nlev; ++r) {
+            for (uint32_t t = lvl_lo(r) + tid; t < lvl_hi(r); t += kAnimThreads) {
+                const TmpNode X = M.tmp[t];
+                if (X.l < 0) continue;
+                M.tmp[X.l].rank = X.rank + 1u;
+                M.tmp[X.l + 1].rank = X.rank + 1u + M.tmp[X.l].splits;
+            }
+            __syncthreads();
+        }
+    }
+    if (f == 0 && tid == 0) M.status[31] = stamp();   // subtree 0: ranks done
+    if (tid == 0 && f < 16u) {   // diagnostics
+        M.status[80 + 2 * f] = t_sub0; M.status[81 + 2 * f] = stamp(); M.status[96 + f] = n;
+    }
+    if (tid == 0) {
+        M.sub[f].nalloc = idend - S0.base;
+        M.sub[f].maxd = Dend - 1u;
+        if (!ranks_ok) atomicOr(&M.status[0], kErrDepth);
+        atomicMax(&M.status[kStSubEnd], stamp());
+    }
+}
+
+// One kernel: workgroup (mesh, 0) runs the set-up and the top levels; workgroups (mesh, 1 + f)
+// wait for them (an epoch flag, agent scope) and build subtree f.  One launch instead of two:
+// a kernel boundary after the top phase cost ~100 us before the first subtree workgroup ran
+// (the idle XCDs' start-up, profiles/r03).  The producers come first in dispatch order
+// (blockIdx.x fastest), so a waiting workgroup never holds back its own mesh's producer.
+constexpr uint64_t kWaitTicks = 20000000ull;   // 200 ms of s_memrealtime: a stuck build reports, never hangs
+__global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
+    const MeshDev& M = L.meshes[blockIdx.x];
+    extern __shared__ float s_dyn[];
+    __shared__ Level Lv;
+    __shared__ Slot slots[kAnimWaves];
+    __shared__ uint32_t lvl_base[kSubLevels + 1];
+    __shared__ uint32_t s_go;
+    const uint32_t tid = threadIdx.x;
+    if (blockIdx.y == 0) {
         if (tid == 0) {
-            uint32_t any = 0;
-            for (int q = 0; q < 4; ++q) { Ls.n[q] = Ls.next[q]; Ls.next[q] = 0; any += Ls.n[q]; }
-            if (any) Ls.depth = depth + 1;
-            if (depth < 50) M.status[10 + depth] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
+            M.status[kStTop0] = stamp();
+            M.status[58] = static_cast<uint32_t>(__builtin_amdgcn_s_memtime());   // diagnostics: shader clock
+            Lv.K = 1; Lv.next = 0; Lv.take = 0; Lv.maxn = M.T; Lv.nmaxn = 0; Lv.ids = 1; Lv.err = 0;
         }
         __syncthreads();
-        cr ^= 1u;
-        cl ^= 1u;
-    }
-    // ---- the reference's numbering: split nodes' children pairs in DFS preorder of the splits
-    const uint32_t ntmp = Ls.ntmp, maxd = Ls.depth;
-    for (int d = static_cast<int>(maxd); d >= 0; --d) {
-        for (uint32_t t = tid; t < ntmp; t += kAnimThreads) {
-            const TmpNode& X = M.tmp[t];
-            if (X.depth != static_cast<uint32_t>(d)) continue;
-            M.tmp[t].splits = X.l >= 0 ? 1u + M.tmp[X.l].splits + M.tmp[X.l + 1].splits : 0u;
-        }
+        if (M.T <= L.top_lds) top_phase<true>(L, M, Lv, slots, s_dyn);
+        else top_phase<false>(L, M, Lv, slots, s_dyn);
         __syncthreads();
+        if (tid == 0) {   // publish every write of the workgroup to the subtree workgroups
+            __threadfence();
+            __hip_atomic_store(&M.status[7], L.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
     }
-    if (tid == 0) { M.tmp[0].rank = 0; M.tmp[0].ref = 0; }
+    const uint32_t f = blockIdx.y - 1u;
+    if (tid == 0) {
+        if (f < 16u) M.status[112 + f] = stamp();   // diagnostics: workgroup entry
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t ok = 1;
+        while (__hip_atomic_load(&M.status[7], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != L.epoch) {
+            __builtin_amdgcn_s_sleep(4);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) { ok = 0; break; }
+        }
+        if (!ok) atomicOr(&M.status[0], kErrTimeout);
+        s_go = ok;
+    }
     __syncthreads();
-    for (uint32_t d = 0; d <= maxd; ++d) {
-        for (uint32_t t = tid; t < ntmp; t += kAnimThreads) {
-            const TmpNode X = M.tmp[t];
-            if (X.depth != d || X.l < 0) continue;
-            const uint32_t r = X.rank;
-            M.tmp[X.l].ref = 1u + 2u * r;
-            M.tmp[X.l + 1].ref = 2u + 2u * r;
-            M.tmp[X.l].rank = r + 1u;
-            M.tmp[X.l + 1].rank = r + 1u + M.tmp[X.l].splits;
-        }
-        __syncthreads();
-    }
-    stamp(60);
-    // ---- outputs: the reference's node array (fields the reference writes), the render
-    // layout's node records (+ octant copies), the permuted state and triangle records
-    const Image& I = L.img;
-    for (uint32_t t = tid; t < ntmp; t += kAnimThreads) {
+    if (!s_go || f >= M.status[4]) return;
+    const uint32_t n = M.tmp[M.sub[f].root].count;
+    if (L.sub_lds && n <= kSubLdsMax) sub_phase<true>(L, M, f, Lv, slots, lvl_base, s_dyn);
+    else sub_phase<false>(L, M, f, Lv, slots, lvl_base, s_dyn);
+}
+
+// ============================================================ launch 3: numbering and output
+constexpr uint32_t kOutCacheIds = 8192;   // temp ids cached in LDS for the frontier walk (meshes up to 4,096 triangles)
+__global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
+    const MeshDev& M = L.meshes[blockIdx.y];
+    const uint32_t g = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t T = M.T;
+    const uint32_t nsub = M.status[4], ntop = M.status[5];
+    __shared__ int32_t s_l[kMaxTop];
+    __shared__ uint32_t s_split[kMaxTop], s_rank[kMaxTop], s_count[kMaxTop];
+    __shared__ uint32_t s_subroot[kMaxSub], s_base[kMaxSub], s_nalloc[kMaxSub], s_smaxd[kMaxSub], s_vbase[kMaxSub + 1];
+    __shared__ uint8_t s_isroot[kMaxTop];
+    __shared__ uint32_t s_maxd;
+    if (g == 0 && tid == 0) M.status[kStOut0] = stamp();
+    // ---- the top nodes' split counts (bottom-up, subtree roots from launch 2) and ranks
+    for (uint32_t t = tid; t < ntop; t += kAnimThreads) {
         const TmpNode X = M.tmp[t];
-        rtx_bvh_node& R = M.ref[X.ref];
-        #pragma unroll
+        s_l[t] = X.l;
+        s_count[t] = X.count;
+        s_isroot[t] = X.sub < static_cast<uint32_t>(kMaxSub) ? 1 : 0;
+        s_split[t] = s_isroot[t] ? X.splits : 0u;   // a subtree root: its own build's count
+    }
+    for (uint32_t f = tid; f < nsub; f += kAnimThreads) {
+        const SubRec s = M.sub[f];
+        s_subroot[f] = s.root; s_base[f] = s.base; s_nalloc[f] = s.nalloc; s_smaxd[f] = s.maxd;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t maxd = M.status[1];
+        for (uint32_t f = 0; f < nsub; ++f) maxd = max(maxd, s_smaxd[f]);
+        s_maxd = maxd;
+        // top nodes are numbered in creation order (parents before children)
+        for (int t = static_cast<int>(ntop) - 1; t >= 0; --t) {
+            const int32_t l = s_l[t];
+            if (!s_isroot[t]) s_split[t] = l >= 0 ? 1u + s_split[l] + s_split[l + 1] : 0u;
+        }
+        s_rank[0] = 0u;
+        for (uint32_t t = 0; t < ntop; ++t) {
+            const int32_t l = s_l[t];
+            if (l >= 0 && !s_isroot[t]) {   // a subtree root's children are subtree nodes
+                s_rank[l] = s_rank[t] + 1u;
+                s_rank[l + 1] = s_rank[t] + 1u + s_split[l];
+            }
+        }
+        s_vbase[0] = ntop;
+        for (uint32_t f = 0; f < nsub; ++f) s_vbase[f + 1] = s_vbase[f] + s_nalloc[f];
+        if (g == 0) M.status[kStRanks] = stamp();
+    }
+    __syncthreads();
+    // absolute DFS rank of a split node (temp id t)
+    auto rank_abs = [&](uint32_t t, const TmpNode& X) -> uint32_t {
+        return t < ntop ? s_rank[t] : s_rank[s_subroot[X.sub]] + X.rank;
+    };
+    // index in the reference's node array: the root 0, the children of the split ranked r at 1 + 2r, 2 + 2r
+    auto ref_of = [&](uint32_t t, const TmpNode& X) -> uint32_t {
+        if (t == 0) return 0u;
+        const uint32_t p = static_cast<uint32_t>(X.parent);
+        const TmpNode P = M.tmp[p];
+        return 1u + 2u * rank_abs(p, P) + (t == static_cast<uint32_t>(P.l) + 1u ? 1u : 0u);
+    };
+    const Image& I = L.img;
+    const uint32_t nvirt = s_vbase[nsub];
+    const uint32_t stride = kOutGroups * kAnimThreads;
+    // ---- the reference's node array (fields the reference writes) and the render records
+    for (uint32_t v = g * kAnimThreads + tid; v < nvirt; v += stride) {
+        uint32_t t = v;
+        if (v >= ntop) {
+            uint32_t f = 0;
+            while (v >= s_vbase[f + 1]) ++f;
+            t = s_base[f] + (v - s_vbase[f]);
+        }
+        const TmpNode X = M.tmp[t];
+        const uint32_t ref = ref_of(t, X);
+        rtx_bvh_node& R = M.ref[ref];
+#pragma unroll
         for (int c = 0; c < 3; ++c) { R.min[c] = X.mn[c]; R.max[c] = X.mx[c]; }
         R.first_idx = 3u * X.first;
         const bool split = X.l >= 0;
         R.idx_count = split ? 0u : 3u * X.count;
-        if (split) R.left_node = M.tmp[X.l].ref;
+        const uint32_t lref = split ? 1u + 2u * rank_abs(t, X) : 0u;
+        if (split) R.left_node = lref;
         else if (t == 0) R.left_node = 0u;   // BuildBVH resets the root's leftNode
-        const uint32_t link = split ? (M.root + M.tmp[X.l].ref) * 32u : (M.tri0 + X.first) * 64u;
+        const uint32_t link = split ? (M.root + lref) * 32u : (M.tri0 + X.first) * 64u;
         const float4 a = make_float4(X.mn[0], X.mx[0], X.mn[1], X.mx[1]);
         const float4 b = make_float4(X.mn[2], X.mx[2], fbits(link), fbits(split ? 0u : X.count));
-        const size_t slot = static_cast<size_t>(M.root) + X.ref;
+        const size_t slot = static_cast<size_t>(M.root) + ref;
         const int copies = I.oct_bytes ? 8 : 1;
         for (int k = 0; k < copies; ++k) {   // copy k stores (hi, lo) on the axes set in k
             float4* dn = reinterpret_cast<float4*>(reinterpret_cast<char*>(I.nodes) + static_cast<size_t>(k) * I.oct_bytes);
@@ -823,10 +971,13 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
             dn[2 * slot + 1] = make_float4(sz ? b.y : b.x, sz ? b.x : b.y, b.z, b.w);
         }
     }
-    const uint32_t* fin = A.perm[0];   // every leaf range is current in both buffers
+    // ---- the permuted state and the triangle records
+    const uint32_t* fin = M.perm[0];   // every leaf range is current in both buffers
+    const int4* idx = M.idx[L.cur];
+    const float4* nrm = M.nrm[L.cur];
     int4* idx_out = M.idx[L.cur ^ 1u];
     float4* nrm_out = M.nrm[L.cur ^ 1u];
-    for (uint32_t k = tid; k < T; k += kAnimThreads) {
+    for (uint32_t k = g * kAnimThreads + tid; k < T; k += stride) {
         const uint32_t id = fin[k];
         const int4 i = idx[id];
         const float4 tn = M.tnrm[id];
@@ -840,69 +991,110 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
         tr[2] = make_float4(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z, tn.z);   // edge2 (:140)
         tr[3] = make_float4(fbits(M.mat_bits), 0.f, 0.f, 0.f);
     }
-    __syncthreads();
-    stamp(61);
+    if (g == 0 && tid == 0) M.status[56] = stamp();   // workgroup 0: records written
+    if (g != 0) return;
     // ---- split-rendering frontier (rtx_hip.hip build_parts): split the part with the most
-    // triangles (first one on a tie) until part_cap parts or only leaves remain
-    if (wave == 0) {
-        if (lane == 0) { s_fr[0][0] = 0; s_fr[0][1] = 0; s_fr[0][2] = 0; s_nfr = 1; }
-        __builtin_amdgcn_wave_barrier();
-        for (;;) {
-            const uint32_t nf = s_nfr;
-            if (nf >= M.part_cap) break;
-            uint32_t key = 0, at = ~0u;   // count + 1 of an eligible entry (0: none), its index
-            for (uint32_t k = lane; k < nf; k += 64u) {
-                const TmpNode& X = M.tmp[s_fr[k][0]];
-                const uint32_t kk = (X.l >= 0 && s_fr[k][2] < 31u) ? X.count + 1u : 0u;
-                if (kk > key) { key = kk; at = k; }
+    // triangles (first one on a tie) until part_cap parts or only leaves remain.  The walk
+    // reads (count, left child) of its nodes from an LDS copy of every node's (count, left
+    // child) by temp id when the mesh is small enough (2T ids), else from HBM.
+    __shared__ uint32_t s_nc[kOutCacheIds];
+    __shared__ int32_t s_nl[kOutCacheIds];
+    const bool cached = 2u * T <= kOutCacheIds;
+    if (cached)
+        for (uint32_t v = tid; v < nvirt; v += kAnimThreads) {
+            uint32_t t = v;
+            if (v >= ntop) {
+                uint32_t f = 0;
+                while (v >= s_vbase[f + 1]) ++f;
+                t = s_base[f] + (v - s_vbase[f]);
             }
-            for (uint32_t off = 32; off > 0; off >>= 1) {   // max key, lowest index
-                const uint32_t ok = __shfl_xor(key, off), oa = __shfl_xor(at, off);
-                if (ok > key || (ok == key && oa < at)) { key = ok; at = oa; }
-            }
-            if (key == 0u) break;
-            const uint32_t e0 = s_fr[at][0], e1 = s_fr[at][1], e2 = s_fr[at][2];
-            // entries after `at` move up by one; reads complete before the writes
-            uint32_t v0[2], v1[2], v2[2];
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t k = lane + 64u * h;
-                if (k < nf) { v0[h] = s_fr[k][0]; v1[h] = s_fr[k][1]; v2[h] = s_fr[k][2]; }
-            }
-            __builtin_amdgcn_wave_barrier();
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t k = lane + 64u * h;
-                if (k < nf && k > at) { s_fr[k + 1][0] = v0[h]; s_fr[k + 1][1] = v1[h]; s_fr[k + 1][2] = v2[h]; }
-            }
-            if (lane == 0) {
-                const uint32_t l = static_cast<uint32_t>(M.tmp[e0].l);
-                s_fr[at][0] = l; s_fr[at][1] = e1; s_fr[at][2] = e2 + 1u;
-                s_fr[at + 1][0] = l + 1u; s_fr[at + 1][1] = e1 | (1u << e2); s_fr[at + 1][2] = e2 + 1u;
-                s_nfr = nf + 1u;
-            }
-            __builtin_amdgcn_wave_barrier();
+            const TmpNode X = M.tmp[t];
+            s_nc[t] = X.count;
+            s_nl[t] = X.l;
         }
+    __syncthreads();
+    if (tid == 0) M.status[57] = stamp();   // frontier cache loaded
+    if (wave != 0) return;
+    auto node_cl = [&](uint32_t t, uint32_t& count, int32_t& l) {
+        if (cached) { count = s_nc[t]; l = s_nl[t]; return; }
+        const TmpNode X = M.tmp[t];
+        count = X.count;
+        l = X.l;
+    };
+    __shared__ uint32_t s_fr[kMaxAnimParts + 1][5];   // temp id, path bits, depth, count, left child
+    __shared__ uint32_t s_nfr;
+    if (lane == 0) {
+        s_fr[0][0] = 0; s_fr[0][1] = 0; s_fr[0][2] = 0; s_fr[0][3] = s_count[0]; s_fr[0][4] = static_cast<uint32_t>(s_l[0]);
+        s_nfr = 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (;;) {
         const uint32_t nf = s_nfr;
-        // A tree deeper than the render kernel's DFS stack must never reach it (its pushes are
-        // unchecked): the mesh is disabled in this image — no frontier parts, node count 0, so
-        // mesh_traverse / part_traverse skip it — and the update reports kErrDepth.
-        const bool too_deep = maxd >= L.depth_limit;
-        for (uint32_t k = lane; k < M.part_cap; k += 64u) {
-            I.parts[M.part0 + k] = (k < nf && !too_deep) ? make_int4(static_cast<int>(M.mesh),
-                                                      static_cast<int>(M.root + M.tmp[s_fr[k][0]].ref),
-                                                      static_cast<int>(s_fr[k][1]), static_cast<int>(s_fr[k][2]))
-                                          : make_int4(-1, 0, 0, 0);
+        if (nf >= M.part_cap) break;
+        uint32_t key = 0, at = ~0u;   // count + 1 of an eligible entry (0: none), its index
+        for (uint32_t k = lane; k < nf; k += 64u) {
+            const uint32_t kk = (static_cast<int32_t>(s_fr[k][4]) >= 0 && s_fr[k][2] < 31u) ? s_fr[k][3] + 1u : 0u;
+            if (kk > key) { key = kk; at = k; }
+        }
+        for (uint32_t off = 32; off > 0; off >>= 1) {   // max key, lowest index
+            const uint32_t ok = __shfl_xor(key, off), oa = __shfl_xor(at, off);
+            if (ok > key || (ok == key && oa < at)) { key = ok; at = oa; }
+        }
+        if (key == 0u) break;
+        const uint32_t e1 = s_fr[at][1], e2 = s_fr[at][2], l = s_fr[at][4];
+        // entries after `at` move up by one; reads complete before the writes
+        uint32_t v[2][5];
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t k = lane + 64u * h;
+            if (k < nf)
+                for (int c = 0; c < 5; ++c) v[h][c] = s_fr[k][c];
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t k = lane + 64u * h;
+            if (k < nf && k > at)
+                for (int c = 0; c < 5; ++c) s_fr[k + 1][c] = v[h][c];
         }
         if (lane == 0) {
-            uint32_t err = Ls.err;
-            if (too_deep) err |= kErrDepth;
-            M.status[0] = err;
-            M.status[1] = maxd;
-            M.status[2] = 1u + 2u * M.tmp[0].splits;   // nodesUsed
-            // the mesh record's node count (0: disabled, see too_deep)
-            I.meshes[M.mesh].y = too_deep ? 0 : static_cast<int>(M.status[2]);
-            M.status[3] = nf;
-            M.status[62] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
+            uint32_t ca, cb;
+            int32_t la, lb;
+            node_cl(l, ca, la);
+            node_cl(l + 1u, cb, lb);
+            s_fr[at][0] = l; s_fr[at][1] = e1; s_fr[at][2] = e2 + 1u; s_fr[at][3] = ca;
+            s_fr[at][4] = static_cast<uint32_t>(la);
+            s_fr[at + 1][0] = l + 1u; s_fr[at + 1][1] = e1 | (1u << e2); s_fr[at + 1][2] = e2 + 1u;
+            s_fr[at + 1][3] = cb; s_fr[at + 1][4] = static_cast<uint32_t>(lb);
+            s_nfr = nf + 1u;
         }
+        __builtin_amdgcn_wave_barrier();
+    }
+    const uint32_t nf = s_nfr;
+    // A tree deeper than the render kernel's DFS stack must never reach it (its pushes are
+    // unchecked): the mesh is disabled in this image — no frontier parts, node count 0, so
+    // mesh_traverse / part_traverse skip it — and the update reports kErrDepth.
+    const uint32_t maxd = s_maxd;
+    const bool too_deep = maxd >= L.depth_limit || (M.status[0] & kErrDepth);
+    for (uint32_t k = lane; k < M.part_cap; k += 64u) {
+        int4 e = make_int4(-1, 0, 0, 0);
+        if (k < nf && !too_deep) {
+            const uint32_t t = s_fr[k][0];
+            const TmpNode X = M.tmp[t];
+            e = make_int4(static_cast<int>(M.mesh), static_cast<int>(M.root + ref_of(t, X)), static_cast<int>(s_fr[k][1]),
+                          static_cast<int>(s_fr[k][2]));
+        }
+        I.parts[M.part0 + k] = e;
+    }
+    if (lane == 0) {
+        uint32_t err = M.status[0];
+        if (too_deep) err |= kErrDepth;
+        const uint32_t used = 1u + 2u * s_split[0];   // nodesUsed
+        M.status[0] = err;
+        M.status[1] = maxd;
+        M.status[2] = used;
+        // the mesh record's node count (0: disabled, see too_deep)
+        I.meshes[M.mesh].y = too_deep ? 0 : static_cast<int>(used);
+        M.status[3] = nf;
+        M.status[kStFrontier] = stamp();
     }
 }
 
@@ -910,16 +1102,14 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
 
 hipError_t launch_build(const Launch& L, hipStream_t stream) {
     if (L.n == 0) return hipSuccess;
-    if (L.lds_bytes == 0) {   // a mesh too large for LDS: every mesh of the launch builds in HBM
-        hipLaunchKernelGGL(rtx_anim_build<false>, dim3(L.n), dim3(kAnimThreads), 0, stream, L);
-        return hipGetLastError();
-    }
-    if (L.lds_bytes > 64u * 1024u) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(rtx_anim_build<true>),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds_bytes));
+    const uint32_t dyn = std::max(L.top_lds * kLdsBytesTop, L.sub_lds ? kSubLdsMax * kLdsBytesSub : 0u);
+    if (dyn > 64u * 1024u) {   // dynamic LDS above 64 KB needs the attribute
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(rtx_anim_build),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(dyn));
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(rtx_anim_build<true>, dim3(L.n), dim3(kAnimThreads), L.lds_bytes, stream, L);
+    hipLaunchKernelGGL(rtx_anim_build, dim3(L.n, 1 + kMaxSub), dim3(kAnimThreads), dyn, stream, L);
+    hipLaunchKernelGGL(rtx_anim_out, dim3(kOutGroups, L.n), dim3(kAnimThreads), 0, stream, L);
     return hipGetLastError();
 }
 

@@ -534,6 +534,7 @@ constexpr int kPlaneCache = 8;   // planes whose shadow-ray numerators are kept 
 // the L2 by the time the walk's scalar load asks for it.  Issued in asm (the compiler does
 // not track it), so every touch is drained with touch_wait (s_waitcnt vmcnt(0), the walk has
 // no other vector loads) before its destination register can be reused.
+#if RTX_PREFETCH
 __device__ __forceinline__ uint32_t touch_ld(const void* base, uint32_t off) {
     const char* p = static_cast<const char*>(base) + off;
     uint32_t v;
@@ -543,6 +544,7 @@ __device__ __forceinline__ uint32_t touch_ld(const void* base, uint32_t off) {
 __device__ __forceinline__ void touch_wait(uint32_t a, uint32_t b) {
     asm volatile("s_waitcnt vmcnt(0)" ::"v"(a), "v"(b) : "memory");
 }
+#endif
 // bvh_walk without counters, shaped for the scalar unit: one inner loop descends through
 // inner nodes with scalar selects (no i1 value crosses a block, so nothing is carried as a
 // VGPR boolean or a lane-mask flow variable), a dead end leaves it as an empty "leaf", and
@@ -2584,14 +2586,14 @@ struct rtx_anim {
     float room_p0[5] = {};   // rtx_ctx::room_p0 of the registration upload
     std::string sig;
     hipEvent_t ev = nullptr;              // the last update
-    uint32_t lds_bytes = 0;               // dynamic LDS of the build launch
-    bool lds_big = false;                 // a mesh exceeds kLdsTris: the launch builds in HBM
     bool built = false;
     uint32_t cur = 0;                     // state buffer of the current order
     // rebuilt trees this deep or deeper are disabled in the image (rtxa::Launch::depth_limit);
     // RTX_ANIM_DEPTH_LIMIT lowers it for the tests of that guard
     uint32_t depth_limit = kStackDepth;
     bool reg_fast = false;                // DevScene::tri_fast condition at registration
+    bool hbm_only = false;                // RTX_ANIM_HBM=1 at registration: build records in HBM (tests)
+    uint32_t epoch = 0;                   // updates so far (the build's publication flag)
     std::vector<double> obj_radius;       // per registered mesh: max |object-space position|
 };
 
@@ -2683,6 +2685,7 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
     rtx_anim* a = new (std::nothrow) rtx_anim;
     if (!a) return RTX_E_NOMEM;
     a->device = c->device;
+    a->hbm_only = std::getenv("RTX_ANIM_HBM") != nullptr;
     if (const char* e = std::getenv("RTX_ANIM_DEPTH_LIMIT")) {
         const int v = std::atoi(e);
         if (v >= 1 && v < kStackDepth) a->depth_limit = static_cast<uint32_t>(v);
@@ -2727,16 +2730,14 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
             ANIM_CREATE_TRY(anim_alloc(a, &d.idx[k], T));
             ANIM_CREATE_TRY(anim_alloc(a, &d.nrm[k], T));
         }
-        for (int k = 0; k < 8; ++k) ANIM_CREATE_TRY(anim_alloc(a, &d.lvl[k], T));
+        for (int k = 0; k < 2; ++k) ANIM_CREATE_TRY(anim_alloc(a, &d.lvl[k], T));
+        ANIM_CREATE_TRY(anim_alloc(a, &d.sub, rtxa::kMaxSub));
         ANIM_CREATE_TRY(anim_alloc(a, &d.tnrm, T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.tnrm_out, T));
-        // build arrays in HBM as well (used when some mesh of the launch exceeds kLdsTris)
+        // build records by triangle id and the two permutation buffers
         ANIM_CREATE_TRY(anim_alloc(a, &d.soa, 9 * T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.perm[0], T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.perm[1], T));
-        // RTX_ANIM_HBM=1 builds from HBM whatever the size (tests: the large-mesh path)
-        if (T > static_cast<size_t>(rtxa::kLdsTris) || std::getenv("RTX_ANIM_HBM")) a->lds_big = true;
-        a->lds_bytes = std::max<uint32_t>(a->lds_bytes, static_cast<uint32_t>((T * rtxa::kLdsBytesPerTri + 15) / 16 * 16));
         ANIM_CREATE_TRY(anim_alloc(a, &d.lb, T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.rs, T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.rk, T));
@@ -2819,8 +2820,13 @@ extern "C" int rtx_anim_update(rtx_anim* a, rtx_ctx* c, const float* transforms)
     L.img.nodes = reinterpret_cast<float4*>(B.d + a->node_off);
     L.img.parts = reinterpret_cast<int4*>(B.d + a->part_off);
     L.img.oct_bytes = a->oct_bytes;
-    L.lds_bytes = a->lds_big ? 0u : a->lds_bytes;
     L.depth_limit = a->depth_limit;
+    L.top_lds = 0;
+    for (const rtxa::MeshDev& d : a->mesh)
+        if (d.T <= rtxa::kTopLdsTris) L.top_lds = std::max(L.top_lds, d.T);
+    if (a->hbm_only) L.top_lds = 0;
+    L.sub_lds = a->hbm_only ? 0u : 1u;
+    L.epoch = ++a->epoch;
     ANIM_TRY(a, rtxa::launch_build(L, c->stream));
     ANIM_TRY(a, hipEventRecord(a->ev, c->stream));
     a->built = true;
@@ -2865,8 +2871,10 @@ extern "C" int rtx_anim_status(rtx_anim* a, uint32_t i, uint32_t status[4]) {
     ANIM_TRY(a, hipSetDevice(a->device));
     if (a->built) ANIM_TRY(a, hipEventSynchronize(a->ev));
     ANIM_TRY(a, hipMemcpy(status, a->mesh[i].status, 16, hipMemcpyDeviceToHost));
-    if (status[0]) return afail(a, RTX_E_UNSUPPORTED, status[0] & rtxa::kErrNaN ? "NaN vertex in an animated mesh"
-                                                                                  : "animated BVH too deep for the render stack");
+    if (status[0])
+        return afail(a, RTX_E_UNSUPPORTED, status[0] & rtxa::kErrNaN       ? "NaN vertex in an animated mesh"
+                                           : status[0] & rtxa::kErrTimeout ? "device build timed out waiting for its top phase"
+                                                                            : "animated BVH too deep for the render stack");
     return RTX_OK;
 }
 

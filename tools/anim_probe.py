@@ -84,12 +84,20 @@ if len(diff):
 st = (C.c_uint32 * 128)()
 abi.check(lib.rtx_anim_stamps(an1.h, 0, st), "rtx_anim_stamps")
 w = [int(x) for x in st]
-t0 = w[8]
-us = lambda x: (x - t0) / 100.0  # noqa: E731
-lv = [us(w[10 + d]) for d in range(w[1] + 1)]
-for d in range(min(12, w[1] + 1)):
-    start_d = w[9] if d == 0 else w[10 + d - 1]
-    print(f"  level {d}: nodes huge/large/small/tiny {w[64 + 4 * d]}/{w[65 + 4 * d]}/{w[66 + 4 * d]}/{w[67 + 4 * d]}, "
-          f"huge part {(w[112 + d] - start_d) / 100:.1f} us, level {(w[10 + d] - start_d) / 100:.1f} us")
-print(f"build phases (us from start): setup {us(w[9]):.1f}, levels {[round(x, 1) for x in lv]}, "
-      f"numbered {us(w[60]):.1f}, written {us(w[61]):.1f}, frontier {us(w[62]):.1f}")
+us = lambda x: ((x - w[8]) & 0xffffffff) / 100.0  # noqa: E731  (s_memrealtime, 100 MHz)
+print(f"status: err {w[0]} deepest {w[1]} nodesUsed {w[2]} parts {w[3]} subtrees {w[4]} top nodes {w[5]} "
+      f"top levels {w[6]}")
+print(f"build phases (us from start): set-up {us(w[9]):.1f}, top levels {us(w[10]):.1f}, "
+      f"subtrees {us(w[11]):.1f} .. {us(w[12]):.1f}, output start {us(w[13]):.1f}, ranks {us(w[14]):.1f}, "
+      f"frontier {us(w[15]):.1f}")
+print("top levels end (us):", [round(us(w[20 + d]), 1) for d in range(min(8, w[6]))])
+print(f"subtree 0: staged {us(w[29]):.1f}, levels end {[round(us(x), 1) for x in w[32:56] if x]}, levels done {us(w[30]):.1f}, "
+      f"ranks {us(w[31]):.1f}")
+print(f"output wg0: records written {us(w[56]):.1f}, frontier cache {us(w[57]):.1f}")
+if w[63]:
+    print("root node steps (us from its start):", [round((w[64 + i] - w[63]) / 100.0, 1) for i in range(9)])
+if w[59] != w[58] and w[10] != w[8]:
+    print(f"shader clock during the top phase: {((w[59] - w[58]) & 0xffffffff) / (((w[10] - w[8]) & 0xffffffff) / 100.0):.0f} MHz")
+print("subtrees (start, end us):", [(round(us(w[80 + 2 * f]), 1), round(us(w[81 + 2 * f]), 1)) for f in range(min(16, w[4]))])
+print("sub workgroup entry (us):", [round(us(w[112 + f]), 1) for f in range(16)])
+print("subtree sizes:", [w[96 + f] for f in range(min(16, w[4]))])
