@@ -25,13 +25,19 @@
 
 namespace rtxa {
 
-constexpr int kAnimThreads = 1024;               // threads of every build workgroup
+#ifndef RTX_ANIM_THREADS
+#define RTX_ANIM_THREADS 1024
+#endif
+constexpr int kAnimThreads = RTX_ANIM_THREADS;   // threads of every build workgroup
 constexpr int kAnimWaves = kAnimThreads / 64;
 constexpr int kMaxAnimMeshes = 8;                // animated meshes per launch
 constexpr int kMaxAnimParts = 128;               // frontier entries per mesh (kPartsPerMesh)
-constexpr int kSubTarget = 16;                   // the top phase stops at a level this wide
-constexpr int kMaxSub = 2 * kSubTarget;          // subtrees per mesh (a level of < 16 nodes doubles at most)
-constexpr int kMaxTop = 4 * kSubTarget;          // top-phase nodes per mesh (< 2 x 16 per level, few levels)
+#ifndef RTX_ANIM_SUB_TARGET
+#define RTX_ANIM_SUB_TARGET 32
+#endif
+constexpr int kSubTarget = RTX_ANIM_SUB_TARGET;   // the top phase stops at a level this wide
+constexpr int kMaxSub = 2 * kSubTarget;          // subtrees per mesh (a level narrower than kSubTarget doubles at most)
+constexpr int kMaxTop = 4 * kSubTarget;          // top-phase nodes per mesh (the top phase stops before exceeding it)
 constexpr int kOutGroups = 16;                   // workgroups per mesh of the output launch
 
 // A node of the build tree before the reference's numbering (64 B).

@@ -80,61 +80,88 @@ __device__ __forceinline__ float min_key_value(unsigned long long k) {
 }
 __device__ __forceinline__ unsigned long long min_key_init() { return min_key(FLT_MAX, 0u); }
 
-// ---- order-free wave reductions (values only, see the header)
-__device__ __forceinline__ float wave_minf(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
-    return v;
-}
-__device__ __forceinline__ float wave_maxf(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    return v;
-}
-__device__ __forceinline__ unsigned long long wave_min64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t lo = __shfl_xor(static_cast<uint32_t>(v), o), hi = __shfl_xor(static_cast<uint32_t>(v >> 32), o);
-        const unsigned long long w = (static_cast<unsigned long long>(hi) << 32) | lo;
-        v = w < v ? w : v;
-    }
-    return v;
-}
-
 // Order-free wave reductions through DPP row shifts (lanes outside the row keep the identity)
-// and the four row results read back in order: about 11 instructions per value.
+// and the four row results read back (values only, see the header).
 template <int N>
 __device__ __forceinline__ uint32_t dpp_shr(uint32_t v, uint32_t identity) {
     return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(identity), static_cast<int>(v),
                                                              0x110 + N, 0xf, 0xf, false));
 }
-__device__ __forceinline__ float dpp_minf(float v) {
-    const uint32_t id = __float_as_uint(FLT_MAX);
-    v = fminf(v, __uint_as_float(dpp_shr<1>(__float_as_uint(v), id)));
-    v = fminf(v, __uint_as_float(dpp_shr<2>(__float_as_uint(v), id)));
-    v = fminf(v, __uint_as_float(dpp_shr<4>(__float_as_uint(v), id)));
-    v = fminf(v, __uint_as_float(dpp_shr<8>(__float_as_uint(v), id)));
-    const uint32_t u = __float_as_uint(v);
-    return fminf(fminf(__uint_as_float(__builtin_amdgcn_readlane(u, 15)), __uint_as_float(__builtin_amdgcn_readlane(u, 31))),
-                 fminf(__uint_as_float(__builtin_amdgcn_readlane(u, 47)), __uint_as_float(__builtin_amdgcn_readlane(u, 63))));
+// Batched forms: N independent values per lane reduced together, one DPP step for all of them
+// at a time (back-to-back independent DPP moves need no hazard waits; a chain per value did:
+// ~7 us per axis of the root's bins), then the four row results read back.  Order-free.
+template <int SH, int N>
+__device__ __forceinline__ void wred_step_min(float (&v)[N]) {
+    float t[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) t[i] = __uint_as_float(dpp_shr<SH>(__float_as_uint(v[i]), __float_as_uint(FLT_MAX)));
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = fminf(v[i], t[i]);
 }
-__device__ __forceinline__ float dpp_maxf(float v) {
-    const uint32_t id = __float_as_uint(FLT_MIN);
-    v = fmaxf(v, __uint_as_float(dpp_shr<1>(__float_as_uint(v), id)));
-    v = fmaxf(v, __uint_as_float(dpp_shr<2>(__float_as_uint(v), id)));
-    v = fmaxf(v, __uint_as_float(dpp_shr<4>(__float_as_uint(v), id)));
-    v = fmaxf(v, __uint_as_float(dpp_shr<8>(__float_as_uint(v), id)));
-    const uint32_t u = __float_as_uint(v);
-    return fmaxf(fmaxf(__uint_as_float(__builtin_amdgcn_readlane(u, 15)), __uint_as_float(__builtin_amdgcn_readlane(u, 31))),
-                 fmaxf(__uint_as_float(__builtin_amdgcn_readlane(u, 47)), __uint_as_float(__builtin_amdgcn_readlane(u, 63))));
+template <int SH, int N>
+__device__ __forceinline__ void wred_step_max(float (&v)[N]) {
+    float t[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) t[i] = __uint_as_float(dpp_shr<SH>(__float_as_uint(v[i]), __float_as_uint(FLT_MIN)));
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = fmaxf(v[i], t[i]);
 }
-__device__ __forceinline__ uint32_t dpp_sum(uint32_t v) {
-    v += dpp_shr<1>(v, 0u);
-    v += dpp_shr<2>(v, 0u);
-    v += dpp_shr<4>(v, 0u);
-    v += dpp_shr<8>(v, 0u);
-    return __builtin_amdgcn_readlane(v, 15) + __builtin_amdgcn_readlane(v, 31) + __builtin_amdgcn_readlane(v, 47) +
-           __builtin_amdgcn_readlane(v, 63);
+template <int SH, int N>
+__device__ __forceinline__ void wred_step_sum(uint32_t (&v)[N]) {
+    uint32_t t[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) t[i] = dpp_shr<SH>(v[i], 0u);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += t[i];
+}
+template <int SH, int N>
+__device__ __forceinline__ void wred_step_min64(unsigned long long (&v)[N]) {
+    uint32_t lo[N], hi[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        lo[i] = dpp_shr<SH>(static_cast<uint32_t>(v[i]), ~0u);
+        hi[i] = dpp_shr<SH>(static_cast<uint32_t>(v[i] >> 32), ~0u);
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const unsigned long long w = (static_cast<unsigned long long>(hi[i]) << 32) | lo[i];
+        v[i] = w < v[i] ? w : v[i];
+    }
+}
+__device__ __forceinline__ float rl(float v, int l) { return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), l)); }
+template <int N>
+__device__ __forceinline__ void wred_min(float (&v)[N]) {
+    wred_step_min<1>(v); wred_step_min<2>(v); wred_step_min<4>(v); wred_step_min<8>(v);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = fminf(fminf(rl(v[i], 15), rl(v[i], 31)), fminf(rl(v[i], 47), rl(v[i], 63)));
+}
+template <int N>
+__device__ __forceinline__ void wred_max(float (&v)[N]) {
+    wred_step_max<1>(v); wred_step_max<2>(v); wred_step_max<4>(v); wred_step_max<8>(v);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = fmaxf(fmaxf(rl(v[i], 15), rl(v[i], 31)), fmaxf(rl(v[i], 47), rl(v[i], 63)));
+}
+template <int N>
+__device__ __forceinline__ void wred_sum(uint32_t (&v)[N]) {
+    wred_step_sum<1>(v); wred_step_sum<2>(v); wred_step_sum<4>(v); wred_step_sum<8>(v);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        v[i] = __builtin_amdgcn_readlane(v[i], 15) + __builtin_amdgcn_readlane(v[i], 31) +
+               __builtin_amdgcn_readlane(v[i], 47) + __builtin_amdgcn_readlane(v[i], 63);
+}
+__device__ __forceinline__ unsigned long long rl64(unsigned long long v, int l) {
+    return (static_cast<unsigned long long>(__builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), l)) << 32) |
+           __builtin_amdgcn_readlane(static_cast<uint32_t>(v), l);
+}
+template <int N>
+__device__ __forceinline__ void wred_min64(unsigned long long (&v)[N]) {
+    wred_step_min64<1>(v); wred_step_min64<2>(v); wred_step_min64<4>(v); wred_step_min64<8>(v);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const unsigned long long r0 = rl64(v[i], 15), r1 = rl64(v[i], 31), r2 = rl64(v[i], 47), r3 = rl64(v[i], 63);
+        const unsigned long long a = r0 < r1 ? r0 : r1, b = r2 < r3 ? r2 : r3;
+        v[i] = a < b ? a : b;
+    }
 }
 
 // The build records and permutation of a build region.  Records: centroid (v0 + v1 + v2) *
@@ -157,9 +184,14 @@ struct Store {
 };
 constexpr uint32_t kLdsBytesTop = 46;    // per element: 9 record floats, 2 + 3 16-bit words
 constexpr uint32_t kLdsBytesSub = 50;    // + the element's triangle id
-constexpr uint32_t kTopLdsMax = kTopLdsTris;   // meshes up to this size run the top phase from LDS
 constexpr uint32_t kSubLdsMax = 2816;    // subtrees up to this size build from LDS
 
+#ifndef RTX_ANIM_TEAM_ELEMS
+#define RTX_ANIM_TEAM_ELEMS 96u   // a team gets another wave only for this many elements per wave
+#endif
+#ifndef RTX_ANIM_BINS_ATOMIC
+#define RTX_ANIM_BINS_ATOMIC 0   // experiment: LDS atomics into per-wave bin copies for every node
+#endif
 #ifndef RTX_ANIM_STEP_STAMPS
 #define RTX_ANIM_STEP_STAMPS 0   // diagnostics: the root node's step times in status[64..72]
 #endif
@@ -279,8 +311,12 @@ struct BoundAcc {
         m0 = fmaxf(m0, St.hi(0, e)); m1 = fmaxf(m1, St.hi(1, e)); m2 = fmaxf(m2, St.hi(2, e));
     }
     __device__ void wave() {
-        k0 = wave_min64(k0); k1 = wave_min64(k1); k2 = wave_min64(k2);
-        m0 = wave_maxf(m0); m1 = wave_maxf(m1); m2 = wave_maxf(m2);
+        unsigned long long k[3] = {k0, k1, k2};
+        float m[3] = {m0, m1, m2};
+        wred_min64(k);
+        wred_max(m);
+        k0 = k[0]; k1 = k[1]; k2 = k[2];
+        m0 = m[0]; m1 = m[1]; m2 = m[2];
     }
     // into the slot's child c: atomics (several waves) or a plain store (one wave)
     __device__ void put(Slot& sl, int c, bool atomic) const {
@@ -295,18 +331,15 @@ struct BoundAcc {
     }
 };
 
-// One axis's bins over the positions [0, n) a lane visits (tl, tl + nl, ...), folded in
-// registers (branch-free: the other bins see their fold identity), then over the wave (DPP),
-// then into the slot: atomics (several waves) or plain stores (one wave).  Order-free (see
-// the header); used where lanes hold several elements, LDS atomics per element otherwise.
-template <class ST, class PT>
-__device__ __forceinline__ void bins_private(const ST& St, const PT* src, uint32_t f0, uint32_t n, uint32_t tl,
-                                             uint32_t nl, uint32_t lane, int ax, float minB, float scale, Slot& sl,
-                                             bool atomic) {
-    uint32_t bc[kBins];
-    float bl[kBins][3], bh[kBins][3];
+template <int Q0, class ST, class PT, class SINK>
+__device__ __forceinline__ void bins_private_half(const ST& St, const PT* src, uint32_t f0, uint32_t n, uint32_t tl,
+                                                  uint32_t nl, uint32_t lane, int ax, float minB, float scale,
+                                                  const SINK& sink) {
+    constexpr int H = kBins / 2;   // bins Q0 .. Q0 + 3 (half the registers of all eight)
+    uint32_t bc[H];
+    float bl[H][3], bh[H][3];
 #pragma unroll
-    for (int q = 0; q < kBins; ++q) {
+    for (int q = 0; q < H; ++q) {
         bc[q] = 0u;
         bl[q][0] = bl[q][1] = bl[q][2] = FLT_MAX;
         bh[q][0] = bh[q][1] = bh[q][2] = FLT_MIN;
@@ -319,8 +352,8 @@ __device__ __forceinline__ void bins_private(const ST& St, const PT* src, uint32
         const float l0 = St.lo(0, e), l1 = St.lo(1, e), l2 = St.lo(2, e);
         const float h0 = St.hi(0, e), h1 = St.hi(1, e), h2 = St.hi(2, e);
 #pragma unroll
-        for (int q = 0; q < kBins; ++q) {
-            const bool h = bi == q;
+        for (int q = 0; q < H; ++q) {
+            const bool h = bi == Q0 + q;
             bc[q] += h ? 3u : 0u;
             bl[q][0] = fminf(bl[q][0], h ? l0 : FLT_MAX);
             bl[q][1] = fminf(bl[q][1], h ? l1 : FLT_MAX);
@@ -330,47 +363,80 @@ __device__ __forceinline__ void bins_private(const ST& St, const PT* src, uint32
             bh[q][2] = fmaxf(bh[q][2], h ? h2 : FLT_MIN);
         }
     }
+    wred_sum(bc);
+    wred_min(reinterpret_cast<float(&)[3 * H]>(bl));
+    wred_max(reinterpret_cast<float(&)[3 * H]>(bh));
+    if (lane == 0)
 #pragma unroll
-    for (int q = 0; q < kBins; ++q) {
-        const uint32_t c = dpp_sum(bc[q]);
-        const float a0 = dpp_minf(bl[q][0]), a1 = dpp_minf(bl[q][1]), a2 = dpp_minf(bl[q][2]);
-        const float b0 = dpp_maxf(bh[q][0]), b1 = dpp_maxf(bh[q][1]), b2 = dpp_maxf(bh[q][2]);
-        if (lane == 0) {
-            if (atomic) {
-                atomicAdd(&sl.bc[ax][q], c);
-                atomicMin(&sl.bl[ax][q][0], a0); atomicMin(&sl.bl[ax][q][1], a1); atomicMin(&sl.bl[ax][q][2], a2);
-                atomicMax(&sl.bh[ax][q][0], b0); atomicMax(&sl.bh[ax][q][1], b1); atomicMax(&sl.bh[ax][q][2], b2);
-            } else {
-                sl.bc[ax][q] = c;
-                sl.bl[ax][q][0] = a0; sl.bl[ax][q][1] = a1; sl.bl[ax][q][2] = a2;
-                sl.bh[ax][q][0] = b0; sl.bh[ax][q][1] = b1; sl.bh[ax][q][2] = b2;
-            }
-        }
+        for (int q = 0; q < H; ++q) sink.put(ax, Q0 + q, bc[q], bl[q][0], bl[q][1], bl[q][2], bh[q][0], bh[q][1], bh[q][2]);
+}
+// One axis's bins over the positions [0, n) a lane visits (tl, tl + nl, ...), folded in
+// registers (branch-free: the other bins see their fold identity), then over the wave (DPP),
+// then into the slot: atomics (several waves) or plain stores (one wave).  Order-free (see
+// the header); used where lanes hold several elements, LDS atomics per element otherwise.
+// Two passes of four bins each keep the accumulators within the 128-VGPR budget of a
+// 1,024-thread workgroup.
+// Sink of a wave's bins: a slot's bins (the team's, or the wave's own partial record that is
+// folded over the team's waves after a barrier — same-address LDS atomics from every wave of a
+// team serialised: 40 us a level).
+struct SlotSink {
+    Slot& sl;
+    __device__ void put(int ax, int b, uint32_t c, float a0, float a1, float a2, float b0, float b1, float b2) const {
+        sl.bc[ax][b] = c;
+        sl.bl[ax][b][0] = a0; sl.bl[ax][b][1] = a1; sl.bl[ax][b][2] = a2;
+        sl.bh[ax][b][0] = b0; sl.bh[ax][b][1] = b1; sl.bh[ax][b][2] = b2;
     }
+};
+template <class ST, class PT, class SINK>
+__device__ __forceinline__ void bins_private(const ST& St, const PT* src, uint32_t f0, uint32_t n, uint32_t tl,
+                                             uint32_t nl, uint32_t lane, int ax, float minB, float scale,
+                                             const SINK& sink) {
+    bins_private_half<0>(St, src, f0, n, tl, nl, lane, ax, minB, scale, sink);
+    bins_private_half<kBins / 2>(St, src, f0, n, tl, nl, lane, ax, minB, scale, sink);
 }
 
 // One node (temp id t, or none: `act` false) by one team.  b: the permutation buffer of this
 // level (depth parity); the next level's is b ^ 1.  Children are appended to rg.nxt.
 template <bool MULTI, bool LDS>
-__device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>& St, const Team& tm, Slot& sl, Level& Lv,
-                             const Region& rg, bool act, uint32_t t, uint32_t b, uint32_t sub) {
+__device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>& St, const Team& tm, Slot* slots,
+                                             Level& Lv, const Region& rg, bool act, uint32_t t, uint32_t b,
+                                             uint32_t sub) {
+    Slot& sl = slots[tm.w0];   // the team's slot; slots[w0 + 1 .. w0 + k - 1] hold partial bins
+    auto sl_of = [&](uint32_t wt) -> Slot& { return slots[tm.w0 + wt]; };
+    // diagnostics (RTX_ANIM_STEP_STAMPS): step times of the top phase's root (status 63-75)
+    // and of subtree 0's root (status 40-52)
+    int wbase = -1;
+    if (RTX_ANIM_STEP_STAMPS && act) {
+        if (blockIdx.y == 0 && t == 0) wbase = 63;
+        else if (blockIdx.y == 1 && t == M.sub[0].root) wbase = 40;
+    }
+    auto stp = [&](int off) {
+        if (RTX_ANIM_STEP_STAMPS && wbase >= 0 && tm.tl == 0) M.status[wbase + off] = stamp();
+    };
+    stp(0);
     using P = typename Store<LDS>::P;
     P* src = b ? St.perm[1] : St.perm[0];   // (selects: a dynamic index would put St in scratch)
     P* dst = b ? St.perm[0] : St.perm[1];
     const uint32_t nl = 64u * tm.k;
-    TmpNode X{};
-    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[63] = stamp();
-    if (act) X = M.tmp[t];
-    const uint32_t n = act ? X.count : 0u, first = X.first, f0 = first - St.pos0;
+    // the node's fields are wave-uniform: scalar registers (the VGPRs are the build's budget)
+    uint32_t n = 0, first = 0, depth = 0;
+    if (act) {
+        n = __builtin_amdgcn_readfirstlane(M.tmp[t].count);
+        first = __builtin_amdgcn_readfirstlane(M.tmp[t].first);
+        depth = __builtin_amdgcn_readfirstlane(M.tmp[t].depth);
+    }
+    const uint32_t f0 = first - St.pos0;
     // Subdivide's termination (idxCount <= 8) and the teams with no node: nothing but the copy
     const bool work = act && 3u * n > 8u;
     // 1. slot init
     if (work) {
         if (tm.tl < 6) sl.cb[tm.tl] = tm.tl < 3 ? FLT_MAX : FLT_MIN;
-        if (tm.tl < 3 * kBins) (&sl.bc[0][0])[tm.tl] = 0u;
-        for (uint32_t i = tm.tl; i < 3 * kBins * 3; i += nl) {
-            (&sl.bl[0][0][0])[i] = FLT_MAX;
-            (&sl.bh[0][0][0])[i] = FLT_MIN;
+        Slot& si = sl_of(RTX_ANIM_BINS_ATOMIC && MULTI ? tm.wt : 0u);   // per-wave copies (atomic bins)
+        const uint32_t li = RTX_ANIM_BINS_ATOMIC && MULTI ? tm.lane : tm.tl, ln = RTX_ANIM_BINS_ATOMIC && MULTI ? 64u : nl;
+        if (li < 3 * kBins) (&si.bc[0][0])[li] = 0u;
+        for (uint32_t i = li; i < 3 * kBins * 3; i += ln) {
+            (&si.bl[0][0][0])[i] = FLT_MAX;
+            (&si.bh[0][0][0])[i] = FLT_MIN;
         }
         if (MULTI && tm.tl < 6) {
             (&sl.cmin[0][0])[tm.tl] = min_key_init();
@@ -378,7 +444,7 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
         }
     }
     tsync<MULTI>();
-    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[64] = stamp();
+    stp(1);
     // 2. centroid bounds (FindBestSplitPlane's minBounds / maxBounds, DataTypes.h:404-419)
     if (work) {
         float a0 = FLT_MAX, a1 = FLT_MAX, a2 = FLT_MAX, b0 = FLT_MIN, b1 = FLT_MIN, b2 = FLT_MIN;
@@ -388,8 +454,11 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
             a0 = fminf(a0, x); a1 = fminf(a1, y); a2 = fminf(a2, z);
             b0 = fmaxf(b0, x); b1 = fmaxf(b1, y); b2 = fmaxf(b2, z);
         }
-        a0 = wave_minf(a0); a1 = wave_minf(a1); a2 = wave_minf(a2);
-        b0 = wave_maxf(b0); b1 = wave_maxf(b1); b2 = wave_maxf(b2);
+        float mn3[3] = {a0, a1, a2}, mx3[3] = {b0, b1, b2};
+        wred_min(mn3);
+        wred_max(mx3);
+        a0 = mn3[0]; a1 = mn3[1]; a2 = mn3[2];
+        b0 = mx3[0]; b1 = mx3[1]; b2 = mx3[2];
         if (tm.lane == 0) {
             if (MULTI) {
                 atomicMin(&sl.cb[0], a0); atomicMin(&sl.cb[1], a1); atomicMin(&sl.cb[2], a2);
@@ -400,7 +469,7 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
         }
     }
     tsync<MULTI>();
-    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[65] = stamp();
+    stp(2);
     float minB[3] = {0.f, 0.f, 0.f}, bd[3] = {0.f, 0.f, 0.f}, scale[3] = {0.f, 0.f, 0.f};
     bool live[3] = {false, false, false};
     if (work) {
@@ -413,10 +482,15 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
         }
         // 3. bins (DataTypes.h:424-440): idxCount += 3 and the box of the three vertices;
         //    in registers when lanes hold several elements, else LDS atomics per element
-        if (n > 2u * nl) {
+        if (!RTX_ANIM_BINS_ATOMIC && n > 2u * nl) {
 #pragma unroll
-            for (int ax = 0; ax < 3; ++ax)
-                if (live[ax]) bins_private(St, src, f0, n, tm.tl, nl, tm.lane, ax, minB[ax], scale[ax], sl, MULTI);
+            for (int ax = 0; ax < 3; ++ax) {
+                if (!live[ax]) continue;
+                // several waves: each its partial bins in its own slot (the team's is slots[w0]),
+                // folded below; one wave: straight into the team's slot
+                bins_private(St, src, f0, n, tm.tl, nl, tm.lane, ax, minB[ax], scale[ax], SlotSink{sl_of(tm.wt)});
+                stp(10 + ax);
+            }
         } else for (uint32_t q = tm.tl; q < n; q += nl) {
             const uint32_t e = src[f0 + q];
             const float l0 = St.lo(0, e), l1 = St.lo(1, e), l2 = St.lo(2, e);
@@ -428,14 +502,37 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
                 // static_cast<int> of x >= 0 (a NaN x only comes from a NaN vertex: flagged, bin 0)
                 int bi = x >= 0.f ? static_cast<int>(fminf(x, 2147483520.f)) : 0;
                 bi = kPlanes < bi ? kPlanes : bi;   // std::min(amountOfPlaneBins, binIdx)
-                atomicAdd(&sl.bc[ax][bi], 3u);
-                atomicMin(&sl.bl[ax][bi][0], l0); atomicMin(&sl.bl[ax][bi][1], l1); atomicMin(&sl.bl[ax][bi][2], l2);
-                atomicMax(&sl.bh[ax][bi][0], h0); atomicMax(&sl.bh[ax][bi][1], h1); atomicMax(&sl.bh[ax][bi][2], h2);
+                Slot& sw = sl_of(RTX_ANIM_BINS_ATOMIC && MULTI ? tm.wt : 0u);   // per-wave copies: folded below
+                atomicAdd(&sw.bc[ax][bi], 3u);
+                atomicMin(&sw.bl[ax][bi][0], l0); atomicMin(&sw.bl[ax][bi][1], l1); atomicMin(&sw.bl[ax][bi][2], l2);
+                atomicMax(&sw.bh[ax][bi][0], h0); atomicMax(&sw.bh[ax][bi][1], h1); atomicMax(&sw.bh[ax][bi][2], h2);
             }
         }
     }
     tsync<MULTI>();
-    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[66] = stamp();
+    if (MULTI) {   // the waves' partial bins (slots w0 .. w0 + k - 1), folded in any order (values only)
+        if (work && (RTX_ANIM_BINS_ATOMIC || n > 2u * nl))
+            for (uint32_t i = tm.tl; i < static_cast<uint32_t>(3 * kBins * 7); i += nl) {
+                const int ax = static_cast<int>(i / (kBins * 7)), b = static_cast<int>((i / 7) % kBins);
+                const int c = static_cast<int>(i % 7);
+                if (!live[ax]) continue;
+                if (c == 0) {
+                    uint32_t sum = 0;
+                    for (uint32_t k = 0; k < tm.k; ++k) sum += sl_of(k).bc[ax][b];
+                    sl.bc[ax][b] = sum;
+                } else if (c < 4) {
+                    float v = FLT_MAX;
+                    for (uint32_t k = 0; k < tm.k; ++k) v = fminf(v, sl_of(k).bl[ax][b][c - 1]);
+                    sl.bl[ax][b][c - 1] = v;
+                } else {
+                    float v = FLT_MIN;
+                    for (uint32_t k = 0; k < tm.k; ++k) v = fmaxf(v, sl_of(k).bh[ax][b][c - 4]);
+                    sl.bh[ax][b][c - 4] = v;
+                }
+            }
+        tsync<true>();
+    }
+    stp(3);
     // 4. the plane sweep (DataTypes.h:443-480): lane j < 21 evaluates plane j % 7 of axis j / 7;
     //    the reference takes the first strictly smaller cost in (axis, plane) order from FLT_MAX
     int axis = 0;
@@ -468,7 +565,11 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
                 if (cost < FLT_MAX) key = min_key(cost, j) & ~1ull;
             }
         }
-        key = wave_min64(key);
+        {
+            unsigned long long k1[1] = {key};
+            wred_min64(k1);
+            key = k1[0];
+        }
         float bestCost = FLT_MAX;
         if (key != ~0ull) {
             const uint32_t jb = static_cast<uint32_t>(key) >> 1;
@@ -478,7 +579,10 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
             pos = minB[axis] + step * static_cast<float>(i + 1);
             bestCost = min_key_value(key);
         }
-        const float noSplitCost = static_cast<float>(3u * n) * area(X.mn[0], X.mn[1], X.mn[2], X.mx[0], X.mx[1], X.mx[2]);
+        const TmpNode& X = M.tmp[t];
+        auto u = [](float v) { return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(v))); };
+        const float noSplitCost = static_cast<float>(3u * n) * area(u(X.mn[0]), u(X.mn[1]), u(X.mn[2]), u(X.mx[0]),
+                                                                    u(X.mx[1]), u(X.mx[2]));
         split = !(bestCost >= noSplitCost);   // Subdivide: `if (splitCost >= noSplitCost) return;`
     }
     // 5. the partition: per-wave blocks of positions in order
@@ -497,7 +601,7 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
     }
     if (MULTI) {
         tsync<true>();
-        if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[67] = stamp();
+        stp(4);
         if (split) {
             S = 0;
             for (uint32_t w = 0; w < tm.k; ++w) S += sl.wc[w][0];
@@ -518,7 +622,7 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
     }
     if (MULTI) {
         tsync<true>();
-        if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[68] = stamp();
+        stp(5);
         if (split)
             for (uint32_t w = 0; w < tm.k; ++w) {
                 if (w < tm.wt) lbase += sl.wc[w][1];
@@ -527,7 +631,7 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
     }
     if (split) wave_ranks(St, src, tm.lane, f0, lo, hi, pL, axis, pos, lbase, rbase);
     tsync<MULTI>();
-    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[69] = stamp();
+    stp(6);
     if (split) {
         for (uint32_t q = tm.tl; q < n; q += nl) {
             const uint32_t e = src[f0 + q];
@@ -537,7 +641,7 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
         for (uint32_t q = tm.tl; q < n; q += nl) dst[f0 + q] = src[f0 + q];   // a leaf: both buffers
     }
     tsync<MULTI>();
-    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[70] = stamp();
+    stp(7);
     // leftCount 0 or all: a leaf with the permutation applied (both buffers)
     const bool kids = split && S != 0u && S != n;
     if (split && !kids)
@@ -553,7 +657,7 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
         }
     }
     tsync<MULTI>();
-    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[71] = stamp();
+    stp(8);
     if (kids && tm.wt == 0 && tm.lane == 0) {
         const uint32_t c = atomicAdd(&Lv.ids, 2u);
         TmpNode a{}, bb{};
@@ -561,8 +665,8 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
             a.mn[q] = min_key_value(sl.cmin[0][q]); a.mx[q] = sl.cmax[0][q];
             bb.mn[q] = min_key_value(sl.cmin[1][q]); bb.mx[q] = sl.cmax[1][q];
         }
-        a.first = first; a.count = S; a.l = -1; a.depth = X.depth + 1; a.parent = static_cast<int32_t>(t); a.sub = sub;
-        bb.first = first + S; bb.count = n - S; bb.l = -1; bb.depth = X.depth + 1; bb.parent = static_cast<int32_t>(t);
+        a.first = first; a.count = S; a.l = -1; a.depth = depth + 1; a.parent = static_cast<int32_t>(t); a.sub = sub;
+        bb.first = first + S; bb.count = n - S; bb.l = -1; bb.depth = depth + 1; bb.parent = static_cast<int32_t>(t);
         bb.sub = sub;
         M.tmp[c] = a;
         M.tmp[c + 1] = bb;
@@ -573,7 +677,7 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
         atomicMax(&Lv.nmaxn, max(S, n - S));
     }
     if (MULTI) tsync<true>();   // the slot is free for the next level
-    if (RTX_ANIM_STEP_STAMPS && MULTI && t == 0 && threadIdx.x == 0) M.status[72] = stamp();
+    stp(9);
 }
 
 // The level loop over a region's list (Lv.K nodes in rg.cur) until no level remains or, with
@@ -596,11 +700,11 @@ __device__ __forceinline__ uint32_t build_levels(const MeshDev& M, const Store<L
         // team size: 16 / K waves (a power of two), fewer while the nodes are small
         uint32_t k = 1;
         while (2u * k * K <= static_cast<uint32_t>(kAnimWaves)) k *= 2u;
-        while (k > 1u && Lv.maxn < 96u * k) k /= 2u;
+        while (k > 1u && Lv.maxn < RTX_ANIM_TEAM_ELEMS * k) k /= 2u;
         if (k > 1u) {
             const Team tm{k, (wave / k) * k, wave % k, (wave % k) * 64u + lane, lane};
             const uint32_t j = wave / k;
-            node_process<true, LDS>(M, St, tm, slots[j], Lv, rg, j < K, j < K ? rg.cur[j] : 0u, b, sub);
+            node_process<true, LDS>(M, St, tm, slots, Lv, rg, j < K, j < K ? rg.cur[j] : 0u, b, sub);
         } else {
             const Team tm{1u, wave, 0u, lane, lane};
             for (;;) {
@@ -608,7 +712,7 @@ __device__ __forceinline__ uint32_t build_levels(const MeshDev& M, const Store<L
                 if (lane == 0) j = atomicAdd(&Lv.take, 1u);
                 j = __shfl(j, 0);
                 if (j >= K) break;
-                node_process<false, LDS>(M, St, tm, slots[wave], Lv, rg, true, rg.cur[j], b, sub);
+                node_process<false, LDS>(M, St, tm, slots, Lv, rg, true, rg.cur[j], b, sub);
             }
         }
         __syncthreads();
@@ -783,7 +887,7 @@ __device__ __forceinline__ void sub_phase(const Launch& L, const MeshDev& M, uin
     __syncthreads();
     Region rg{M.lvl[0] + X0.first, M.lvl[1] + X0.first};
     const uint32_t Dend = build_levels<LDS>(M, St, Lv, slots, rg, D, false, f, lvl_base, kSubLevels,
-                                            f == 0 ? M.status + 32 : nullptr, 24u);
+                                            f == 0 ? M.status + 32 : nullptr, 8u);
     if (f == 0 && tid == 0) M.status[30] = stamp();   // subtree 0: levels done
     if (LDS)   // the final order (every leaf range is current in both buffers) as triangle ids
         for (uint32_t q = tid; q < n; q += kAnimThreads) M.perm[0][X0.first + q] = gmap[St.perm[0][q]];
@@ -818,8 +922,9 @@ __device__ __forceinline__ void sub_phase(const Launch& L, const MeshDev& M, uin
         }
     }
     if (f == 0 && tid == 0) M.status[31] = stamp();   // subtree 0: ranks done
-    if (tid == 0 && f < 16u) {   // diagnostics
-        M.status[80 + 2 * f] = t_sub0; M.status[81 + 2 * f] = stamp(); M.status[96 + f] = n;
+    if (tid == 0 && f < 16u) {   // diagnostics: subtrees 0-7 start / end, subtrees 0-15 sizes
+        if (f < 8u) { M.status[80 + 2 * f] = t_sub0; M.status[81 + 2 * f] = stamp(); }
+        M.status[96 + f] = n;
     }
     if (tid == 0) {
         M.sub[f].nalloc = idend - S0.base;

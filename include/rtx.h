@@ -302,15 +302,17 @@ const char* rtx_anim_last_error(const rtx_anim* anim);
  * afterwards see the new geometry.  Build errors are reported by rtx_anim_status. */
 int rtx_anim_update(rtx_anim* anim, rtx_ctx* ctx, const float* transforms);
 /* Waits for the last update.  status = {error bits (1: NaN vertex, 2: BVH too deep for the
- * render stack; the frames rendered from it are invalid), deepest level, nodesUsed,
- * frontier parts}; returns RTX_E_UNSUPPORTED when error bits are set. */
+ * render stack, 4: a subtree workgroup timed out waiting for the top levels; the frames
+ * rendered from it are invalid), deepest level, nodesUsed, frontier parts}; returns
+ * RTX_E_UNSUPPORTED when error bits are set. */
 int rtx_anim_status(rtx_anim* anim, uint32_t i, uint32_t status[4]);
+/* Diagnostics: 128 status words of the last update of registered mesh i (0-3 as above,
+ * 4-6 subtrees / top-phase nodes / top-phase levels, 8-16 phase stamps of the device build at
+ * 100 MHz; csrc/rtx_anim.h). */
+int rtx_anim_stamps(rtx_anim* anim, uint32_t i, uint32_t out[128]);
 /* Waits for the last update and copies registered mesh i's state in the reference's own
  * form: transformedPositions (3V), indices (3T), normals (object space, 3T),
  * transformedNormals (3T), the node array pBVHNodes (3T entries).  NULL skips a part. */
-/* Diagnostics: 128 status words of the last update of registered mesh i (0-3 as above,
- * 8-62 phase stamps of the device build at 100 MHz). */
-int rtx_anim_stamps(rtx_anim* anim, uint32_t i, uint32_t out[128]);
 int rtx_anim_download(rtx_anim* anim, uint32_t i, float* positions, int32_t* indices, float* normals,
                       float* transformed_normals, rtx_bvh_node* nodes);
 

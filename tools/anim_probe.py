@@ -91,13 +91,18 @@ print(f"build phases (us from start): set-up {us(w[9]):.1f}, top levels {us(w[10
       f"subtrees {us(w[11]):.1f} .. {us(w[12]):.1f}, output start {us(w[13]):.1f}, ranks {us(w[14]):.1f}, "
       f"frontier {us(w[15]):.1f}")
 print("top levels end (us):", [round(us(w[20 + d]), 1) for d in range(min(8, w[6]))])
-print(f"subtree 0: staged {us(w[29]):.1f}, levels end {[round(us(x), 1) for x in w[32:56] if x]}, levels done {us(w[30]):.1f}, "
+print(f"subtree 0: staged {us(w[29]):.1f}, levels end {[round(us(x), 1) for x in w[32:40] if x]}, levels done {us(w[30]):.1f}, "
       f"ranks {us(w[31]):.1f}")
 print(f"output wg0: records written {us(w[56]):.1f}, frontier cache {us(w[57]):.1f}")
 if w[63]:
-    print("root node steps (us from its start):", [round((w[64 + i] - w[63]) / 100.0, 1) for i in range(9)])
+    print("top root steps (us from its start):", [round(((w[64 + i] - w[63]) & 0xffffffff) / 100.0, 1) for i in range(9)])
+if w[40]:
+    print("subtree-0 root steps (us from its start):", [round(((w[41 + i] - w[40]) & 0xffffffff) / 100.0, 1) for i in range(9)],
+          "bins/axis:", [round(((w[50 + a] - w[40]) & 0xffffffff) / 100.0, 1) for a in range(3)])
 if w[59] != w[58] and w[10] != w[8]:
     print(f"shader clock during the top phase: {((w[59] - w[58]) & 0xffffffff) / (((w[10] - w[8]) & 0xffffffff) / 100.0):.0f} MHz")
-print("subtrees (start, end us):", [(round(us(w[80 + 2 * f]), 1), round(us(w[81 + 2 * f]), 1)) for f in range(min(16, w[4]))])
+print("subtrees (start, end us):", [(round(us(w[80 + 2 * f]), 1), round(us(w[81 + 2 * f]), 1)) for f in range(min(8, w[4]))])
 print("sub workgroup entry (us):", [round(us(w[112 + f]), 1) for f in range(16)])
 print("subtree sizes:", [w[96 + f] for f in range(min(16, w[4]))])
+if w[63]:
+    print("top root bins per axis done (us from its start):", [round(((w[73 + a] - w[63]) & 0xffffffff) / 100.0, 1) for a in range(3)])
