@@ -14,9 +14,10 @@
 //                     kSubTarget nodes; those become independent subtrees, built by
 //                     workgroups (mesh, 1 + f) once the top phase is published: their levels,
 //                     then their split counts and DFS ranks
-//   2 rtx_anim_out    kOutGroups workgroups per mesh: the reference's numbering, the node
-//                   array, node records, triangle records and permuted state; workgroup 0
-//                   also the split-rendering frontier and the status words
+//   2 rtx_anim_out    kOutGroups + 1 workgroups per mesh: the reference's numbering, then the
+//                   node array, node records, triangle records and permuted state (workgroups
+//                   0 .. kOutGroups - 1) beside the split-rendering frontier and the status
+//                   words (workgroup kOutGroups)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -114,8 +115,10 @@ struct Launch {
     uint32_t top_lds;            // meshes up to this many triangles run the top phase from LDS (0: none)
     uint32_t sub_lds;            // subtrees build from LDS when they fit (0: always from HBM)
     uint32_t epoch;              // this update's number (> 0): the top phase publishes it in status[7]
+    uint32_t frontier_max;       // meshes up to this many triangles select the frontier in parallel (else serially)
 };
 constexpr uint32_t kTopLdsTris = 3136;   // the largest top_lds (rtx_anim.hip's LDS budget)
+constexpr uint32_t kFrontierHistMax = 4096;   // the largest frontier_max (the count histogram's bins)
 
 enum : uint32_t { kErrNaN = 1u, kErrDepth = 2u, kErrTimeout = 4u };
 

@@ -164,6 +164,56 @@ __device__ __forceinline__ void wred_min64(unsigned long long (&v)[N]) {
     }
 }
 
+// Transposing wave reduction of 32 values per lane, index q * 8 + c (c 0: a sum, 1-3: a
+// minimum, 4-6: a maximum, 7: unused).  Each step pairs every lane with the lane whose id
+// differs in one bit; of its current values the lane keeps one half (the upper when its bit is
+// set), sends the other half to its partner and folds what it receives into what it keeps:
+// 16 + 8 + 4 + 2 + 1 folds and one exchange of the two 32-lane halves instead of 32 full
+// reductions of 15 steps each.  Lane l ends with the wave's fold of value
+// q = 2 (l & 1) + ((l >> 1) & 1), c = 4 ((l >> 2) & 1) + 2 ((l >> 3) & 1) + ((l >> 4) & 1)
+// (lanes l and l + 32 alike).  Order-free, like the other wave reductions.
+#ifndef RTX_ANIM_BINS_TRANSPOSE
+#define RTX_ANIM_BINS_TRANSPOSE 1
+#endif
+__device__ __forceinline__ float fold_c(uint32_t c, float a, float b) {
+    return c == 0u ? a + b : (c < 4u ? fminf(a, b) : fmaxf(a, b));
+}
+template <int X>   // the value of lane l ^ X (X = 1, 2: DPP quad permutes; 4, 8, 16: LDS swizzles)
+__device__ __forceinline__ float xchg(float v) {
+    const int u = __float_as_int(v);
+    if constexpr (X == 1) return __int_as_float(__builtin_amdgcn_mov_dpp(u, 0xB1, 0xf, 0xf, false));   // [1,0,3,2]
+    else if constexpr (X == 2) return __int_as_float(__builtin_amdgcn_mov_dpp(u, 0x4E, 0xf, 0xf, false));   // [2,3,0,1]
+    else return __int_as_float(__builtin_amdgcn_ds_swizzle(u, 0x1F | (X << 10)));   // bitmask mode: and 31, xor X
+}
+template <int X, int N>
+__device__ __forceinline__ void tstep(float (&v)[32], uint32_t lane, uint32_t& cbase) {
+    constexpr int H = N / 2;
+    const bool hi = (lane & static_cast<uint32_t>(X)) != 0u;
+    float snd[H], kp[H];
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+        snd[i] = hi ? v[i] : v[i + H];
+        kp[i] = hi ? v[i + H] : v[i];
+    }
+#pragma unroll
+    for (int i = 0; i < H; ++i) snd[i] = xchg<X>(snd[i]);
+    if (N <= 8 && hi) cbase += static_cast<uint32_t>(H);   // the kept values' components
+#pragma unroll
+    for (int i = 0; i < H; ++i) v[i] = fold_c(N > 8 ? static_cast<uint32_t>(i & 7) : cbase + i, kp[i], snd[i]);
+}
+__device__ __forceinline__ float wred_transpose(float (&v)[32], uint32_t lane, uint32_t& q, uint32_t& c) {
+    uint32_t cb = 0;
+    tstep<1, 32>(v, lane, cb);
+    tstep<2, 16>(v, lane, cb);
+    tstep<4, 8>(v, lane, cb);
+    tstep<8, 4>(v, lane, cb);
+    tstep<16, 2>(v, lane, cb);
+    const float r = fold_c(cb, v[0], __shfl_xor(v[0], 32));
+    q = 2u * (lane & 1u) + ((lane >> 1) & 1u);
+    c = cb;
+    return r;
+}
+
 // The build records and permutation of a build region.  Records: centroid (v0 + v1 + v2) *
 // 0.3333f and the triangle box min(min(v0, v1), v2) / max(max(v0, v1), v2) — growing a node or
 // bin by the box equals growing it by the three vertices in order (first occurrence
@@ -363,12 +413,26 @@ __device__ __forceinline__ void bins_private_half(const ST& St, const PT* src, u
             bh[q][2] = fmaxf(bh[q][2], h ? h2 : FLT_MIN);
         }
     }
+#if RTX_ANIM_BINS_TRANSPOSE
+    float v[32];   // index q * 8 + c: c 0 the count (exact: < 2^24), 1-3 the box minimum, 4-6 its maximum
+#pragma unroll
+    for (int q = 0; q < H; ++q) {
+        v[q * 8] = static_cast<float>(bc[q]);
+        v[q * 8 + 1] = bl[q][0]; v[q * 8 + 2] = bl[q][1]; v[q * 8 + 3] = bl[q][2];
+        v[q * 8 + 4] = bh[q][0]; v[q * 8 + 5] = bh[q][1]; v[q * 8 + 6] = bh[q][2];
+        v[q * 8 + 7] = 0.f;
+    }
+    uint32_t q, c;
+    const float r = wred_transpose(v, lane, q, c);
+    if (lane < 32u && c < 7u) sink.put1(ax, Q0 + static_cast<int>(q), c, r);
+#else
     wred_sum(bc);
     wred_min(reinterpret_cast<float(&)[3 * H]>(bl));
     wred_max(reinterpret_cast<float(&)[3 * H]>(bh));
     if (lane == 0)
 #pragma unroll
         for (int q = 0; q < H; ++q) sink.put(ax, Q0 + q, bc[q], bl[q][0], bl[q][1], bl[q][2], bh[q][0], bh[q][1], bh[q][2]);
+#endif
 }
 // One axis's bins over the positions [0, n) a lane visits (tl, tl + nl, ...), folded in
 // registers (branch-free: the other bins see their fold identity), then over the wave (DPP),
@@ -385,6 +449,12 @@ struct SlotSink {
         sl.bc[ax][b] = c;
         sl.bl[ax][b][0] = a0; sl.bl[ax][b][1] = a1; sl.bl[ax][b][2] = a2;
         sl.bh[ax][b][0] = b0; sl.bh[ax][b][1] = b1; sl.bh[ax][b][2] = b2;
+    }
+    // one component c (0 the count, 1-3 the minimum, 4-6 the maximum) of bin b
+    __device__ void put1(int ax, int b, uint32_t c, float v) const {   // one store, no branches
+        uint32_t* const w = c == 0u ? &sl.bc[ax][b]
+                                    : reinterpret_cast<uint32_t*>(c < 4u ? &sl.bl[ax][b][c - 1u] : &sl.bh[ax][b][c - 4u]);
+        *w = c == 0u ? static_cast<uint32_t>(v) : __float_as_uint(v);
     }
 };
 template <class ST, class PT, class SINK>
@@ -544,20 +614,39 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
         if (j < 3u * kPlanes) {
             const int ax = static_cast<int>(j / kPlanes), i = static_cast<int>(j % kPlanes);
             if (live[ax]) {
+                // all eight bins read at once (a fixed loop, no per-lane trip counts); a bin on
+                // the other side enters as the fold identity (rmin(m, FLT_MAX) = m, and
+                // rmax(m, FLT_MIN) = m for every m >= FLT_MIN, which all maxima are)
+                uint32_t bcq[kBins];
+                float bq[kBins][6];
+#pragma unroll
+                for (int q = 0; q < kBins; ++q) {
+                    bcq[q] = sl.bc[ax][q];
+                    bq[q][0] = sl.bl[ax][q][0]; bq[q][1] = sl.bl[ax][q][1]; bq[q][2] = sl.bl[ax][q][2];
+                    bq[q][3] = sl.bh[ax][q][0]; bq[q][4] = sl.bh[ax][q][1]; bq[q][5] = sl.bh[ax][q][2];
+                }
                 int lc = 0, rc = 0;
                 float l0 = FLT_MAX, l1 = FLT_MAX, l2 = FLT_MAX, h0 = FLT_MIN, h1 = FLT_MIN, h2 = FLT_MIN;
-                for (int q = 0; q <= i; ++q) {   // leftBox.Grow(bins[q].bounds), q = 0..i
-                    lc += static_cast<int>(sl.bc[ax][q]);
-                    l0 = rmin(l0, sl.bl[ax][q][0]); l1 = rmin(l1, sl.bl[ax][q][1]); l2 = rmin(l2, sl.bl[ax][q][2]);
-                    h0 = rmax(h0, sl.bh[ax][q][0]); h1 = rmax(h1, sl.bh[ax][q][1]); h2 = rmax(h2, sl.bh[ax][q][2]);
+#pragma unroll
+                for (int q = 0; q < kBins; ++q) {   // leftBox.Grow(bins[q].bounds), q = 0..i
+                    const bool in = q <= i;
+                    lc += in ? static_cast<int>(bcq[q]) : 0;
+                    l0 = rmin(l0, in ? bq[q][0] : FLT_MAX); l1 = rmin(l1, in ? bq[q][1] : FLT_MAX);
+                    l2 = rmin(l2, in ? bq[q][2] : FLT_MAX);
+                    h0 = rmax(h0, in ? bq[q][3] : FLT_MIN); h1 = rmax(h1, in ? bq[q][4] : FLT_MIN);
+                    h2 = rmax(h2, in ? bq[q][5] : FLT_MIN);
                 }
                 const float la = area(l0, l1, l2, h0, h1, h2);
                 l0 = l1 = l2 = FLT_MAX;
                 h0 = h1 = h2 = FLT_MIN;
-                for (int q = kPlanes; q > i; --q) {   // rightBox.Grow(bins[q].bounds), q = 7..i+1
-                    rc += static_cast<int>(sl.bc[ax][q]);
-                    l0 = rmin(l0, sl.bl[ax][q][0]); l1 = rmin(l1, sl.bl[ax][q][1]); l2 = rmin(l2, sl.bl[ax][q][2]);
-                    h0 = rmax(h0, sl.bh[ax][q][0]); h1 = rmax(h1, sl.bh[ax][q][1]); h2 = rmax(h2, sl.bh[ax][q][2]);
+#pragma unroll
+                for (int q = kPlanes; q >= 0; --q) {   // rightBox.Grow(bins[q].bounds), q = 7..i+1
+                    const bool in = q > i;
+                    rc += in ? static_cast<int>(bcq[q]) : 0;
+                    l0 = rmin(l0, in ? bq[q][0] : FLT_MAX); l1 = rmin(l1, in ? bq[q][1] : FLT_MAX);
+                    l2 = rmin(l2, in ? bq[q][2] : FLT_MAX);
+                    h0 = rmax(h0, in ? bq[q][3] : FLT_MIN); h1 = rmax(h1, in ? bq[q][4] : FLT_MIN);
+                    h2 = rmax(h2, in ? bq[q][5] : FLT_MIN);
                 }
                 const float ra = area(l0, l1, l2, h0, h1, h2);
                 const float cost = static_cast<float>(lc) * la + static_cast<float>(rc) * ra;
@@ -647,14 +736,24 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
     if (split && !kids)
         for (uint32_t q = tm.tl; q < n; q += nl) src[f0 + q] = dst[f0 + q];
     // 6. UpdateNodeBounds of both children (DataTypes.h:310-321), positions in the new order
-    if (kids) {
-        for (int c = 0; c < 2; ++c) {   // one child at a time (registers)
-            BoundAcc A;
-            const uint32_t a = c ? S : 0u, z = c ? n : S;
-            for (uint32_t q = a + tm.tl; q < z; q += nl) A.add(St, dst[f0 + q], 1u + (q - a));
-            A.wave();
-            if (tm.lane == 0) A.put(sl, c, MULTI);
+    if (kids) {   // both children in one pass over the node and one batched wave reduction
+        BoundAcc A[2];
+        for (uint32_t q = tm.tl; q < n; q += nl) {
+            const bool right = q >= S;
+            const uint32_t e = dst[f0 + q];
+            if (right) A[1].add(St, e, 1u + (q - S));
+            else A[0].add(St, e, 1u + q);
         }
+        unsigned long long k[6] = {A[0].k0, A[0].k1, A[0].k2, A[1].k0, A[1].k1, A[1].k2};
+        float m[6] = {A[0].m0, A[0].m1, A[0].m2, A[1].m0, A[1].m1, A[1].m2};
+        wred_min64(k);
+        wred_max(m);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            A[c].k0 = k[3 * c]; A[c].k1 = k[3 * c + 1]; A[c].k2 = k[3 * c + 2];
+            A[c].m0 = m[3 * c]; A[c].m1 = m[3 * c + 1]; A[c].m2 = m[3 * c + 2];
+        }
+        if (tm.lane == 0) { A[0].put(sl, 0, MULTI); A[1].put(sl, 1, MULTI); }
     }
     tsync<MULTI>();
     stp(8);
@@ -984,10 +1083,244 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
 }
 
 // ============================================================ launch 3: numbering and output
-constexpr uint32_t kOutCacheIds = 8192;   // temp ids cached in LDS for the frontier walk (meshes up to 4,096 triangles)
+// The split-rendering frontier of rtx_hip.hip build_parts — split the part with the most
+// triangles (the first in frontier order on a tie) while fewer than part_cap parts exist and a
+// part is an internal node less than 31 levels deep — and the status words; workgroup
+// kOutGroups of the output launch, beside the records.
+//
+// The greedy's choices are the first part_cap - 1 eligible nodes (internal, depth < 31) in
+// (count descending, DFS preorder) order: a child holds strictly fewer triangles than its
+// parent (both sides of a split are nonempty), so when a node comes first in that order all its
+// ancestors have been split and it is in the frontier, where frontier order is DFS order.  So
+// the split set is a threshold selection — every eligible node with count > c*, and of those
+// with count == c* the lowest DFS ranks (their parents all have count > c*: at most 2 (m - 1)
+// + 1 of them) — found from a histogram of counts.  The parts are the unsplit children of the
+// split nodes (the root alone if none), ordered by their root paths read as bit strings.
+// Meshes above Launch::frontier_max (<= kFrontierHistMax) triangles keep the serial greedy over HBM.
+__device__ __forceinline__ void out_frontier(const Launch& L, const MeshDev& M, const uint32_t* s_vbase,
+                                             const uint32_t* s_base, const uint32_t* s_rank,
+                                             const uint32_t* s_subroot, uint32_t ntop, uint32_t nsub, uint32_t nvirt,
+                                             uint32_t maxd, uint32_t nused, uint32_t root_count, int32_t root_l) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t T = M.T, cap = M.part_cap;
+    auto tmap = [&](uint32_t v) -> uint32_t {   // virtual index -> temp id (the records' enumeration)
+        if (v < ntop) return v;
+        uint32_t f = 0;
+        while (v >= s_vbase[f + 1]) ++f;
+        return s_base[f] + (v - s_vbase[f]);
+    };
+    auto rank_abs = [&](uint32_t t, const TmpNode& X) -> uint32_t {
+        return t < ntop ? s_rank[t] : s_rank[s_subroot[X.sub]] + X.rank;
+    };
+    auto ref_of = [&](uint32_t t, const TmpNode& X) -> uint32_t {
+        if (t == 0) return 0u;
+        const uint32_t p = static_cast<uint32_t>(X.parent);
+        const TmpNode P = M.tmp[p];
+        return 1u + 2u * rank_abs(p, P) + (t == static_cast<uint32_t>(P.l) + 1u ? 1u : 0u);
+    };
+    __shared__ uint32_t s_fr[kMaxAnimParts + 1][4];   // parts: temp id, path bits, depth, sort key
+    __shared__ uint32_t s_nfr;
+    const uint32_t msplit = cap > 0u ? cap - 1u : 0u;   // splits wanted
+    if (T <= min(L.frontier_max, kFrontierHistMax)) {
+        __shared__ uint32_t s_hist[kFrontierHistMax + 1];
+        __shared__ uint32_t s_bits[2 * kFrontierHistMax / 32];   // split set by temp id
+        __shared__ uint32_t s_wsum[kAnimWaves];
+        __shared__ uint32_t s_sel[kMaxAnimParts], s_pidx[kMaxAnimParts], s_dep[kMaxAnimParts], s_path[kMaxAnimParts];
+        __shared__ int32_t s_sl[kMaxAnimParts];
+        __shared__ uint32_t s_tie[2 * kMaxAnimParts][2];
+        __shared__ uint32_t s_nsel, s_ntie, s_cstar, s_take, s_total;
+        for (uint32_t i = tid; i <= T; i += kAnimThreads) s_hist[i] = 0u;
+        for (uint32_t i = tid; i < 2u * kFrontierHistMax / 32u; i += kAnimThreads) s_bits[i] = 0u;
+        if (tid == 0) { s_nsel = 0; s_ntie = 0; s_cstar = ~0u; s_take = 0; s_total = 0; }
+        __syncthreads();
+        for (uint32_t v = tid; v < nvirt; v += kAnimThreads) {
+            const TmpNode& X = M.tmp[tmap(v)];
+            if (X.l >= 0 && X.depth < 31u) atomicAdd(&s_hist[X.count], 1u);
+        }
+        __syncthreads();
+        // c*: the count where the suffix sums of the histogram reach msplit
+        const uint32_t per = (T + 1u + kAnimThreads - 1u) / kAnimThreads;
+        const uint32_t b0 = min(T + 1u, tid * per), b1 = min(T + 1u, b0 + per);
+        uint32_t own = 0;
+        for (uint32_t b = b0; b < b1; ++b) own += s_hist[b];
+        uint32_t x = own;   // sum over lanes >= lane of the wave
+        for (uint32_t off = 1; off < 64u; off <<= 1) {
+            const uint32_t y = __shfl_down(x, off);
+            if (lane + off < 64u) x += y;
+        }
+        if (lane == 0) s_wsum[wave] = x;
+        __syncthreads();
+        uint32_t run = x - own;   // eligible nodes in the bins above this thread's
+        for (uint32_t w = wave + 1u; w < static_cast<uint32_t>(kAnimWaves); ++w) run += s_wsum[w];
+        if (tid == 0) s_total = run + own;
+        for (uint32_t b = b1; b > b0;) {
+            --b;
+            const uint32_t h = s_hist[b];
+            if (run < msplit && run + h >= msplit) { s_cstar = b; s_take = msplit - run; }
+            run += h;
+        }
+        __syncthreads();
+        // every eligible node if there are no more than msplit (c* stays ~0u)
+        const uint32_t cstar = s_total <= msplit ? 0u : s_cstar;
+        const bool all = s_total <= msplit;
+        for (uint32_t v = tid; v < nvirt; v += kAnimThreads) {
+            const uint32_t t = tmap(v);
+            const TmpNode& X = M.tmp[t];
+            if (!(X.l >= 0 && X.depth < 31u)) continue;
+            if (all || X.count > cstar) {
+                s_sel[atomicAdd(&s_nsel, 1u)] = t;
+                atomicOr(&s_bits[t >> 5], 1u << (t & 31u));
+            } else if (X.count == cstar) {
+                const uint32_t i = atomicAdd(&s_ntie, 1u);
+                s_tie[i][0] = t;
+                s_tie[i][1] = rank_abs(t, X);
+            }
+        }
+        __syncthreads();
+        if (!all) {   // of the ties, the s_take lowest DFS ranks
+            const uint32_t nt = s_ntie;
+            if (tid < nt) {
+                const uint32_t r = s_tie[tid][1];
+                uint32_t below = 0;
+                for (uint32_t j = 0; j < nt; ++j) below += s_tie[j][1] < r ? 1u : 0u;
+                if (below < s_take) {
+                    const uint32_t t = s_tie[tid][0];
+                    s_sel[atomicAdd(&s_nsel, 1u)] = t;
+                    atomicOr(&s_bits[t >> 5], 1u << (t & 31u));
+                }
+            }
+            __syncthreads();
+        }
+        const uint32_t nsel = s_nsel;
+        if (tid < nsel) {   // each split node's parent in the list, depth, left child, side
+            const uint32_t t = s_sel[tid];
+            const TmpNode X = M.tmp[t];
+            uint32_t pi = ~0u;
+            for (uint32_t j = 0; j < nsel; ++j)
+                if (X.parent >= 0 && s_sel[j] == static_cast<uint32_t>(X.parent)) pi = j;
+            const bool right = X.parent >= 0 && t == static_cast<uint32_t>(M.tmp[X.parent].l) + 1u;
+            s_pidx[tid] = pi;
+            s_dep[tid] = X.depth;
+            s_sl[tid] = X.l;
+            s_path[tid] = right ? 1u : 0u;   // own side for now
+        }
+        if (tid == 0) s_nfr = 0;
+        __syncthreads();
+        uint32_t path = 0;
+        if (tid < nsel)   // root path: the side of each split ancestor at its parent's depth
+            for (uint32_t p = tid, it = 0; it < 32u && p < nsel && s_dep[p] > 0u; p = s_pidx[p], ++it)   // (bounded)
+                path |= s_path[p] << (s_dep[p] - 1u);
+        __syncthreads();
+        if (tid < nsel) {
+            const uint32_t d = s_dep[tid], l = static_cast<uint32_t>(s_sl[tid]);
+            for (uint32_t c = 0; c < 2u; ++c) {
+                const uint32_t ch = l + c;
+                if (s_bits[ch >> 5] & (1u << (ch & 31u))) continue;
+                const uint32_t k = atomicAdd(&s_nfr, 1u);
+                const uint32_t pb = path | (c << d);
+                s_fr[k][0] = ch; s_fr[k][1] = pb; s_fr[k][2] = d + 1u; s_fr[k][3] = __brev(pb);
+            }
+        }
+        if (tid == 0 && nsel == 0) { s_fr[0][0] = 0; s_fr[0][1] = 0; s_fr[0][2] = 0; s_fr[0][3] = 0; s_nfr = 1; }
+        __syncthreads();
+        // frontier order: the parts' root paths as bit strings (distinct for disjoint subtrees)
+        const uint32_t nf = s_nfr;
+        uint32_t mine[3] = {0, 0, 0}, pos = 0;
+        if (tid < nf) {
+            const uint32_t key = s_fr[tid][3];
+            for (uint32_t j = 0; j < nf; ++j) pos += s_fr[j][3] < key ? 1u : 0u;
+            mine[0] = s_fr[tid][0]; mine[1] = s_fr[tid][1]; mine[2] = s_fr[tid][2];
+        }
+        __syncthreads();
+        if (tid < nf) { s_fr[pos][0] = mine[0]; s_fr[pos][1] = mine[1]; s_fr[pos][2] = mine[2]; }
+        __syncthreads();
+    } else {
+        if (wave != 0) return;
+        // the serial greedy: entries (temp id, path bits, depth, count, left child) in frontier order
+        __shared__ uint32_t s_fs[kMaxAnimParts + 1][5];
+        if (lane == 0) {
+            s_fs[0][0] = 0; s_fs[0][1] = 0; s_fs[0][2] = 0; s_fs[0][3] = root_count;
+            s_fs[0][4] = static_cast<uint32_t>(root_l);
+            s_nfr = 1;
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (;;) {
+            const uint32_t nf = s_nfr;
+            if (nf >= cap) break;
+            uint32_t key = 0, at = ~0u;   // count + 1 of an eligible entry (0: none), its index
+            for (uint32_t k = lane; k < nf; k += 64u) {
+                const uint32_t kk = (static_cast<int32_t>(s_fs[k][4]) >= 0 && s_fs[k][2] < 31u) ? s_fs[k][3] + 1u : 0u;
+                if (kk > key) { key = kk; at = k; }
+            }
+            for (uint32_t off = 32; off > 0; off >>= 1) {   // max key, lowest index
+                const uint32_t ok = __shfl_xor(key, off), oa = __shfl_xor(at, off);
+                if (ok > key || (ok == key && oa < at)) { key = ok; at = oa; }
+            }
+            if (key == 0u) break;
+            const uint32_t e1 = s_fs[at][1], e2 = s_fs[at][2], l = s_fs[at][4];
+            // entries after `at` move up by one; reads complete before the writes
+            uint32_t v[2][5];
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t k = lane + 64u * h;
+                if (k < nf)
+                    for (int c = 0; c < 5; ++c) v[h][c] = s_fs[k][c];
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t k = lane + 64u * h;
+                if (k < nf && k > at)
+                    for (int c = 0; c < 5; ++c) s_fs[k + 1][c] = v[h][c];
+            }
+            if (lane == 0) {
+                const TmpNode A = M.tmp[l], B = M.tmp[l + 1u];
+                s_fs[at][0] = l; s_fs[at][1] = e1; s_fs[at][2] = e2 + 1u; s_fs[at][3] = A.count;
+                s_fs[at][4] = static_cast<uint32_t>(A.l);
+                s_fs[at + 1][0] = l + 1u; s_fs[at + 1][1] = e1 | (1u << e2); s_fs[at + 1][2] = e2 + 1u;
+                s_fs[at + 1][3] = B.count; s_fs[at + 1][4] = static_cast<uint32_t>(B.l);
+                s_nfr = nf + 1u;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        const uint32_t nf = s_nfr;
+        for (uint32_t k = lane; k < nf; k += 64u) {
+            s_fr[k][0] = s_fs[k][0]; s_fr[k][1] = s_fs[k][1]; s_fr[k][2] = s_fs[k][2];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (wave != 0) return;
+    const Image& I = L.img;
+    const uint32_t nf = s_nfr;
+    // A tree deeper than the render kernel's DFS stack must never reach it (its pushes are
+    // unchecked): the mesh is disabled in this image — no frontier parts, node count 0, so
+    // mesh_traverse / part_traverse skip it — and the update reports kErrDepth.
+    const bool too_deep = maxd >= L.depth_limit || (M.status[0] & kErrDepth);
+    for (uint32_t k = lane; k < M.part_cap; k += 64u) {
+        int4 e = make_int4(-1, 0, 0, 0);
+        if (k < nf && !too_deep) {
+            const uint32_t t = s_fr[k][0];
+            const TmpNode X = M.tmp[t];
+            e = make_int4(static_cast<int>(M.mesh), static_cast<int>(M.root + ref_of(t, X)), static_cast<int>(s_fr[k][1]),
+                          static_cast<int>(s_fr[k][2]));
+        }
+        I.parts[M.part0 + k] = e;
+    }
+    if (lane == 0) {
+        uint32_t err = M.status[0];
+        if (too_deep) err |= kErrDepth;
+        const uint32_t used = nused;   // nodesUsed
+        M.status[0] = err;
+        M.status[1] = maxd;
+        M.status[2] = used;
+        // the mesh record's node count (0: disabled, see too_deep)
+        I.meshes[M.mesh].y = too_deep ? 0 : static_cast<int>(used);
+        M.status[3] = nf;
+        M.status[kStFrontier] = stamp();
+    }
+}
+
 __global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
     const MeshDev& M = L.meshes[blockIdx.y];
-    const uint32_t g = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t g = blockIdx.x, tid = threadIdx.x;
     const uint32_t T = M.T;
     const uint32_t nsub = M.status[4], ntop = M.status[5];
     __shared__ int32_t s_l[kMaxTop];
@@ -1028,7 +1361,7 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
         }
         s_vbase[0] = ntop;
         for (uint32_t f = 0; f < nsub; ++f) s_vbase[f + 1] = s_vbase[f] + s_nalloc[f];
-        if (g == 0) M.status[kStRanks] = stamp();
+        if (g == kOutGroups) M.status[kStRanks] = stamp();
     }
     __syncthreads();
     // absolute DFS rank of a split node (temp id t)
@@ -1044,6 +1377,11 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
     };
     const Image& I = L.img;
     const uint32_t nvirt = s_vbase[nsub];
+    if (g == kOutGroups) {   // the frontier and the status words, beside the records
+        out_frontier(L, M, s_vbase, s_base, s_rank, s_subroot, ntop, nsub, nvirt, s_maxd, 1u + 2u * s_split[0],
+                     s_count[0], s_l[0]);
+        return;
+    }
     const uint32_t stride = kOutGroups * kAnimThreads;
     // ---- the reference's node array (fields the reference writes) and the render records
     for (uint32_t v = g * kAnimThreads + tid; v < nvirt; v += stride) {
@@ -1097,110 +1435,6 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
         tr[3] = make_float4(fbits(M.mat_bits), 0.f, 0.f, 0.f);
     }
     if (g == 0 && tid == 0) M.status[56] = stamp();   // workgroup 0: records written
-    if (g != 0) return;
-    // ---- split-rendering frontier (rtx_hip.hip build_parts): split the part with the most
-    // triangles (first one on a tie) until part_cap parts or only leaves remain.  The walk
-    // reads (count, left child) of its nodes from an LDS copy of every node's (count, left
-    // child) by temp id when the mesh is small enough (2T ids), else from HBM.
-    __shared__ uint32_t s_nc[kOutCacheIds];
-    __shared__ int32_t s_nl[kOutCacheIds];
-    const bool cached = 2u * T <= kOutCacheIds;
-    if (cached)
-        for (uint32_t v = tid; v < nvirt; v += kAnimThreads) {
-            uint32_t t = v;
-            if (v >= ntop) {
-                uint32_t f = 0;
-                while (v >= s_vbase[f + 1]) ++f;
-                t = s_base[f] + (v - s_vbase[f]);
-            }
-            const TmpNode X = M.tmp[t];
-            s_nc[t] = X.count;
-            s_nl[t] = X.l;
-        }
-    __syncthreads();
-    if (tid == 0) M.status[57] = stamp();   // frontier cache loaded
-    if (wave != 0) return;
-    auto node_cl = [&](uint32_t t, uint32_t& count, int32_t& l) {
-        if (cached) { count = s_nc[t]; l = s_nl[t]; return; }
-        const TmpNode X = M.tmp[t];
-        count = X.count;
-        l = X.l;
-    };
-    __shared__ uint32_t s_fr[kMaxAnimParts + 1][5];   // temp id, path bits, depth, count, left child
-    __shared__ uint32_t s_nfr;
-    if (lane == 0) {
-        s_fr[0][0] = 0; s_fr[0][1] = 0; s_fr[0][2] = 0; s_fr[0][3] = s_count[0]; s_fr[0][4] = static_cast<uint32_t>(s_l[0]);
-        s_nfr = 1;
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (;;) {
-        const uint32_t nf = s_nfr;
-        if (nf >= M.part_cap) break;
-        uint32_t key = 0, at = ~0u;   // count + 1 of an eligible entry (0: none), its index
-        for (uint32_t k = lane; k < nf; k += 64u) {
-            const uint32_t kk = (static_cast<int32_t>(s_fr[k][4]) >= 0 && s_fr[k][2] < 31u) ? s_fr[k][3] + 1u : 0u;
-            if (kk > key) { key = kk; at = k; }
-        }
-        for (uint32_t off = 32; off > 0; off >>= 1) {   // max key, lowest index
-            const uint32_t ok = __shfl_xor(key, off), oa = __shfl_xor(at, off);
-            if (ok > key || (ok == key && oa < at)) { key = ok; at = oa; }
-        }
-        if (key == 0u) break;
-        const uint32_t e1 = s_fr[at][1], e2 = s_fr[at][2], l = s_fr[at][4];
-        // entries after `at` move up by one; reads complete before the writes
-        uint32_t v[2][5];
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t k = lane + 64u * h;
-            if (k < nf)
-                for (int c = 0; c < 5; ++c) v[h][c] = s_fr[k][c];
-        }
-        __builtin_amdgcn_wave_barrier();
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t k = lane + 64u * h;
-            if (k < nf && k > at)
-                for (int c = 0; c < 5; ++c) s_fr[k + 1][c] = v[h][c];
-        }
-        if (lane == 0) {
-            uint32_t ca, cb;
-            int32_t la, lb;
-            node_cl(l, ca, la);
-            node_cl(l + 1u, cb, lb);
-            s_fr[at][0] = l; s_fr[at][1] = e1; s_fr[at][2] = e2 + 1u; s_fr[at][3] = ca;
-            s_fr[at][4] = static_cast<uint32_t>(la);
-            s_fr[at + 1][0] = l + 1u; s_fr[at + 1][1] = e1 | (1u << e2); s_fr[at + 1][2] = e2 + 1u;
-            s_fr[at + 1][3] = cb; s_fr[at + 1][4] = static_cast<uint32_t>(lb);
-            s_nfr = nf + 1u;
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-    const uint32_t nf = s_nfr;
-    // A tree deeper than the render kernel's DFS stack must never reach it (its pushes are
-    // unchecked): the mesh is disabled in this image — no frontier parts, node count 0, so
-    // mesh_traverse / part_traverse skip it — and the update reports kErrDepth.
-    const uint32_t maxd = s_maxd;
-    const bool too_deep = maxd >= L.depth_limit || (M.status[0] & kErrDepth);
-    for (uint32_t k = lane; k < M.part_cap; k += 64u) {
-        int4 e = make_int4(-1, 0, 0, 0);
-        if (k < nf && !too_deep) {
-            const uint32_t t = s_fr[k][0];
-            const TmpNode X = M.tmp[t];
-            e = make_int4(static_cast<int>(M.mesh), static_cast<int>(M.root + ref_of(t, X)), static_cast<int>(s_fr[k][1]),
-                          static_cast<int>(s_fr[k][2]));
-        }
-        I.parts[M.part0 + k] = e;
-    }
-    if (lane == 0) {
-        uint32_t err = M.status[0];
-        if (too_deep) err |= kErrDepth;
-        const uint32_t used = 1u + 2u * s_split[0];   // nodesUsed
-        M.status[0] = err;
-        M.status[1] = maxd;
-        M.status[2] = used;
-        // the mesh record's node count (0: disabled, see too_deep)
-        I.meshes[M.mesh].y = too_deep ? 0 : static_cast<int>(used);
-        M.status[3] = nf;
-        M.status[kStFrontier] = stamp();
-    }
 }
 
 }  // namespace
@@ -1214,7 +1448,7 @@ hipError_t launch_build(const Launch& L, hipStream_t stream) {
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(rtx_anim_build, dim3(L.n, 1 + kMaxSub), dim3(kAnimThreads), dyn, stream, L);
-    hipLaunchKernelGGL(rtx_anim_out, dim3(kOutGroups, L.n), dim3(kAnimThreads), 0, stream, L);
+    hipLaunchKernelGGL(rtx_anim_out, dim3(kOutGroups + 1, L.n), dim3(kAnimThreads), 0, stream, L);
     return hipGetLastError();
 }
 

@@ -830,6 +830,8 @@ __device__ __forceinline__ uint32_t q8(float c) {
 #endif
 // DEEP: the variant for scenes whose BVH is kStackDepth or more levels deep (a DFS stack of
 // kStackDepthDeep entries per wave in LDS; fewer waves fit a CU, so it is used only then).
+// HSTK (with DEEP): the stacks in HBM instead (DevScene::hstk, any depth: the reference's
+// recursion has no limit), for trees kStackDepthDeep or more levels deep.
 // SPEC (kSpec* bits, rtx_kernels.h): uniform facts of the scene and frame the host checked at
 // launch, compiled in instead of branched on (same operations, so the same pixels; fewer
 // uniform branches, selects and registers; constant plane / mesh counts unroll their loops:
@@ -845,8 +847,8 @@ __device__ __forceinline__ uint32_t q8(float c) {
 #ifndef RTX_SPEC_WAVES_PARTIAL
 #define RTX_SPEC_WAVES_PARTIAL 7
 #endif
-template <bool COUNT, int PHASE, bool DEEP = false, int SPEC = 0>
-__global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
+template <bool COUNT, int PHASE, bool DEEP = false, int SPEC = 0, bool HSTK = false>
+__global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                                                   : ((SPEC & (kSpecOneMesh | kSpecNoMesh))
                                                          ? RTX_SPEC_WAVES
                                                          : (SPEC ? RTX_SPEC_WAVES_PARTIAL : RTX_MIN_WAVES_PER_EU)))
@@ -863,9 +865,9 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
 #define n_sph (kNoSph ? 0u : S.n_spheres)
 #define n_pl (kP5 ? 5u : S.n_planes)          // constant trip counts: the plane and mesh loops unroll
 #define n_mesh (kNoMesh ? 0u : (kOneMesh ? 1u : S.n_meshes))
-    constexpr int kDepth = DEEP ? kStackDepthDeep : kStackDepth;
+    constexpr int kDepth = HSTK ? 1 : (DEEP ? kStackDepthDeep : kStackDepth);
     __shared__ uint4 stkE[kBlockThreads / 64][kDepth];
-    __shared__ unsigned long long stkT[COUNT ? kBlockThreads / 64 : 1][COUNT ? kDepth : 1];
+    __shared__ unsigned long long stkT[(COUNT && !HSTK) ? kBlockThreads / 64 : 1][(COUNT && !HSTK) ? kDepth : 1];
     // per-lane shadow-ray plane numerators, shared by every light (see the light loop)
     __shared__ float pnumS[RTX_PNUM_CACHE ? kBlockThreads / 64 : 1][RTX_PNUM_CACHE ? kPlaneCache : 1][64];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -909,6 +911,10 @@ __global__ void __launch_bounds__(kBlockThreads, DEEP ? 2
         part = blockIdx.y;
         light = blockIdx.z;
         tile = ldc(F.heavy_list, widx);
+    }
+    if constexpr (HSTK) {   // this wave's stacks in HBM
+        stk = S.hstk + static_cast<size_t>(widx) * S.hstk_depth;
+        if (COUNT) sT = S.hstkT + static_cast<size_t>(widx) * S.hstk_depth;
     }
     const uint32_t slot = widx * 64u + lane;                 // heavy-pixel slot (PHASE > 0)
     const uint32_t per_view = F.tiles_x * F.tiles_y;
@@ -1300,6 +1306,8 @@ template __global__ void rtx_render_kernel<false, 2>(const DevScene, const Frame
 template __global__ void rtx_render_kernel<false, 3>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 0, true>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<true, 0, true>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<false, 0, true, 0, true>(const DevScene, const FrameArgs);
+template __global__ void rtx_render_kernel<true, 0, true, 0, true>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[0]>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[1]>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[2]>(const DevScene, const FrameArgs);
@@ -1546,6 +1554,11 @@ struct rtx_ctx {
     uint32_t split_parts = kPartsPerMesh;            // RTX_SPLIT_PARTS (tuning)
     bool split_ok = false;           // the uploaded scene admits split rendering
     bool deep_stack = false;         // the uploaded scene needs rtx_render_kernel<..., DEEP = true>
+    bool hbm_stack = false;          // ... with its stacks in HBM (HSTK = true): kStackDepthDeep or more levels
+    uint32_t max_depth = 0;          // deepest BVH level of the uploaded scene
+    uint4* d_hstk = nullptr;         // the HBM stacks (and the instrumented variant's masks), grown on demand
+    unsigned long long* d_hstkT = nullptr;
+    size_t hstk_entries = 0;
     int scene_spec = 0;              // kSpec* facts of the uploaded scene (kernel specialisation)
     float room_p0[5] = {};           // kSpecRoomPlanes: plane k's origin on axis kRoomAxes[k]
     bool no_spec = false;            // RTX_NO_SPEC=1: always the generic kernel (tests)
@@ -1578,7 +1591,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // Deepest DFS stack a wave can need for this BVH (pending right siblings on a path): at
 // most the depth of the deepest node, returned in `depth`.  RTX_E_INVALID for a malformed
-// tree, RTX_E_UNSUPPORTED for one deeper than the deep-stack variant handles.
+// tree.
 int bvh_depth_check(const rtx_mesh& m, std::string& why, int& depth) {
     std::vector<std::pair<uint32_t, int>> st{{0u, 0}};
     int maxd = 0;
@@ -1596,11 +1609,6 @@ int bvh_depth_check(const rtx_mesh& m, std::string& why, int& depth) {
         }
     }
     depth = maxd;
-    if (maxd >= kStackDepthDeep) {
-        why = "BVH deeper than the deep-variant device stack (" + std::to_string(maxd) + " >= " +
-              std::to_string(kStackDepthDeep) + " levels)";
-        return RTX_E_UNSUPPORTED;
-    }
     return RTX_OK;
 }
 
@@ -1753,6 +1761,8 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     if (c->h_heavy_n) (void)hipHostFree(c->h_heavy_n);
     (void)hipFree(c->d_hit_key);
     (void)hipFree(c->d_occ);
+    (void)hipFree(c->d_hstk);
+    (void)hipFree(c->d_hstkT);
     if (c->ev_heavy) (void)hipEventDestroy(c->ev_heavy);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -2038,8 +2048,11 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
     d.oct_bytes = (RTX_OCTANT && oct_ok && !std::getenv("RTX_NO_OCTANT")) ? static_cast<uint32_t>(node_bytes) : 0u;
     d.n_tris = static_cast<uint32_t>(tri.size() / 4); d.n_nodes = static_cast<uint32_t>(nodes.size() / 2);
     c->dev = d;
-    // a BVH kStackDepth or more levels deep renders with the deep-stack variant, unsplit
+    // a BVH kStackDepth or more levels deep renders with the deep-stack variant, unsplit;
+    // kStackDepthDeep or more with its stacks in HBM
     c->deep_stack = max_depth >= kStackDepth;
+    c->hbm_stack = max_depth >= kStackDepthDeep;
+    c->max_depth = static_cast<uint32_t>(max_depth);
     {   // uniform facts for the specialised kernels (kSpec*): the material kinds the geometry
         // references, every light a point light, the sphere / plane / mesh counts
         int kinds = 0;
@@ -2248,14 +2261,44 @@ void launch_phase(int v, dim3 g, hipStream_t s, const DevScene& d, const FrameAr
     }
 }
 
+// The HBM stacks of the HSTK variant: max_depth + 1 entries for each wave of a launch of
+// `groups` workgroups (sized per launch: a wave's index in it selects its stack).
+int ensure_hbm_stacks(rtx_ctx* c, uint32_t groups) {
+    const size_t depth = static_cast<size_t>(c->max_depth) + 1u;
+    const size_t need = static_cast<size_t>(groups) * kWavesPerBlock * depth;
+    constexpr size_t kEntryBytes = sizeof(uint4) + sizeof(unsigned long long);
+    if (need * kEntryBytes > (size_t(64) << 30))
+        return fail(c, RTX_E_UNSUPPORTED, "DFS stacks of a " + std::to_string(c->max_depth) + "-level BVH for this frame exceed 64 GB");
+    if (need > c->hstk_entries) {
+        (void)hipFree(c->d_hstk);
+        (void)hipFree(c->d_hstkT);
+        c->d_hstk = nullptr;
+        c->d_hstkT = nullptr;
+        c->hstk_entries = 0;
+        HIP_TRY(c, hipMalloc(&c->d_hstk, need * sizeof(uint4)));
+        HIP_TRY(c, hipMalloc(&c->d_hstkT, need * sizeof(unsigned long long)));
+        c->hstk_entries = need;
+    }
+    c->dev.hstk = c->d_hstk;
+    c->dev.hstkT = c->d_hstkT;
+    c->dev.hstk_depth = static_cast<uint32_t>(depth);
+    return RTX_OK;
+}
+
 int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
     if (grid.x == 0 || grid.y == 0) return RTX_OK;
+    if (c->hbm_stack) {
+        const int rc = ensure_hbm_stacks(c, grid.x);
+        if (rc != RTX_OK) return rc;
+    }
     if (count) {
         FrameArgs G = F;   // the instrumented variant neither reads nor feeds the schedule
         G.order = nullptr;
         G.cost = nullptr;
         G.heavy_flag = nullptr;
-        if (c->deep_stack)
+        if (c->hbm_stack)
+            hipLaunchKernelGGL((rtx_render_kernel<true, 0, true, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, G);
+        else if (c->deep_stack)
             hipLaunchKernelGGL((rtx_render_kernel<true, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, G);
         else
             hipLaunchKernelGGL((rtx_render_kernel<true, 0>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, G);
@@ -2284,7 +2327,9 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(c->ev_join, s2));
     }
-    if (c->deep_stack)
+    if (c->hbm_stack)
+        hipLaunchKernelGGL((rtx_render_kernel<false, 0, true, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
+    else if (c->deep_stack)
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
     else if (v == 0)
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecVariants[0]>), grid, dim3(kBlockThreads), 0,
@@ -2593,6 +2638,7 @@ struct rtx_anim {
     uint32_t depth_limit = kStackDepth;
     bool reg_fast = false;                // DevScene::tri_fast condition at registration
     bool hbm_only = false;                // RTX_ANIM_HBM=1 at registration: build records in HBM (tests)
+    bool serial_frontier = false;         // RTX_ANIM_SERIAL_FRONTIER=1: the frontier's serial greedy for every mesh (tests)
     uint32_t epoch = 0;                   // updates so far (the build's publication flag)
     std::vector<double> obj_radius;       // per registered mesh: max |object-space position|
 };
@@ -2686,6 +2732,7 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
     if (!a) return RTX_E_NOMEM;
     a->device = c->device;
     a->hbm_only = std::getenv("RTX_ANIM_HBM") != nullptr;
+    a->serial_frontier = std::getenv("RTX_ANIM_SERIAL_FRONTIER") != nullptr;
     if (const char* e = std::getenv("RTX_ANIM_DEPTH_LIMIT")) {
         const int v = std::atoi(e);
         if (v >= 1 && v < kStackDepth) a->depth_limit = static_cast<uint32_t>(v);
@@ -2826,6 +2873,7 @@ extern "C" int rtx_anim_update(rtx_anim* a, rtx_ctx* c, const float* transforms)
         if (d.T <= rtxa::kTopLdsTris) L.top_lds = std::max(L.top_lds, d.T);
     if (a->hbm_only) L.top_lds = 0;
     L.sub_lds = a->hbm_only ? 0u : 1u;
+    L.frontier_max = a->serial_frontier ? 0u : rtxa::kFrontierHistMax;
     L.epoch = ++a->epoch;
     ANIM_TRY(a, rtxa::launch_build(L, c->stream));
     ANIM_TRY(a, hipEventRecord(a->ev, c->stream));
@@ -2857,6 +2905,7 @@ extern "C" int rtx_anim_update(rtx_anim* a, rtx_ctx* c, const float* transforms)
     }
     c->dev.tri_fast = fast ? 1u : 0u;
     c->deep_stack = false;
+    c->hbm_stack = false;
     c->split_ok = a->split_ok;
     c->scene_spec = a->spec;
     std::memcpy(c->room_p0, a->room_p0, sizeof c->room_p0);

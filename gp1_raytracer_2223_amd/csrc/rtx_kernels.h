@@ -10,7 +10,7 @@ namespace rtxd {
 // every uploaded BVH's depth against this before accepting the scene.
 constexpr int kStackDepth = 64;
 // Deep-stack variant (BVH kStackDepth..kStackDepthDeep-1 levels deep): 16 KB of LDS per
-// wave for the stack; deeper trees are refused at upload with RTX_E_UNSUPPORTED.
+// wave for the stack; deeper trees take the variant whose stacks are in HBM (DevScene::hstk).
 constexpr int kStackDepthDeep = 1024;
 #ifndef RTX_BLOCK_THREADS
 #define RTX_BLOCK_THREADS 64
@@ -116,6 +116,11 @@ struct DevScene {
     // upload); links, counts and slots are the same in every copy.  Copy 0 is the array
     // the other slab forms read.
     uint32_t oct_bytes;
+    // DFS stacks in HBM for a BVH kStackDepthDeep or more levels deep (rtx_render_kernel<...,
+    // HSTK = true>): hstk_depth entries per wave, by the wave's index in the launch
+    uint4* hstk;
+    unsigned long long* hstkT;   // the instrumented variant's tested-lane masks
+    uint32_t hstk_depth;
 };
 
 #ifndef RTX_OCT_MAX_BYTES

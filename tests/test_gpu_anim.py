@@ -160,10 +160,15 @@ def _image(ctx):
     return buf
 
 
+@pytest.mark.parametrize("serial", [False, True], ids=["parallel_frontier", "serial_frontier"])
 @pytest.mark.parametrize("name", SCENES)
-def test_device_update_image_equals_host_built_image(name):
+def test_device_update_image_equals_host_built_image(name, serial, monkeypatch):
     """The whole scene image after device Updates equals, word for word, the image the upload
-    path lays out from the host-updated scene (registration of a second anim = host build)."""
+    path lays out from the host-updated scene (registration of a second anim = host build),
+    split-rendering parts included: selected by the count histogram (meshes up to 4,096
+    triangles) or by the serial greedy (larger meshes; forced with RTX_ANIM_SERIAL_FRONTIER=1)."""
+    if serial:
+        monkeypatch.setenv("RTX_ANIM_SERIAL_FRONTIER", "1")   # read at rtx_anim_create
     d, h = _scene(name), _scene(name)
     c1, c2 = DeviceContext(0), DeviceContext(0)
     a1 = DeviceAnimation(d, c1)

@@ -1,6 +1,6 @@
 """BVHs deeper than the default per-wave DFS stack (kStackDepth = 64 entries in LDS) render
-with the deep-stack kernel variant (kStackDepthDeep = 1024 entries), bit-exact against the
-oracle; deeper trees are refused with RTX_E_UNSUPPORTED instead of rendering wrong.
+with the deep-stack kernel variant (kStackDepthDeep = 1024 entries), and deeper ones with the
+variant whose stacks are in HBM (any depth), bit-exact against the oracle.
 
 The reference traverses recursively (Utils.h:246-288) and has no depth limit.  The scenes
 here are the Bunny scene's room, lights and camera with the bunny replaced by a mesh whose
@@ -81,7 +81,7 @@ def deep_scene(T: int):
     return s, cam, keep
 
 
-@pytest.mark.parametrize("T", [40, 65, 300, 1000])
+@pytest.mark.parametrize("T", [40, 65, 300, 1000, 1100, 2500])
 def test_deep_bvh_renders_bit_exact(gpu_ctx, T):
     s, cam, keep = deep_scene(T)
     gpu_ctx.upload(s)
@@ -97,9 +97,14 @@ def test_deep_bvh_renders_bit_exact(gpu_ctx, T):
     del keep
 
 
-def test_too_deep_bvh_is_refused(gpu_ctx):
-    s, cam, keep = deep_scene(1100)   # 1099 levels >= kStackDepthDeep
-    rc = gpu_ctx.lib.rtx_upload_scene(gpu_ctx.h, C.byref(s))
-    assert rc == abi.RTX_E_UNSUPPORTED
-    assert b"deeper" in gpu_ctx.lib.rtx_last_error(gpu_ctx.h)
+def test_hbm_stack_variant_serves_frames_of_any_size(gpu_ctx):
+    """The HBM stacks grow with the frame (one stack per wave of the launch): a larger frame
+    after a smaller one, and the smaller one again, both equal the oracle."""
+    s, cam, keep = deep_scene(1500)
+    gpu_ctx.upload(s)
+    for w, h in [(96, 64), (400, 224), (96, 64)]:
+        p = abi.make_params(w, h)
+        gpx, _ = gpu_ctx.render(cam, p)
+        rpx, _ = oracle_bind.render(s, cam, p)
+        assert np.array_equal(gpx, rpx), f"{w}x{h}"
     del keep
