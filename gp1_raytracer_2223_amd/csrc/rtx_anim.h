@@ -9,11 +9,12 @@
 // transformedNormals, which the next Update starts from — and write the result straight
 // into a scene image in the render layout of rtx_upload_scene (triangle records, the node
 // pairs with their 8 octant copies, the split-rendering frontier):
-//   1 rtx_anim_build  workgroup (mesh, 0): transforms, per-triangle build records, the top
-//                     levels of the tree (whole-workgroup teams) until a level holds
-//                     kSubTarget nodes; those become independent subtrees, built by
-//                     workgroups (mesh, 1 + f) once the top phase is published: their levels,
-//                     then their split counts and DFS ranks
+//   1 rtx_anim_build  workgroup (mesh, 0): transforms, per-triangle build records and the
+//                     root's split; then it and kWorkers more workgroups per mesh take tasks
+//                     from the mesh's queue (MeshDev::q): a node above Launch::cut triangles
+//                     is split by a whole workgroup and its children queued, a smaller one is
+//                     a subtree one workgroup builds level by level (then its split counts
+//                     and DFS ranks)
 //   2 rtx_anim_out    kOutGroups + 1 workgroups per mesh: the reference's numbering, then the
 //                   node array, node records, triangle records and permuted state (workgroups
 //                   0 .. kOutGroups - 1) beside the split-rendering frontier and the status
@@ -27,19 +28,25 @@
 namespace rtxa {
 
 #ifndef RTX_ANIM_THREADS
-#define RTX_ANIM_THREADS 1024
+#define RTX_ANIM_THREADS 512
 #endif
 constexpr int kAnimThreads = RTX_ANIM_THREADS;   // threads of every build workgroup
 constexpr int kAnimWaves = kAnimThreads / 64;
 constexpr int kMaxAnimMeshes = 8;                // animated meshes per launch
 constexpr int kMaxAnimParts = 128;               // frontier entries per mesh (kPartsPerMesh)
-#ifndef RTX_ANIM_SUB_TARGET
-#define RTX_ANIM_SUB_TARGET 32
+constexpr int kMaxTop = 256;                     // temp ids of task-split nodes and their children per mesh
+constexpr int kMaxSub = kMaxTop;                 // subtrees per mesh (each root is one of those ids)
+#ifndef RTX_ANIM_WORKERS
+#define RTX_ANIM_WORKERS 64
 #endif
-constexpr int kSubTarget = RTX_ANIM_SUB_TARGET;   // the top phase stops at a level this wide
-constexpr int kMaxSub = 2 * kSubTarget;          // subtrees per mesh (a level narrower than kSubTarget doubles at most)
-constexpr int kMaxTop = 4 * kSubTarget;          // top-phase nodes per mesh (the top phase stops before exceeding it)
+constexpr int kWorkers = RTX_ANIM_WORKERS;       // task workgroups per mesh besides (mesh, 0)
 constexpr int kOutGroups = 16;                   // workgroups per mesh of the output launch
+// The task queue of a mesh (MeshDev::q): counters, then entries {what, reserved ids, epoch, -}
+// (what: bit 31 set = a node to split, its temp id below; clear = subtree index).  head, tail
+// and done are zeroed by the output launch (and at creation); the producer sets the id counters.
+enum : uint32_t { kQHead = 0, kQTail = 1, kQTop = 2, kQSubIds = 3, kQDone = 4, kQEntries = 8 };
+constexpr uint32_t kQCap = 2 * kMaxTop + kWorkers + 8;   // entries (tasks + the workers' last pops)
+constexpr uint32_t kQWords = kQEntries + 4 * kQCap;
 
 // A node of the build tree before the reference's numbering (64 B).
 struct alignas(16) TmpNode {
@@ -49,15 +56,15 @@ struct alignas(16) TmpNode {
     uint32_t depth;
     uint32_t splits;             // split nodes in the subtree, itself included
     uint32_t rank;               // DFS preorder rank among the split nodes (relative to its subtree root)
-    int32_t parent;              // -1 for the root
-    uint32_t sub;                // subtree index (kMaxSub: a top-phase node)
+    int32_t parent;              // -1 for the root, -2 for a reserved id never used (no split)
+    uint32_t sub;                // subtree index (kMaxSub: a task-split node or a leaf child of one)
     uint32_t pad[2];
 };
 
 // Per-subtree record written by the top phase and completed by the subtree build.
 struct SubRec {
-    uint32_t root;               // temp id of the subtree root (a node of the top phase's last level)
-    uint32_t base;               // first temp id of its descendants (2 n - 2 slots reserved)
+    uint32_t root;               // temp id of the subtree root (a child of a task-split node, or the root)
+    uint32_t base;               // first temp id of its descendants (2 n - 2 slots reserved, from kMaxTop on)
     uint32_t nalloc;             // descendants allocated
     uint32_t maxd;               // deepest level reached (absolute depth)
 };
@@ -74,11 +81,12 @@ struct MeshDev {
     uint32_t* lb;                // partition scratch: left-stream wrong-side positions by rank, T
     uint32_t* rs;                // right-stream ones by rank, T
     uint32_t* rk;                // rank of each position, T
-    TmpNode* tmp;                // 2T
+    TmpNode* tmp;                // kMaxTop + 2T: task-split nodes and their children, then subtree ranges
     uint32_t* lvl[2];            // level lists (current / next), T each; a subtree uses [first, first + n)
     SubRec* sub;                 // kMaxSub
     rtx_bvh_node* ref;           // the reference's node array (3T entries, persistent)
     uint32_t* status;            // {error bits, deepest level, nodesUsed, frontier parts, ...} + stamps
+    uint32_t* q;                 // the task queue, kQWords
     uint32_t V, T;
     uint32_t mat_bits;           // material index (the triangle record's 4th float4)
     uint32_t mesh;               // mesh index in the scene
@@ -88,11 +96,12 @@ struct MeshDev {
 };
 
 // status words: 0 error bits, 1 deepest level, 2 nodesUsed, 3 frontier parts, 4 subtrees,
-// 5 top-phase nodes, 6 top-phase levels, 7 the epoch of the last published top phase; 8.. phase stamps (s_memrealtime, 100 MHz, low 32 bits):
-// 8 top start, 9 set-up done, 10 top levels done, 11 first subtree start, 12 last subtree end,
-// 13 output start, 14 numbering known (workgroup 0), 15 frontier done, 16 last output end
+// 5 task-split ids (output launch), 6 tasks split, 7 -; 8.. phase stamps (s_memrealtime, 100 MHz, low 32 bits):
+// 8 build start, 9 set-up done, 10 root split, 11 first subtree start, 12 last subtree end,
+// 13 output start, 14 numbering known (frontier workgroup), 15 frontier done; 16-19 the first
+// four task splits' sizes, 20-27 their start / end
 enum : uint32_t { kStTop0 = 8, kStSetup = 9, kStTopDone = 10, kStSub0 = 11, kStSubEnd = 12, kStOut0 = 13,
-                  kStRanks = 14, kStFrontier = 15, kStOutEnd = 16 };
+                  kStRanks = 14, kStFrontier = 15 };
 
 struct Image {                   // sections of the destination scene image
     int4* meshes;                // mesh records {root byte offset, nodesUsed, cull, material}
@@ -112,9 +121,10 @@ struct Launch {
     // kStackDepth-entry DFS stack: the build then disables the mesh in the image (node count
     // 0, no frontier parts) and reports kErrDepth.  rtxd::kStackDepth; lower only in tests.
     uint32_t depth_limit;
-    uint32_t top_lds;            // meshes up to this many triangles run the top phase from LDS (0: none)
-    uint32_t sub_lds;            // subtrees build from LDS when they fit (0: always from HBM)
-    uint32_t epoch;              // this update's number (> 0): the top phase publishes it in status[7]
+    uint32_t top_lds;            // meshes up to this many triangles split the root from LDS (0: none)
+    uint32_t sub_lds;            // tasks and subtrees build from LDS when they fit (0: always from HBM)
+    uint32_t epoch;              // this update's number (> 0): tags the queue entries it publishes
+    uint32_t cut;                // nodes above this many triangles are split as tasks, smaller ones are subtrees
     uint32_t frontier_max;       // meshes up to this many triangles select the frontier in parallel (else serially)
 };
 constexpr uint32_t kTopLdsTris = 3136;   // the largest top_lds (rtx_anim.hip's LDS budget)

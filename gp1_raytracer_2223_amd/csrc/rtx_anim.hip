@@ -2,11 +2,12 @@
 //
 // The reference rebuilds each turning mesh's BVH top-down by binned SAH (DataTypes.h:294-483):
 // per node, the centroid bounds, 8 bins per live axis, the 7-plane sweep, the in-place swap
-// partition and UpdateNodeBounds of both children.  Here the tree is grown level by level by
-// TEAMS of waves (a node per team; 16, 8, 4, 2 waves while a level is narrow, one wave per node
-// once it is wide), first for the top levels of every mesh (launch 1, one workgroup per mesh),
-// then for each of the top phase's last-level nodes as an independent subtree (launch 2, one
-// workgroup per subtree, so the build spreads over as many CUs as there are subtrees).
+// partition and UpdateNodeBounds of both children.  Here a node is processed by a TEAM of waves
+// (16, 8, 4, 2 waves for a big node, one wave per node once a level is wide).  Nodes above
+// Launch::cut triangles are split one at a time by a whole workgroup, as tasks of a per-mesh
+// queue that 65 workgroups take from (the root by the workgroup that ran the set-up); their
+// children below the cut become subtrees, each built level by level by one workgroup.  So the
+// build spreads over as many CUs as there are independent nodes, from the root's children on.
 //
 // Exactness of the folds.  The reference folds with std::min / std::max from FLT_MAX /
 // FLT_MIN, keeping the first of equal values; only a signed zero can observe that order.
@@ -20,8 +21,8 @@
 //     +0, then the fold position, the sign riding in the low bit).  Maxima start at FLT_MIN
 //     and can never be a zero: any order.
 //   * The partition is the swap loop's closed form (derivation at team_ranks), a scatter.
-// Launch 3 numbers the tree as the reference's recursion allocates it (children pairs in DFS
-// preorder of the splits) and writes the node array, the render layout and the state.
+// The output launch numbers the tree as the reference's recursion allocates it (children pairs
+// in DFS preorder of the splits) and writes the node array, the render layout and the state.
 // Built with the render library's flags (-ffp-contract=off, correctly rounded div/sqrt).
 #include <hip/hip_runtime.h>
 
@@ -468,8 +469,8 @@ __device__ __forceinline__ void bins_private(const ST& St, const PT* src, uint32
 // One node (temp id t, or none: `act` false) by one team.  b: the permutation buffer of this
 // level (depth parity); the next level's is b ^ 1.  Children are appended to rg.nxt.
 template <bool MULTI, bool LDS>
-__device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>& St, const Team& tm, Slot* slots,
-                                             Level& Lv, const Region& rg, bool act, uint32_t t, uint32_t b,
+__device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>& St, TmpNode* nodes, const Team& tm,
+                                             Slot* slots, Level& Lv, const Region& rg, bool act, uint32_t t, uint32_t b,
                                              uint32_t sub) {
     Slot& sl = slots[tm.w0];   // the team's slot; slots[w0 + 1 .. w0 + k - 1] hold partial bins
     auto sl_of = [&](uint32_t wt) -> Slot& { return slots[tm.w0 + wt]; };
@@ -477,8 +478,8 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
     // and of subtree 0's root (status 40-52)
     int wbase = -1;
     if (RTX_ANIM_STEP_STAMPS && act) {
-        if (blockIdx.y == 0 && t == 0) wbase = 63;
-        else if (blockIdx.y == 1 && t == M.sub[0].root) wbase = 40;
+        if (sub == kMaxSub && t == 0 && nodes == M.tmp) wbase = 63;
+        else if (sub == 0 && (nodes == M.tmp ? t == M.sub[0].root : t == 0)) wbase = 40;
     }
     auto stp = [&](int off) {
         if (RTX_ANIM_STEP_STAMPS && wbase >= 0 && tm.tl == 0) M.status[wbase + off] = stamp();
@@ -488,12 +489,13 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
     P* src = b ? St.perm[1] : St.perm[0];   // (selects: a dynamic index would put St in scratch)
     P* dst = b ? St.perm[0] : St.perm[1];
     const uint32_t nl = 64u * tm.k;
+    const uint32_t priv_min = 2u * nl;   // register bins when lanes hold several elements
     // the node's fields are wave-uniform: scalar registers (the VGPRs are the build's budget)
     uint32_t n = 0, first = 0, depth = 0;
     if (act) {
-        n = __builtin_amdgcn_readfirstlane(M.tmp[t].count);
-        first = __builtin_amdgcn_readfirstlane(M.tmp[t].first);
-        depth = __builtin_amdgcn_readfirstlane(M.tmp[t].depth);
+        n = __builtin_amdgcn_readfirstlane(nodes[t].count);
+        first = __builtin_amdgcn_readfirstlane(nodes[t].first);
+        depth = __builtin_amdgcn_readfirstlane(nodes[t].depth);
     }
     const uint32_t f0 = first - St.pos0;
     // Subdivide's termination (idxCount <= 8) and the teams with no node: nothing but the copy
@@ -552,7 +554,7 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
         }
         // 3. bins (DataTypes.h:424-440): idxCount += 3 and the box of the three vertices;
         //    in registers when lanes hold several elements, else LDS atomics per element
-        if (!RTX_ANIM_BINS_ATOMIC && n > 2u * nl) {
+        if (!RTX_ANIM_BINS_ATOMIC && n > priv_min) {
 #pragma unroll
             for (int ax = 0; ax < 3; ++ax) {
                 if (!live[ax]) continue;
@@ -581,7 +583,7 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
     }
     tsync<MULTI>();
     if (MULTI) {   // the waves' partial bins (slots w0 .. w0 + k - 1), folded in any order (values only)
-        if (work && (RTX_ANIM_BINS_ATOMIC || n > 2u * nl))
+        if (work && (RTX_ANIM_BINS_ATOMIC || n > priv_min))
             for (uint32_t i = tm.tl; i < static_cast<uint32_t>(3 * kBins * 7); i += nl) {
                 const int ax = static_cast<int>(i / (kBins * 7)), b = static_cast<int>((i / 7) % kBins);
                 const int c = static_cast<int>(i % 7);
@@ -668,7 +670,7 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
             pos = minB[axis] + step * static_cast<float>(i + 1);
             bestCost = min_key_value(key);
         }
-        const TmpNode& X = M.tmp[t];
+        const TmpNode& X = nodes[t];
         auto u = [](float v) { return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(v))); };
         const float noSplitCost = static_cast<float>(3u * n) * area(u(X.mn[0]), u(X.mn[1]), u(X.mn[2]), u(X.mx[0]),
                                                                     u(X.mx[1]), u(X.mx[2]));
@@ -767,9 +769,9 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
         a.first = first; a.count = S; a.l = -1; a.depth = depth + 1; a.parent = static_cast<int32_t>(t); a.sub = sub;
         bb.first = first + S; bb.count = n - S; bb.l = -1; bb.depth = depth + 1; bb.parent = static_cast<int32_t>(t);
         bb.sub = sub;
-        M.tmp[c] = a;
-        M.tmp[c + 1] = bb;
-        M.tmp[t].l = static_cast<int32_t>(c);
+        nodes[c] = a;
+        nodes[c + 1] = bb;
+        nodes[t].l = static_cast<int32_t>(c);
         const uint32_t w = atomicAdd(&Lv.next, 2u);
         rg.nxt[w] = c;
         rg.nxt[w + 1] = c + 1;
@@ -779,21 +781,21 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
     stp(9);
 }
 
-// The level loop over a region's list (Lv.K nodes in rg.cur) until no level remains or, with
-// stop_wide, the level is kSubTarget wide or would take the top phase past kMaxTop nodes.
-// depth: the level of the list's nodes.  lvl_base (optional): the first temp id created while
-// processing each level (relative to the first).
+// The level loop over a region's list (Lv.K nodes in rg.cur) until no level remains or
+// max_levels levels are done (rg.cur then lists the next level's Lv.K nodes).  depth: the level
+// of the list's nodes.  lvl_base (optional): the first temp id created while processing each
+// level (relative to the first).
 template <bool LDS>
-__device__ __forceinline__ uint32_t build_levels(const MeshDev& M, const Store<LDS>& St, Level& Lv, Slot* slots, Region& rg,
-                                 uint32_t depth, bool stop_wide, uint32_t sub, uint32_t* lvl_base, uint32_t lvl_cap,
+__device__ __forceinline__ uint32_t build_levels(const MeshDev& M, const Store<LDS>& St, TmpNode* nodes, Level& Lv,
+                                                 Slot* slots, Region& rg,
+                                 uint32_t depth, uint32_t max_levels, uint32_t sub, uint32_t* lvl_base, uint32_t lvl_cap,
                                  uint32_t* stamps = nullptr, uint32_t nstamps = 0) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t depth0 = depth;
     for (;; ++depth) {
         const uint32_t K = Lv.K;
         if (K == 0) break;
-        if (stop_wide && (K >= static_cast<uint32_t>(kSubTarget) || Lv.ids + 2u * K > static_cast<uint32_t>(kMaxTop)))
-            break;
+        if (depth - depth0 >= max_levels) break;
         if (lvl_base && tid == 0 && depth - depth0 < lvl_cap) lvl_base[depth - depth0] = Lv.ids;
         const uint32_t b = depth & 1u;
         // team size: 16 / K waves (a power of two), fewer while the nodes are small
@@ -803,7 +805,7 @@ __device__ __forceinline__ uint32_t build_levels(const MeshDev& M, const Store<L
         if (k > 1u) {
             const Team tm{k, (wave / k) * k, wave % k, (wave % k) * 64u + lane, lane};
             const uint32_t j = wave / k;
-            node_process<true, LDS>(M, St, tm, slots, Lv, rg, j < K, j < K ? rg.cur[j] : 0u, b, sub);
+            node_process<true, LDS>(M, St, nodes, tm, slots, Lv, rg, j < K, j < K ? rg.cur[j] : 0u, b, sub);
         } else {
             const Team tm{1u, wave, 0u, lane, lane};
             for (;;) {
@@ -811,7 +813,7 @@ __device__ __forceinline__ uint32_t build_levels(const MeshDev& M, const Store<L
                 if (lane == 0) j = atomicAdd(&Lv.take, 1u);
                 j = __shfl(j, 0);
                 if (j >= K) break;
-                node_process<false, LDS>(M, St, tm, slots, Lv, rg, true, rg.cur[j], b, sub);
+                node_process<false, LDS>(M, St, nodes, tm, slots, Lv, rg, true, rg.cur[j], b, sub);
             }
         }
         __syncthreads();
@@ -831,10 +833,79 @@ __device__ __forceinline__ uint32_t build_levels(const MeshDev& M, const Store<L
     return depth;
 }
 
+// ---- the task queue (MeshDev::q; single threads of a workgroup, after a barrier)
+// Publish a task: its words, then the entry's epoch with release semantics at agent scope
+// (the writes of the whole workgroup before the barrier become visible with it).
+__device__ __forceinline__ void push_task(const Launch& L, const MeshDev& M, uint32_t what, uint32_t ids) {
+    const uint32_t j = atomicAdd(&M.q[kQHead], 1u);
+    if (j >= kQCap) { atomicOr(&M.status[0], kErrTimeout); return; }   // (cannot happen: kQCap bounds the tasks)
+    uint32_t* e = M.q + kQEntries + 4u * j;
+    e[0] = what;
+    e[1] = ids;
+    __threadfence();
+    __hip_atomic_store(&e[2], L.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+// temp ids r, r + 1 reserved for a node's children: marked unused until the split writes them
+__device__ __forceinline__ void reserve_ids(const MeshDev& M, uint32_t r) {
+    for (uint32_t i = r; i < r + 2u && i < static_cast<uint32_t>(kMaxTop); ++i) {
+        M.tmp[i].parent = -2;
+        M.tmp[i].l = -1;
+        M.tmp[i].sub = kMaxSub;
+        M.tmp[i].count = 0u;
+    }
+}
+// Node t (n triangles, depth d) becomes subtree f: its descendants get 2 n - 2 temp ids
+__device__ __forceinline__ void make_subtree(const Launch& L, const MeshDev& M, uint32_t t, uint32_t n, uint32_t d) {
+    const uint32_t f = atomicAdd(&M.status[4], 1u);   // < kMaxSub: every subtree root is a distinct id < kMaxTop
+    if (f >= static_cast<uint32_t>(kMaxSub)) { atomicOr(&M.status[0], kErrTimeout); return; }   // (guard only)
+    const uint32_t base = atomicAdd(&M.q[kQSubIds], n > 1u ? 2u * n - 2u : 0u);
+    M.sub[f] = SubRec{t, base, 0u, d};
+    M.tmp[t].sub = f;
+    push_task(L, M, f, 0u);
+}
+// After node (n triangles, depth d) was processed: K = 2 children from temp id c, or a leaf.
+// A child of 3 n <= 8 indices is a leaf (Subdivide returns at once), a child above the cut a
+// split task (ids for its children reserved now), any other a subtree.  `done` counts the
+// triangles whose leaves are final: the workers stop when it reaches T.
+__device__ __forceinline__ void dispatch_children(const Launch& L, const MeshDev& M, uint32_t n, uint32_t d, uint32_t K,
+                                                  uint32_t c0, uint32_t t_start) {
+    __threadfence();
+    const uint32_t k = atomicAdd(&M.status[6], 1u);
+    if (k < 4u) {   // diagnostics: the first four splits' size, start and end
+        M.status[16 + k] = n;
+        M.status[20 + 2 * k] = t_start;
+        M.status[21 + 2 * k] = stamp();
+    }
+    if (K == 0u) {
+        atomicMax(&M.status[1], d);
+        atomicAdd(&M.q[kQDone], n);
+        return;
+    }
+    atomicMax(&M.status[1], d + 1u);
+    for (uint32_t c = c0; c < c0 + 2u; ++c) {
+        const uint32_t nc = M.tmp[c].count;
+        if (3u * nc <= 8u) {
+            atomicAdd(&M.q[kQDone], nc);
+            continue;
+        }
+        if (nc > L.cut) {
+            const uint32_t r = atomicAdd(&M.q[kQTop], 2u);
+            reserve_ids(M, r);
+            if (r + 2u <= static_cast<uint32_t>(kMaxTop)) {
+                __threadfence();
+                push_task(L, M, 0x80000000u | c, r);
+                continue;
+            }
+        }
+        make_subtree(L, M, c, nc, d + 1u);
+    }
+}
+
 // ============================================================ launch 1: set-up + top levels
 template <bool LDS>
-__device__ __forceinline__ void top_phase(const Launch& L, const MeshDev& M, Level& Lv, Slot* slots, float* dyn) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+__device__ __forceinline__ void top_phase(const Launch& L, const MeshDev& M, Level& Lv, Slot* slots, float* dyn,
+                                          uint32_t* s_list) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const float* mat = L.m[blockIdx.x];
     const uint32_t T = M.T, V = M.V;
     const int4* idx = M.idx[L.cur];
@@ -895,157 +966,222 @@ __device__ __forceinline__ void top_phase(const Launch& L, const MeshDev& M, Lev
         for (int q = 0; q < 3; ++q) { r.mn[q] = min_key_value(s0.cmin[0][q]); r.mx[q] = s0.cmax[0][q]; }
         r.first = 0; r.count = T; r.l = -1; r.depth = 0; r.parent = -1; r.sub = kMaxSub;
         M.tmp[0] = r;
-        M.lvl[0][0] = 0;
         M.status[kStSetup] = stamp();
     }
     __syncthreads();
-    // ---- Subdivide (DataTypes.h:323-389), the top levels
-    Region rg{M.lvl[0], M.lvl[1]};
-    const uint32_t D = build_levels<LDS>(M, St, Lv, slots, rg, 0u, true, kMaxSub, nullptr, 0u, M.status + 20, 8u);
-    if (LDS) {   // both permutation buffers back to HBM (subtrees stage from them, the output reads them)
-        for (uint32_t k = tid; k < T; k += kAnimThreads) {
-            M.perm[0][k] = St.perm[0][k];
-            M.perm[1][k] = St.perm[1][k];
-        }
+    // ---- Subdivide (DataTypes.h:323-389): the root's split here, its descendants as tasks
+    if (tid == 0) {
+        M.status[0] = Lv.err;
+        M.status[1] = 0u;
+        M.status[4] = 0u;
+        M.status[6] = 0u;
+        M.status[kStSub0] = 0xffffffffu;
+        M.status[kStSubEnd] = 0u;
+        M.q[kQSubIds] = kMaxTop;
     }
-    // the last level's nodes become subtrees: descendants' temp ids in disjoint ranges
-    if (wave == 0) {
-        const uint32_t K = Lv.K;
-        uint32_t base = Lv.ids;
-        for (uint32_t j0 = 0; j0 < K; j0 += 64u) {
-            const uint32_t j = j0 + lane;
-            uint32_t t = 0, need = 0;
-            if (j < K) {
-                t = rg.cur[j];
-                const uint32_t n = M.tmp[t].count;
-                need = n > 1u ? 2u * n - 2u : 0u;
-            }
-            // inclusive prefix of `need` over the wave (in j order)
-            uint32_t incl = need;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t v = __shfl_up(incl, o);
-                if (lane >= static_cast<uint32_t>(o)) incl += v;
-            }
-            if (j < K) {
-                M.sub[j] = SubRec{t, base + incl - need, 0u, D};
-                M.tmp[t].sub = j;
-            }
-            base += __shfl(incl, 63);
-        }
-        if (lane == 0) {
-            M.status[0] = Lv.err;
-            M.status[1] = K ? D : (D ? D - 1u : 0u);   // deepest level so far
-            M.status[4] = K;
-            M.status[5] = Lv.ids;
-            M.status[6] = D;
+    if (T > L.cut && !LDS) {   // the root is a task like any node (records and order in HBM)
+        __syncthreads();
+        if (tid == 0) {
+            M.q[kQTop] = 3u;   // the root's children: ids 1 and 2
+            reserve_ids(M, 1u);
             M.status[kStTopDone] = stamp();
-            M.status[59] = static_cast<uint32_t>(__builtin_amdgcn_s_memtime());
-            M.status[kStSub0] = 0xffffffffu;
-            M.status[kStSubEnd] = 0u;
+            __threadfence();
+            push_task(L, M, 0x80000000u, 1u);
+        }
+    } else if (T > L.cut) {   // (LDS: the records are staged by triangle id already)
+        if (tid == 0) {
+            M.q[kQTop] = 3u;   // the root's children: ids 1 and 2
+            reserve_ids(M, 1u);
+            Lv.ids = 1u;
+            s_list[0] = 0u;
+        }
+        __syncthreads();
+        Region rg{s_list, s_list + 2};
+        if constexpr (LDS) build_levels<LDS>(M, St, M.tmp, Lv, slots, rg, 0u, 1u, kMaxSub, nullptr, 0u);
+        // the new order (triangle ids) into both buffers (a leaf child's range is final)
+        for (uint32_t k = tid; k < T; k += kAnimThreads) {
+            const uint32_t v = LDS ? static_cast<uint32_t>(St.perm[1][k]) : M.perm[1][k];
+            if (LDS) M.perm[1][k] = v;
+            M.perm[0][k] = v;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            M.status[kStTopDone] = stamp();
+            dispatch_children(L, M, T, 0u, Lv.K, rg.cur[0], M.status[kStSetup]);
+        }
+    } else {
+        if (LDS)
+            for (uint32_t k = tid; k < T; k += kAnimThreads) M.perm[0][k] = k;
+        __syncthreads();
+        if (tid == 0) {
+            M.q[kQTop] = 1u;
+            M.status[kStTopDone] = stamp();
+            make_subtree(L, M, 0u, T, 0u);
         }
     }
 }
 
-// ============================================================ launch 2: one subtree per workgroup
+// ============================================================ tasks: one workgroup each
+// A node of more than Launch::cut triangles (what: bit 31 | temp id; ids: the two reserved for
+// its children), split once by the whole workgroup; or subtree `what`, built level by level.
+// LDS = true: the records, permutation and partition scratch staged by local element index
+// (a subtree also keeps its nodes in an LDS pool under local ids — 0 its root, 1 .. in
+// allocation order — with its level lists, written back under temp ids at the end); false:
+// everything in HBM.  One call site of the level loop per storage kind keeps the kernel's code
+// small (a single wave walking a level runs cold code otherwise).
 constexpr uint32_t kSubLevels = 256;
+constexpr uint32_t kPoolMax = 700;   // subtrees staged with their node pool: 50 + 128 + 8 bytes per element
 template <bool LDS>
-__device__ __forceinline__ void sub_phase(const Launch& L, const MeshDev& M, uint32_t f, Level& Lv, Slot* slots, uint32_t* lvl_base,
-                          float* dyn) {
+__device__ __forceinline__ void run_task(const Launch& L, const MeshDev& M, uint32_t what, uint32_t ids, Level& Lv,
+                                         Slot* slots, uint32_t* lvl_base, float* dyn, uint32_t* s_list) {
     const uint32_t tid = threadIdx.x;
-    const SubRec S0 = M.sub[f];
-    const TmpNode X0 = M.tmp[S0.root];
-    const uint32_t D = M.status[6], n = X0.count, b = D & 1u;
-    const uint32_t t_sub0 = stamp();
+    const uint32_t t_start = stamp();
+    const bool split = (what & 0x80000000u) != 0u;
+    const uint32_t f = split ? static_cast<uint32_t>(kMaxSub) : what;
+    SubRec S0{};
+    if (!split) S0 = M.sub[f];
+    const uint32_t t = split ? (what & 0x7fffffffu) : S0.root;
+    const TmpNode X0 = M.tmp[t];
+    const uint32_t D = X0.depth, n = X0.count, b = D & 1u, first = X0.first;
+    using P = typename Store<LDS>::P;
     Store<LDS> St;
     uint32_t* gmap = nullptr;
-    if (LDS) {   // stage the subtree's records by local element index
-        using P = typename Store<LDS>::P;
+    TmpNode* nodes = M.tmp;
+    Region rg = split ? Region{s_list, s_list + 2} : Region{M.lvl[0] + first, M.lvl[1] + first};
+    uint32_t root = t, ids0 = split ? ids : S0.base;
+    if (LDS) {   // stage by local element index
         gmap = reinterpret_cast<uint32_t*>(dyn + 9 * n);
         P* p16 = reinterpret_cast<P*>(gmap + n);
-        St = Store<LDS>{{p16, p16 + n}, p16 + 2 * n, p16 + 3 * n, p16 + 4 * n, dyn, n, X0.first};
+        St = Store<LDS>{{p16, p16 + n}, p16 + 2 * n, p16 + 3 * n, p16 + 4 * n, dyn, n, first};
         for (uint32_t q = tid; q < n; q += kAnimThreads) {
-            const uint32_t g = M.perm[b][X0.first + q];
+            const uint32_t g = M.perm[b][first + q];
             gmap[q] = g;
 #pragma unroll
             for (int c = 0; c < 9; ++c) dyn[c * n + q] = M.soa[c * M.T + g];
             (b ? St.perm[1] : St.perm[0])[q] = static_cast<P>(q);
         }
+        if (!split) {
+            nodes = reinterpret_cast<TmpNode*>(dyn + ((50u * n + 15u) & ~15u) / 4u);
+            uint32_t* lists = reinterpret_cast<uint32_t*>(nodes + (2u * n - 1u));
+            rg = Region{lists, lists + n};
+            root = 0u;
+            ids0 = 1u;
+            if (tid == 0) nodes[0] = X0;
+        }
     } else {
-        St = Store<LDS>{{reinterpret_cast<typename Store<LDS>::P*>(M.perm[0]),
-                         reinterpret_cast<typename Store<LDS>::P*>(M.perm[1])},
-                        reinterpret_cast<typename Store<LDS>::P*>(M.lb), reinterpret_cast<typename Store<LDS>::P*>(M.rs),
-                        reinterpret_cast<typename Store<LDS>::P*>(M.rk), M.soa, M.T, 0u};
+        St = Store<LDS>{{reinterpret_cast<P*>(M.perm[0]), reinterpret_cast<P*>(M.perm[1])}, reinterpret_cast<P*>(M.lb),
+                        reinterpret_cast<P*>(M.rs), reinterpret_cast<P*>(M.rk), M.soa, M.T, 0u};
     }
     if (tid == 0) {
-        if (f == 0) M.status[29] = stamp();   // subtree 0: staged
-        atomicMin(&M.status[kStSub0], stamp());
-        Lv.K = 1; Lv.next = 0; Lv.take = 0; Lv.maxn = n; Lv.nmaxn = 0; Lv.ids = S0.base; Lv.err = 0;
-        M.lvl[0][X0.first] = S0.root;
+        if (!split) {
+            if (f == 0) M.status[29] = stamp();   // subtree 0: staged
+            atomicMin(&M.status[kStSub0], stamp());
+        }
+        Lv.K = 1; Lv.next = 0; Lv.take = 0; Lv.maxn = n; Lv.nmaxn = 0; Lv.ids = ids0; Lv.err = 0;
+        rg.cur[0] = root;
     }
     __syncthreads();
-    Region rg{M.lvl[0] + X0.first, M.lvl[1] + X0.first};
-    const uint32_t Dend = build_levels<LDS>(M, St, Lv, slots, rg, D, false, f, lvl_base, kSubLevels,
-                                            f == 0 ? M.status + 32 : nullptr, 8u);
+    const uint32_t Dend = build_levels<LDS>(M, St, nodes, Lv, slots, rg, D, split ? 1u : ~0u, f,
+                                            split ? nullptr : lvl_base, kSubLevels,
+                                            (!split && f == 0) ? M.status + 32 : nullptr, 8u);
+    if (split) {
+        // the node's range in its new order into both buffers (a leaf child's range is final)
+        const P* dst = b ? St.perm[0] : St.perm[1];
+        uint32_t* hdst = M.perm[b ^ 1u];
+        for (uint32_t q = tid; q < n; q += kAnimThreads) {
+            const uint32_t v = LDS ? gmap[dst[q]] : hdst[first + q];
+            if (LDS) hdst[first + q] = v;
+            M.perm[b][first + q] = v;
+        }
+        __syncthreads();
+        if (tid == 0) dispatch_children(L, M, n, D, Lv.K, rg.cur[0], t_start);
+        return;
+    }
     if (f == 0 && tid == 0) M.status[30] = stamp();   // subtree 0: levels done
     if (LDS)   // the final order (every leaf range is current in both buffers) as triangle ids
-        for (uint32_t q = tid; q < n; q += kAnimThreads) M.perm[0][X0.first + q] = gmap[St.perm[0][q]];
+        for (uint32_t q = tid; q < n; q += kAnimThreads) M.perm[0][first + q] = gmap[St.perm[0][q]];
     // levels D .. Dend - 1 hold nodes: level D the root, level D + r (r >= 1) the ids
     // [lvl_base[r - 1], lvl_base[r])
     const uint32_t nlev = Dend - D, idend = Lv.ids;
     const bool ranks_ok = nlev < kSubLevels;
     if (tid == 0 && ranks_ok) lvl_base[nlev] = idend;
     __syncthreads();
-    auto lvl_lo = [&](uint32_t r) { return r == 0 ? S0.root : lvl_base[r - 1]; };
-    auto lvl_hi = [&](uint32_t r) { return r == 0 ? S0.root + 1u : lvl_base[r]; };
+    auto lvl_lo = [&](uint32_t r) { return r == 0 ? root : lvl_base[r - 1]; };
+    auto lvl_hi = [&](uint32_t r) { return r == 0 ? root + 1u : lvl_base[r]; };
     // split counts bottom-up, then the DFS preorder ranks of the split nodes top-down
     // (relative to the subtree root: its descendants' ranks follow its own)
     if (ranks_ok) {
         for (int r = static_cast<int>(nlev) - 1; r >= 0; --r) {
-            for (uint32_t t = lvl_lo(r) + tid; t < lvl_hi(r); t += kAnimThreads) {
-                const int32_t l = M.tmp[t].l;
-                M.tmp[t].splits = l >= 0 ? 1u + M.tmp[l].splits + M.tmp[l + 1].splits : 0u;
+            for (uint32_t u = lvl_lo(r) + tid; u < lvl_hi(r); u += kAnimThreads) {
+                const int32_t l = nodes[u].l;
+                nodes[u].splits = l >= 0 ? 1u + nodes[l].splits + nodes[l + 1].splits : 0u;
             }
             __syncthreads();
         }
-        if (tid == 0) M.tmp[S0.root].rank = 0u;
+        if (tid == 0) nodes[root].rank = 0u;
         __syncthreads();
         for (uint32_t r = 0; r < nlev; ++r) {
-            for (uint32_t t = lvl_lo(r) + tid; t < lvl_hi(r); t += kAnimThreads) {
-                const TmpNode X = M.tmp[t];
-                if (X.l < 0) continue;
-                M.tmp[X.l].rank = X.rank + 1u;
-                M.tmp[X.l + 1].rank = X.rank + 1u + M.tmp[X.l].splits;
+            for (uint32_t u = lvl_lo(r) + tid; u < lvl_hi(r); u += kAnimThreads) {
+                const int32_t l = nodes[u].l;
+                if (l < 0) continue;
+                const uint32_t rk = nodes[u].rank;
+                nodes[l].rank = rk + 1u;
+                nodes[l + 1].rank = rk + 1u + nodes[l].splits;
             }
             __syncthreads();
+        }
+    }
+    if (LDS) {   // the pool under temp ids: local 0 is S0.root, local i >= 1 is S0.base + i - 1
+        auto gid = [&](int32_t i) -> int32_t {
+            return i < 0 ? i : (i == 0 ? static_cast<int32_t>(S0.root) : static_cast<int32_t>(S0.base) + i - 1);
+        };
+        for (uint32_t i = 1u + tid; i < idend; i += kAnimThreads) {
+            TmpNode X = nodes[i];
+            X.l = gid(X.l);
+            X.parent = gid(X.parent);
+            M.tmp[S0.base + i - 1u] = X;
+        }
+        if (tid == 0) {
+            M.tmp[S0.root].l = gid(nodes[0].l);
+            M.tmp[S0.root].splits = nodes[0].splits;
+            M.tmp[S0.root].rank = nodes[0].rank;
         }
     }
     if (f == 0 && tid == 0) M.status[31] = stamp();   // subtree 0: ranks done
     if (tid == 0 && f < 16u) {   // diagnostics: subtrees 0-7 start / end, subtrees 0-15 sizes
-        if (f < 8u) { M.status[80 + 2 * f] = t_sub0; M.status[81 + 2 * f] = stamp(); }
+        if (f < 8u) { M.status[80 + 2 * f] = t_start; M.status[81 + 2 * f] = stamp(); }
         M.status[96 + f] = n;
     }
+    __syncthreads();
     if (tid == 0) {
-        M.sub[f].nalloc = idend - S0.base;
+        M.sub[f].nalloc = idend - ids0;
         M.sub[f].maxd = Dend - 1u;
         if (!ranks_ok) atomicOr(&M.status[0], kErrDepth);
         atomicMax(&M.status[kStSubEnd], stamp());
+        __threadfence();
+        atomicAdd(&M.q[kQDone], n);
     }
 }
 
-// One kernel: workgroup (mesh, 0) runs the set-up and the top levels; workgroups (mesh, 1 + f)
-// wait for them (an epoch flag, agent scope) and build subtree f.  One launch instead of two:
-// a kernel boundary after the top phase cost ~100 us before the first subtree workgroup ran
-// (the idle XCDs' start-up, profiles/r03).  The producers come first in dispatch order
-// (blockIdx.x fastest), so a waiting workgroup never holds back its own mesh's producer.
+// One kernel: workgroup (mesh, 0) runs the set-up and the root's split, then it and workgroups
+// (mesh, 1 .. kWorkers) take tasks from the mesh's queue until every triangle is in a final
+// leaf.  A worker takes the next entry index (atomic tail) and waits for its epoch (bounded);
+// a task is pushed only by a workgroup that runs, after its writes, so a waiting worker always
+// has a running producer (the producers of all meshes come first in dispatch order,
+// blockIdx.x fastest).  One launch with the waits in it instead of a kernel per level: a kernel
+// boundary cost ~100 us before the next workgroups ran (the idle XCDs' start-up, profiles/r03).
 constexpr uint64_t kWaitTicks = 20000000ull;   // 200 ms of s_memrealtime: a stuck build reports, never hangs
+#ifndef RTX_ANIM_POLL_SLEEP
+#define RTX_ANIM_POLL_SLEEP 8   // s_sleep units (64 clocks) between a waiting worker's polls
+#endif
 __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
     const MeshDev& M = L.meshes[blockIdx.x];
     extern __shared__ float s_dyn[];
     __shared__ Level Lv;
     __shared__ Slot slots[kAnimWaves];
     __shared__ uint32_t lvl_base[kSubLevels + 1];
-    __shared__ uint32_t s_go;
+    __shared__ uint32_t s_list[4];
+    __shared__ uint32_t s_task[3];
     const uint32_t tid = threadIdx.x;
     if (blockIdx.y == 0) {
         if (tid == 0) {
@@ -1054,32 +1190,49 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
             Lv.K = 1; Lv.next = 0; Lv.take = 0; Lv.maxn = M.T; Lv.nmaxn = 0; Lv.ids = 1; Lv.err = 0;
         }
         __syncthreads();
-        if (M.T <= L.top_lds) top_phase<true>(L, M, Lv, slots, s_dyn);
-        else top_phase<false>(L, M, Lv, slots, s_dyn);
+        if (M.T <= L.top_lds) top_phase<true>(L, M, Lv, slots, s_dyn, s_list);
+        else top_phase<false>(L, M, Lv, slots, s_dyn, s_list);
         __syncthreads();
-        if (tid == 0) {   // publish every write of the workgroup to the subtree workgroups
-            __threadfence();
-            __hip_atomic_store(&M.status[7], L.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
+    } else if (tid == 0 && blockIdx.y <= 16u) {
+        M.status[111 + blockIdx.y] = stamp();   // diagnostics: workgroup entry (workers 1-16)
     }
-    const uint32_t f = blockIdx.y - 1u;
-    if (tid == 0) {
-        if (f < 16u) M.status[112 + f] = stamp();   // diagnostics: workgroup entry
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        uint32_t ok = 1;
-        while (__hip_atomic_load(&M.status[7], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != L.epoch) {
-            __builtin_amdgcn_s_sleep(4);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) { ok = 0; break; }
+    for (;;) {
+        if (tid == 0) {
+            const uint32_t i = atomicAdd(&M.q[kQTail], 1u);
+            const uint32_t* e = M.q + kQEntries + 4u * i;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t go = 0;
+            // relaxed polls (an acquire per poll would invalidate this XCD's L2 under the
+            // running workgroups), one acquire fence once the entry is seen
+            for (;;) {
+                if (i < kQCap && __hip_atomic_load(&e[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == L.epoch) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    go = 1;
+                    s_task[0] = e[0];
+                    s_task[1] = e[1];
+                    break;
+                }
+                if (__hip_atomic_load(&M.q[kQDone], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= M.T) break;
+                __builtin_amdgcn_s_sleep(RTX_ANIM_POLL_SLEEP);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) {
+                    atomicOr(&M.status[0], kErrTimeout);
+                    break;
+                }
+            }
+            s_task[2] = go;
         }
-        if (!ok) atomicOr(&M.status[0], kErrTimeout);
-        s_go = ok;
+        __syncthreads();
+        const uint32_t what = s_task[0], ids = s_task[1], go = s_task[2];
+        __syncthreads();
+        if (!go) return;
+        const bool split = (what & 0x80000000u) != 0u;
+        const uint32_t n = M.tmp[split ? (what & 0x7fffffffu) : M.sub[what].root].count;
+        if (L.sub_lds && n <= (split ? kSubLdsMax : kPoolMax))
+            run_task<true>(L, M, what, ids, Lv, slots, lvl_base, s_dyn, s_list);
+        else
+            run_task<false>(L, M, what, ids, Lv, slots, lvl_base, s_dyn, s_list);
+        __syncthreads();
     }
-    __syncthreads();
-    if (!s_go || f >= M.status[4]) return;
-    const uint32_t n = M.tmp[M.sub[f].root].count;
-    if (L.sub_lds && n <= kSubLdsMax) sub_phase<true>(L, M, f, Lv, slots, lvl_base, s_dyn);
-    else sub_phase<false>(L, M, f, Lv, slots, lvl_base, s_dyn);
 }
 
 // ============================================================ launch 3: numbering and output
@@ -1105,8 +1258,12 @@ __device__ __forceinline__ void out_frontier(const Launch& L, const MeshDev& M, 
     const uint32_t T = M.T, cap = M.part_cap;
     auto tmap = [&](uint32_t v) -> uint32_t {   // virtual index -> temp id (the records' enumeration)
         if (v < ntop) return v;
-        uint32_t f = 0;
-        while (v >= s_vbase[f + 1]) ++f;
+        uint32_t f = 0, hi = nsub;   // the last subtree whose range starts at or before v
+        while (hi - f > 1u) {
+            const uint32_t mid = (f + hi) >> 1;
+            if (s_vbase[mid] <= v) f = mid;
+            else hi = mid;
+        }
         return s_base[f] + (v - s_vbase[f]);
     };
     auto rank_abs = [&](uint32_t t, const TmpNode& X) -> uint32_t {
@@ -1314,6 +1471,11 @@ __device__ __forceinline__ void out_frontier(const Launch& L, const MeshDev& M, 
         // the mesh record's node count (0: disabled, see too_deep)
         I.meshes[M.mesh].y = too_deep ? 0 : static_cast<int>(used);
         M.status[3] = nf;
+        M.status[5] = ntop;
+        // the next update's queue starts empty (every build workgroup has ended: kernel order)
+        M.q[kQHead] = 0u;
+        M.q[kQTail] = 0u;
+        M.q[kQDone] = 0u;
         M.status[kStFrontier] = stamp();
     }
 }
@@ -1322,14 +1484,14 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
     const MeshDev& M = L.meshes[blockIdx.y];
     const uint32_t g = blockIdx.x, tid = threadIdx.x;
     const uint32_t T = M.T;
-    const uint32_t nsub = M.status[4], ntop = M.status[5];
+    const uint32_t nsub = M.status[4], ntop = min(M.q[kQTop], static_cast<uint32_t>(kMaxTop));
     __shared__ int32_t s_l[kMaxTop];
     __shared__ uint32_t s_split[kMaxTop], s_rank[kMaxTop], s_count[kMaxTop];
     __shared__ uint32_t s_subroot[kMaxSub], s_base[kMaxSub], s_nalloc[kMaxSub], s_smaxd[kMaxSub], s_vbase[kMaxSub + 1];
     __shared__ uint8_t s_isroot[kMaxTop];
     __shared__ uint32_t s_maxd;
     if (g == 0 && tid == 0) M.status[kStOut0] = stamp();
-    // ---- the top nodes' split counts (bottom-up, subtree roots from launch 2) and ranks
+    // ---- the task-split nodes' split counts (bottom-up, subtree roots from their builds) and ranks
     for (uint32_t t = tid; t < ntop; t += kAnimThreads) {
         const TmpNode X = M.tmp[t];
         s_l[t] = X.l;
@@ -1346,7 +1508,7 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
         uint32_t maxd = M.status[1];
         for (uint32_t f = 0; f < nsub; ++f) maxd = max(maxd, s_smaxd[f]);
         s_maxd = maxd;
-        // top nodes are numbered in creation order (parents before children)
+        // task-split ids are allocated after their parents' (parents before children)
         for (int t = static_cast<int>(ntop) - 1; t >= 0; --t) {
             const int32_t l = s_l[t];
             if (!s_isroot[t]) s_split[t] = l >= 0 ? 1u + s_split[l] + s_split[l + 1] : 0u;
@@ -1387,11 +1549,16 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
     for (uint32_t v = g * kAnimThreads + tid; v < nvirt; v += stride) {
         uint32_t t = v;
         if (v >= ntop) {
-            uint32_t f = 0;
-            while (v >= s_vbase[f + 1]) ++f;
+            uint32_t f = 0, hi = nsub;   // the last subtree whose range starts at or before v
+            while (hi - f > 1u) {
+                const uint32_t mid = (f + hi) >> 1;
+                if (s_vbase[mid] <= v) f = mid;
+                else hi = mid;
+            }
             t = s_base[f] + (v - s_vbase[f]);
         }
         const TmpNode X = M.tmp[t];
+        if (X.parent == -2) continue;   // an id reserved for children of a node that did not split
         const uint32_t ref = ref_of(t, X);
         rtx_bvh_node& R = M.ref[ref];
 #pragma unroll
@@ -1447,7 +1614,7 @@ hipError_t launch_build(const Launch& L, hipStream_t stream) {
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(dyn));
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(rtx_anim_build, dim3(L.n, 1 + kMaxSub), dim3(kAnimThreads), dyn, stream, L);
+    hipLaunchKernelGGL(rtx_anim_build, dim3(L.n, 1 + kWorkers), dim3(kAnimThreads), dyn, stream, L);
     hipLaunchKernelGGL(rtx_anim_out, dim3(kOutGroups + 1, L.n), dim3(kAnimThreads), 0, stream, L);
     return hipGetLastError();
 }

@@ -2616,6 +2616,10 @@ extern "C" int rtx_debug_stamps(rtx_ctx* c, const rtx_camera* cam, const rtx_ren
 // meshes and keeps that image as a template; an update copies the template into the
 // context's next scene image and lets the build kernel overwrite the animated meshes'
 // triangle records, node pairs (+ octant copies) and frontier parts.
+// Device Update: nodes above this many triangles are split by a whole workgroup as queue
+// tasks, smaller ones built as subtrees by one workgroup each (rtx_anim.h)
+constexpr uint32_t kAnimCut = 128;
+
 struct rtx_anim {
     int device = 0;
     std::string err;
@@ -2639,6 +2643,7 @@ struct rtx_anim {
     bool reg_fast = false;                // DevScene::tri_fast condition at registration
     bool hbm_only = false;                // RTX_ANIM_HBM=1 at registration: build records in HBM (tests)
     bool serial_frontier = false;         // RTX_ANIM_SERIAL_FRONTIER=1: the frontier's serial greedy for every mesh (tests)
+    uint32_t cut = kAnimCut;              // RTX_ANIM_CUT: nodes above this many triangles split as queue tasks
     uint32_t epoch = 0;                   // updates so far (the build's publication flag)
     std::vector<double> obj_radius;       // per registered mesh: max |object-space position|
 };
@@ -2733,6 +2738,10 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
     a->device = c->device;
     a->hbm_only = std::getenv("RTX_ANIM_HBM") != nullptr;
     a->serial_frontier = std::getenv("RTX_ANIM_SERIAL_FRONTIER") != nullptr;
+    if (const char* e = std::getenv("RTX_ANIM_CUT")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 8 && v < (1l << 30)) a->cut = static_cast<uint32_t>(v);
+    }
     if (const char* e = std::getenv("RTX_ANIM_DEPTH_LIMIT")) {
         const int v = std::atoi(e);
         if (v >= 1 && v < kStackDepth) a->depth_limit = static_cast<uint32_t>(v);
@@ -2788,9 +2797,10 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
         ANIM_CREATE_TRY(anim_alloc(a, &d.lb, T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.rs, T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.rk, T));
-        ANIM_CREATE_TRY(anim_alloc(a, &d.tmp, 2 * T));
+        ANIM_CREATE_TRY(anim_alloc(a, &d.tmp, 2 * T + rtxa::kMaxTop));
         ANIM_CREATE_TRY(anim_alloc(a, &d.ref, 3 * T));
         ANIM_CREATE_TRY(anim_alloc(a, &d.status, 128));
+        ANIM_CREATE_TRY(anim_alloc(a, &d.q, rtxa::kQWords));
         double rad = 0.0;
         for (size_t k = 0; k < V; ++k) {
             const double x = q.positions[3 * k], y = q.positions[3 * k + 1], z = q.positions[3 * k + 2];
@@ -2874,6 +2884,7 @@ extern "C" int rtx_anim_update(rtx_anim* a, rtx_ctx* c, const float* transforms)
     if (a->hbm_only) L.top_lds = 0;
     L.sub_lds = a->hbm_only ? 0u : 1u;
     L.frontier_max = a->serial_frontier ? 0u : rtxa::kFrontierHistMax;
+    L.cut = a->cut;
     L.epoch = ++a->epoch;
     ANIM_TRY(a, rtxa::launch_build(L, c->stream));
     ANIM_TRY(a, hipEventRecord(a->ev, c->stream));

@@ -85,24 +85,23 @@ st = (C.c_uint32 * 128)()
 abi.check(lib.rtx_anim_stamps(an1.h, 0, st), "rtx_anim_stamps")
 w = [int(x) for x in st]
 us = lambda x: ((x - w[8]) & 0xffffffff) / 100.0  # noqa: E731  (s_memrealtime, 100 MHz)
-print(f"status: err {w[0]} deepest {w[1]} nodesUsed {w[2]} parts {w[3]} subtrees {w[4]} top nodes {w[5]} "
-      f"top levels {w[6]}")
-print(f"build phases (us from start): set-up {us(w[9]):.1f}, top levels {us(w[10]):.1f}, "
+print(f"status: err {w[0]} deepest {w[1]} nodesUsed {w[2]} parts {w[3]} subtrees {w[4]} task-split ids {w[5]} "
+      f"nodes split as tasks {w[6]}")
+print(f"build phases (us from start): set-up {us(w[9]):.1f}, root split {us(w[10]):.1f}, "
       f"subtrees {us(w[11]):.1f} .. {us(w[12]):.1f}, output start {us(w[13]):.1f}, ranks {us(w[14]):.1f}, "
       f"frontier {us(w[15]):.1f}")
-print("top levels end (us):", [round(us(w[20 + d]), 1) for d in range(min(8, w[6]))])
 print(f"subtree 0: staged {us(w[29]):.1f}, levels end {[round(us(x), 1) for x in w[32:40] if x]}, levels done {us(w[30]):.1f}, "
       f"ranks {us(w[31]):.1f}")
-print(f"output wg0: records written {us(w[56]):.1f}, frontier cache {us(w[57]):.1f}")
+print(f"output wg0: records written {us(w[56]):.1f}")
+print("first splits (size, start, end us):", [(w[16 + k], round(us(w[20 + 2 * k]), 1), round(us(w[21 + 2 * k]), 1))
+                                               for k in range(min(4, w[6]))])
 if w[63]:
     print("top root steps (us from its start):", [round(((w[64 + i] - w[63]) & 0xffffffff) / 100.0, 1) for i in range(9)])
 if w[40]:
     print("subtree-0 root steps (us from its start):", [round(((w[41 + i] - w[40]) & 0xffffffff) / 100.0, 1) for i in range(9)],
           "bins/axis:", [round(((w[50 + a] - w[40]) & 0xffffffff) / 100.0, 1) for a in range(3)])
-if w[59] != w[58] and w[10] != w[8]:
-    print(f"shader clock during the top phase: {((w[59] - w[58]) & 0xffffffff) / (((w[10] - w[8]) & 0xffffffff) / 100.0):.0f} MHz")
 print("subtrees (start, end us):", [(round(us(w[80 + 2 * f]), 1), round(us(w[81 + 2 * f]), 1)) for f in range(min(8, w[4]))])
-print("sub workgroup entry (us):", [round(us(w[112 + f]), 1) for f in range(16)])
+print("worker workgroup entry (us):", [round(us(w[112 + f]), 1) for f in range(16)])
 print("subtree sizes:", [w[96 + f] for f in range(min(16, w[4]))])
 if w[63]:
     print("top root bins per axis done (us from its start):", [round(((w[73 + a] - w[63]) & 0xffffffff) / 100.0, 1) for a in range(3)])
