@@ -32,7 +32,7 @@ namespace rtxa {
 #endif
 constexpr int kAnimThreads = RTX_ANIM_THREADS;   // threads of every build workgroup
 constexpr int kAnimWaves = kAnimThreads / 64;
-constexpr int kMaxAnimMeshes = 8;                // animated meshes per launch
+constexpr int kMaxAnimMeshes = 32;               // animated meshes per launch (their matrices travel in the kernel arguments)
 constexpr int kMaxAnimParts = 128;               // frontier entries per mesh (kPartsPerMesh)
 constexpr int kMaxTop = 256;                     // temp ids of task-split nodes and their children per mesh
 constexpr int kMaxSub = kMaxTop;                 // subtrees per mesh (each root is one of those ids)

@@ -656,11 +656,13 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
                 if (cost < FLT_MAX) key = min_key(cost, j) & ~1ull;
             }
         }
+        stp(15);
         {
             unsigned long long k1[1] = {key};
             wred_min64(k1);
             key = k1[0];
         }
+        stp(16);
         float bestCost = FLT_MAX;
         if (key != ~0ull) {
             const uint32_t jb = static_cast<uint32_t>(key) >> 1;
@@ -746,10 +748,12 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
             if (right) A[1].add(St, e, 1u + (q - S));
             else A[0].add(St, e, 1u + q);
         }
+        stp(13);
         unsigned long long k[6] = {A[0].k0, A[0].k1, A[0].k2, A[1].k0, A[1].k1, A[1].k2};
         float m[6] = {A[0].m0, A[0].m1, A[0].m2, A[1].m0, A[1].m1, A[1].m2};
         wred_min64(k);
         wred_max(m);
+        stp(14);
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             A[c].k0 = k[3 * c]; A[c].k1 = k[3 * c + 1]; A[c].k2 = k[3 * c + 2];
@@ -1074,7 +1078,10 @@ __device__ __forceinline__ void run_task(const Launch& L, const MeshDev& M, uint
     }
     if (tid == 0) {
         if (!split) {
-            if (f == 0) M.status[29] = stamp();   // subtree 0: staged
+            if (f == 0) {   // subtree 0: staged (and the shader clock counter, diagnostics)
+                M.status[29] = stamp();
+                M.status[60] = static_cast<uint32_t>(__builtin_amdgcn_s_memtime());
+            }
             atomicMin(&M.status[kStSub0], stamp());
         }
         Lv.K = 1; Lv.next = 0; Lv.take = 0; Lv.maxn = n; Lv.nmaxn = 0; Lv.ids = ids0; Lv.err = 0;
@@ -1147,7 +1154,10 @@ __device__ __forceinline__ void run_task(const Launch& L, const MeshDev& M, uint
             M.tmp[S0.root].rank = nodes[0].rank;
         }
     }
-    if (f == 0 && tid == 0) M.status[31] = stamp();   // subtree 0: ranks done
+    if (f == 0 && tid == 0) {   // subtree 0: ranks done
+        M.status[31] = stamp();
+        M.status[61] = static_cast<uint32_t>(__builtin_amdgcn_s_memtime());
+    }
     if (tid == 0 && f < 16u) {   // diagnostics: subtrees 0-7 start / end, subtrees 0-15 sizes
         if (f < 8u) { M.status[80 + 2 * f] = t_start; M.status[81 + 2 * f] = stamp(); }
         M.status[96 + f] = n;
@@ -1601,7 +1611,7 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
         tr[2] = make_float4(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z, tn.z);   // edge2 (:140)
         tr[3] = make_float4(fbits(M.mat_bits), 0.f, 0.f, 0.f);
     }
-    if (g == 0 && tid == 0) M.status[56] = stamp();   // workgroup 0: records written
+    if (g == 0 && tid == 0) M.status[57] = stamp();   // workgroup 0: records written
 }
 
 }  // namespace

@@ -2701,7 +2701,7 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
     *out = nullptr;
     g_anim_err.clear();
     if (!c || !s || !ids || !src || n == 0) return afail(nullptr, RTX_E_INVALID, "null argument or no mesh");
-    if (n > static_cast<uint32_t>(rtxa::kMaxAnimMeshes)) return afail(nullptr, RTX_E_UNSUPPORTED, "more than 8 animated meshes");
+    if (n > static_cast<uint32_t>(rtxa::kMaxAnimMeshes)) return afail(nullptr, RTX_E_UNSUPPORTED, "more than 32 animated meshes");
     if (c->split_parts > static_cast<uint32_t>(rtxa::kMaxAnimParts))
         return afail(nullptr, RTX_E_UNSUPPORTED, "frontier target above the device builder's 128 parts");
     std::vector<uint8_t> seen(s->n_meshes, 0);
@@ -2729,8 +2729,6 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
     lay.depth.assign(s->n_meshes, 0);
     int rc = upload_scene(c, s, &lay);
     if (rc != RTX_OK) return afail(nullptr, rc, std::string("upload: ") + c->err);
-    for (uint32_t i = 0; i < n; ++i)
-        if (lay.depth[ids[i]] >= 40) return afail(nullptr, RTX_E_UNSUPPORTED, "animated BVH 40 or more levels deep");
     if (c->deep_stack) return afail(nullptr, RTX_E_UNSUPPORTED, "scene needs the deep-stack kernel");
 
     rtx_anim* a = new (std::nothrow) rtx_anim;

@@ -289,8 +289,10 @@ typedef struct rtx_mesh_source {
 typedef struct rtx_anim rtx_anim;
 /* Register meshes mesh_ids[0..n) of `scene` (its current flattened state, what
  * rtx_upload_scene takes) as device-animated, with their object-space state src[0..n), and
- * upload the scene to `ctx` with rebuild-sized regions reserved for them.  n <= 8; the
- * meshes must be NaN-free with BVHs under 40 levels. */
+ * upload the scene to `ctx` with rebuild-sized regions reserved for them.  n <= 32; the
+ * meshes must be NaN-free, and the scene must render with the default-depth kernel (BVHs under
+ * 64 levels; a rebuilt tree that deep is disabled in the image and reported, see
+ * rtx_anim_status). */
 int rtx_anim_create(rtx_anim** out, rtx_ctx* ctx, const rtx_scene* scene, const int32_t* mesh_ids,
                     const rtx_mesh_source* src, uint32_t n);
 void rtx_anim_destroy(rtx_anim* anim);

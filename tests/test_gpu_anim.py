@@ -19,7 +19,8 @@ from gp1_raytracer_2223_amd.scene import HostScene
 
 pytestmark = pytest.mark.gpu
 
-SCENES = ["W4_Bunny", "W4_Optional", "W4_Reference", "Bunny8Lights", "file:scenes/gallery.rtxscene"]
+SCENES = ["W4_Bunny", "W4_Optional", "W4_Reference", "Bunny8Lights", "file:scenes/gallery.rtxscene",
+          "file:scenes/crowd.rtxscene"]   # crowd: 12 turning meshes, three of 12 triangles (a root subtree)
 TIMES = [1.3, 2.7, 0.4, 4.1, 5.9, 3.3]
 
 
@@ -150,6 +151,24 @@ def test_device_update_hbm_build_path(gpu_ctx, name, monkeypatch):
     anim.close()
 
 
+@pytest.mark.parametrize("cut", [8, 16, 100000])
+def test_device_update_task_cut_extremes(gpu_ctx, cut, monkeypatch):
+    """The split / subtree boundary (Launch::cut, RTX_ANIM_CUT read at rtx_anim_create) does not
+    change the tree: 8 and 16 split nearly every node as a queue task and run out of task ids
+    (kMaxTop; the rest become subtrees), 100000 builds each mesh as one subtree from its root."""
+    monkeypatch.setenv("RTX_ANIM_CUT", str(cut))
+    for name in ["W4_Optional", "file:scenes/crowd.rtxscene"]:
+        dev_scene, host_scene = _scene(name), _scene(name)
+        anim = DeviceAnimation(dev_scene, gpu_ctx)
+        for t in TIMES[:3]:
+            anim.update(t, gpu_ctx)
+            host_scene.update(t)
+            assert list(anim.status(0)[:1]) == [0]
+            for k in range(len(anim.mesh_ids)):
+                _compare_state(anim, host_scene, k)
+        anim.close()
+
+
 def _image(ctx):
     import ctypes as C
     lib = abi.load_hip()
@@ -196,7 +215,7 @@ def test_anim_create_rejects_bad_input(gpu_ctx):
     assert lib.rtx_anim_last_error(None)
     ok = (C.c_int32 * 1)(0)
     assert lib.rtx_anim_create(C.byref(h), gpu_ctx.h, C.byref(s), ok, src, 0) == abi.RTX_E_INVALID
-    assert lib.rtx_anim_create(C.byref(h), gpu_ctx.h, C.byref(s), ok, src, 9) != abi.RTX_OK
+    assert lib.rtx_anim_create(C.byref(h), gpu_ctx.h, C.byref(s), ok, src, 33) == abi.RTX_E_UNSUPPORTED   # > 32 meshes
 
 
 def test_device_update_too_deep_tree_is_disabled_not_rendered(monkeypatch):

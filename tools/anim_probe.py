@@ -92,14 +92,18 @@ print(f"build phases (us from start): set-up {us(w[9]):.1f}, root split {us(w[10
       f"frontier {us(w[15]):.1f}")
 print(f"subtree 0: staged {us(w[29]):.1f}, levels end {[round(us(x), 1) for x in w[32:40] if x]}, levels done {us(w[30]):.1f}, "
       f"ranks {us(w[31]):.1f}")
-print(f"output wg0: records written {us(w[56]):.1f}")
+print(f"output wg0: records written {us(w[57]):.1f}")
+if w[61] != w[60] and w[31] != w[29]:
+    print(f"shader clock during subtree 0: {((w[61] - w[60]) & 0xffffffff) / (((w[31] - w[29]) & 0xffffffff) / 100.0):.0f} MHz")
 print("first splits (size, start, end us):", [(w[16 + k], round(us(w[20 + 2 * k]), 1), round(us(w[21 + 2 * k]), 1))
                                                for k in range(min(4, w[6]))])
 if w[63]:
     print("top root steps (us from its start):", [round(((w[64 + i] - w[63]) & 0xffffffff) / 100.0, 1) for i in range(9)])
 if w[40]:
     print("subtree-0 root steps (us from its start):", [round(((w[41 + i] - w[40]) & 0xffffffff) / 100.0, 1) for i in range(9)],
-          "bins/axis:", [round(((w[50 + a] - w[40]) & 0xffffffff) / 100.0, 1) for a in range(3)])
+          "bins/axis:", [round(((w[50 + a] - w[40]) & 0xffffffff) / 100.0, 1) for a in range(3)],
+          "sweep lanes done, key reduced:", [round(((w[55 + a] - w[40]) & 0xffffffff) / 100.0, 1) for a in range(2)],
+          "child bounds loop done, reduced:", [round(((w[53 + a] - w[40]) & 0xffffffff) / 100.0, 1) for a in range(2)])
 print("subtrees (start, end us):", [(round(us(w[80 + 2 * f]), 1), round(us(w[81 + 2 * f]), 1)) for f in range(min(8, w[4]))])
 print("worker workgroup entry (us):", [round(us(w[112 + f]), 1) for f in range(16)])
 print("subtree sizes:", [w[96 + f] for f in range(min(16, w[4]))])
