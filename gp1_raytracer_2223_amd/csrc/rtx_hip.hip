@@ -2635,6 +2635,10 @@ struct rtx_anim {
     float room_p0[5] = {};   // rtx_ctx::room_p0 of the registration upload
     std::string sig;
     hipEvent_t ev = nullptr;              // the last update
+    // The updates' own stream, high priority (RTX_ANIM_SAME_STREAM=1: the context's stream): an
+    // update then runs beside the render of the previous frame (another context's stream)
+    // instead of queueing behind its workgroups; the context's next render waits for it.
+    hipStream_t stream = nullptr;
     bool built = false;
     uint32_t cur = 0;                     // state buffer of the current order
     // rebuilt trees this deep or deeper are disabled in the image (rtxa::Launch::depth_limit);
@@ -2691,6 +2695,7 @@ extern "C" void rtx_anim_destroy(rtx_anim* a) {
     if (!a) return;
     (void)hipSetDevice(a->device);
     if (a->ev) { (void)hipEventSynchronize(a->ev); (void)hipEventDestroy(a->ev); }
+    if (a->stream) { (void)hipStreamSynchronize(a->stream); (void)hipStreamDestroy(a->stream); }
     for (void* p : a->allocs) (void)hipFree(p);
     delete a;
 }
@@ -2752,6 +2757,11 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
     } while (0)
     ANIM_CREATE_TRY(hipSetDevice(c->device));
     ANIM_CREATE_TRY(hipEventCreateWithFlags(&a->ev, hipEventDisableTiming));
+    if (!std::getenv("RTX_ANIM_SAME_STREAM")) {
+        int lo_prio = 0, hi_prio = 0;
+        ANIM_CREATE_TRY(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+        ANIM_CREATE_TRY(hipStreamCreateWithPriority(&a->stream, hipStreamNonBlocking, hi_prio));
+    }
     a->total = lay.total;
     a->tri_off = lay.tri_off; a->node_off = lay.node_off; a->part_off = lay.part_off; a->mesh_off = lay.mesh_off;
     a->oct_bytes = lay.oct_bytes;
@@ -2861,8 +2871,10 @@ extern "C" int rtx_anim_update(rtx_anim* a, rtx_ctx* c, const float* transforms)
         ANIM_TRY(a, hipHostMalloc(&B.h, a->total));
         B.cap = a->total;
     }
-    if (a->built) ANIM_TRY(a, hipStreamWaitEvent(c->stream, a->ev, 0));
-    ANIM_TRY(a, hipMemcpyAsync(B.d, a->d_template, a->total, hipMemcpyDeviceToDevice, c->stream));
+    // (image B's earlier renders on this context have completed: B.done above)
+    hipStream_t s = a->stream ? a->stream : c->stream;
+    if (a->built) ANIM_TRY(a, hipStreamWaitEvent(s, a->ev, 0));
+    ANIM_TRY(a, hipMemcpyAsync(B.d, a->d_template, a->total, hipMemcpyDeviceToDevice, s));
     rtxa::Launch L{};
     L.meshes = a->d_mesh;
     L.n = static_cast<uint32_t>(a->mesh.size());
@@ -2884,8 +2896,9 @@ extern "C" int rtx_anim_update(rtx_anim* a, rtx_ctx* c, const float* transforms)
     L.frontier_max = a->serial_frontier ? 0u : rtxa::kFrontierHistMax;
     L.cut = a->cut;
     L.epoch = ++a->epoch;
-    ANIM_TRY(a, rtxa::launch_build(L, c->stream));
-    ANIM_TRY(a, hipEventRecord(a->ev, c->stream));
+    ANIM_TRY(a, rtxa::launch_build(L, s));
+    ANIM_TRY(a, hipEventRecord(a->ev, s));
+    if (s != c->stream) ANIM_TRY(a, hipStreamWaitEvent(c->stream, a->ev, 0));   // the next render reads image B
     a->built = true;
     a->cur ^= 1u;
     // the context now renders from image k (the bookkeeping of rtx_upload_scene)
