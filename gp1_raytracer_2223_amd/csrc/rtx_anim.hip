@@ -240,6 +240,9 @@ constexpr uint32_t kSubLdsMax = 2816;    // subtrees up to this size build from 
 #ifndef RTX_ANIM_TEAM_ELEMS
 #define RTX_ANIM_TEAM_ELEMS 96u   // a team gets another wave only for this many elements per wave
 #endif
+#ifndef RTX_ANIM_SMALL
+#define RTX_ANIM_SMALL 1   // one-wave nodes of up to 128 elements by node_small (0: node_process for all)
+#endif
 #ifndef RTX_ANIM_BINS_ATOMIC
 #define RTX_ANIM_BINS_ATOMIC 0   // experiment: LDS atomics into per-wave bin copies for every node
 #endif
@@ -361,6 +364,12 @@ struct BoundAcc {
         if (a2 == a2) { const unsigned long long k = min_key(a2, r); k2 = k < k2 ? k : k2; }
         m0 = fmaxf(m0, St.hi(0, e)); m1 = fmaxf(m1, St.hi(1, e)); m2 = fmaxf(m2, St.hi(2, e));
     }
+    __device__ void addv(float a0, float a1, float a2, float h0, float h1, float h2, uint32_t r) {   // from registers
+        if (a0 == a0) { const unsigned long long k = min_key(a0, r); k0 = k < k0 ? k : k0; }
+        if (a1 == a1) { const unsigned long long k = min_key(a1, r); k1 = k < k1 ? k : k1; }
+        if (a2 == a2) { const unsigned long long k = min_key(a2, r); k2 = k < k2 ? k : k2; }
+        m0 = fmaxf(m0, h0); m1 = fmaxf(m1, h1); m2 = fmaxf(m2, h2);
+    }
     __device__ void wave() {
         unsigned long long k[3] = {k0, k1, k2};
         float m[3] = {m0, m1, m2};
@@ -466,6 +475,260 @@ __device__ __forceinline__ void bins_private(const ST& St, const PT* src, uint32
     bins_private_half<kBins / 2>(St, src, f0, n, tl, nl, lane, ax, minB, scale, sink);
 }
 
+// 4. the plane sweep (DataTypes.h:443-480) over the bins in the slot: lane j < 21 evaluates
+//    plane j % 7 of axis j / 7; the reference takes the first strictly smaller cost in
+//    (axis, plane) order from FLT_MAX.  Returns whether the node splits (at axis, pos).
+__device__ __forceinline__ bool plane_sweep(const Slot& sl, uint32_t lane, const bool (&live)[3], const float (&minB)[3],
+                                            const float (&bd)[3], uint32_t n, const TmpNode& X, int& axis, float& pos) {
+    unsigned long long key = ~0ull;
+    const uint32_t j = lane;
+    if (j < 3u * kPlanes) {
+        const int ax = static_cast<int>(j / kPlanes), i = static_cast<int>(j % kPlanes);
+        if (live[ax]) {
+            // all eight bins read at once (a fixed loop, no per-lane trip counts); a bin on
+            // the other side enters as the fold identity (rmin(m, FLT_MAX) = m, and
+            // rmax(m, FLT_MIN) = m for every m >= FLT_MIN, which all maxima are)
+            uint32_t bcq[kBins];
+            float bq[kBins][6];
+#pragma unroll
+            for (int q = 0; q < kBins; ++q) {
+                bcq[q] = sl.bc[ax][q];
+                bq[q][0] = sl.bl[ax][q][0]; bq[q][1] = sl.bl[ax][q][1]; bq[q][2] = sl.bl[ax][q][2];
+                bq[q][3] = sl.bh[ax][q][0]; bq[q][4] = sl.bh[ax][q][1]; bq[q][5] = sl.bh[ax][q][2];
+            }
+            int lc = 0, rc = 0;
+            float l0 = FLT_MAX, l1 = FLT_MAX, l2 = FLT_MAX, h0 = FLT_MIN, h1 = FLT_MIN, h2 = FLT_MIN;
+#pragma unroll
+            for (int q = 0; q < kBins; ++q) {   // leftBox.Grow(bins[q].bounds), q = 0..i
+                const bool in = q <= i;
+                lc += in ? static_cast<int>(bcq[q]) : 0;
+                l0 = rmin(l0, in ? bq[q][0] : FLT_MAX); l1 = rmin(l1, in ? bq[q][1] : FLT_MAX);
+                l2 = rmin(l2, in ? bq[q][2] : FLT_MAX);
+                h0 = rmax(h0, in ? bq[q][3] : FLT_MIN); h1 = rmax(h1, in ? bq[q][4] : FLT_MIN);
+                h2 = rmax(h2, in ? bq[q][5] : FLT_MIN);
+            }
+            const float la = area(l0, l1, l2, h0, h1, h2);
+            l0 = l1 = l2 = FLT_MAX;
+            h0 = h1 = h2 = FLT_MIN;
+#pragma unroll
+            for (int q = kPlanes; q >= 0; --q) {   // rightBox.Grow(bins[q].bounds), q = 7..i+1
+                const bool in = q > i;
+                rc += in ? static_cast<int>(bcq[q]) : 0;
+                l0 = rmin(l0, in ? bq[q][0] : FLT_MAX); l1 = rmin(l1, in ? bq[q][1] : FLT_MAX);
+                l2 = rmin(l2, in ? bq[q][2] : FLT_MAX);
+                h0 = rmax(h0, in ? bq[q][3] : FLT_MIN); h1 = rmax(h1, in ? bq[q][4] : FLT_MIN);
+                h2 = rmax(h2, in ? bq[q][5] : FLT_MIN);
+            }
+            const float ra = area(l0, l1, l2, h0, h1, h2);
+            const float cost = static_cast<float>(lc) * la + static_cast<float>(rc) * ra;
+            // candidates: cost < FLT_MAX (NaN never is); ties keep the earlier (axis, plane)
+            if (cost < FLT_MAX) key = min_key(cost, j) & ~1ull;
+        }
+    }
+    {
+        unsigned long long k1[1] = {key};
+        wred_min64(k1);
+        key = k1[0];
+    }
+    float bestCost = FLT_MAX;
+    if (key != ~0ull) {
+        const uint32_t jb = static_cast<uint32_t>(key) >> 1;
+        axis = static_cast<int>(jb / kPlanes);
+        const int i = static_cast<int>(jb % kPlanes);
+        const float step = bd[axis] / kBins;
+        pos = minB[axis] + step * static_cast<float>(i + 1);
+        bestCost = min_key_value(key);
+    }
+    auto u = [](float v) { return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(v))); };
+    const float noSplitCost = static_cast<float>(3u * n) * area(u(X.mn[0]), u(X.mn[1]), u(X.mn[2]), u(X.mx[0]),
+                                                                u(X.mx[1]), u(X.mx[2]));
+    return !(bestCost >= noSplitCost);   // Subdivide: `if (splitCost >= noSplitCost) return;`
+}
+
+// ---- 128-position masks (two ballots) for a one-wave node of at most 128 elements
+struct Mask128 {
+    unsigned long long w[2];
+};
+__device__ __forceinline__ uint32_t pop_below(const Mask128& m, uint32_t q) {   // set bits at positions < q
+    const unsigned long long b0 = q >= 64u ? ~0ull : ((1ull << q) - 1ull);
+    const unsigned long long b1 = q <= 64u ? 0ull : (q >= 128u ? ~0ull : ((1ull << (q - 64u)) - 1ull));
+    return static_cast<uint32_t>(__popcll(m.w[0] & b0) + __popcll(m.w[1] & b1));
+}
+__device__ __forceinline__ uint32_t sel64(unsigned long long m, uint32_t k) {   // position of the k-th set bit (lowest first)
+    uint32_t p = 0;
+#pragma unroll
+    for (uint32_t w = 32; w >= 1u; w >>= 1) {
+        const uint32_t c = static_cast<uint32_t>(__popcll(m & ((1ull << w) - 1ull)));
+        const bool up = k >= c;
+        k = up ? k - c : k;
+        m = up ? m >> w : m;
+        p = up ? p + w : p;
+    }
+    return p;
+}
+__device__ __forceinline__ uint32_t sel128(const Mask128& m, uint32_t k) {
+    const uint32_t c0 = static_cast<uint32_t>(__popcll(m.w[0]));
+    return k < c0 ? sel64(m.w[0], k) : 64u + sel64(m.w[1], k - c0);
+}
+
+// One node of n <= 128 elements by one wave, the elements in registers (positions lane and
+// lane + 64): the same decisions and outputs as node_process, without the LDS round trips of
+// its element passes.  The partition's closed form (wave_ranks / part_dest) is evaluated on
+// the wave's ballot masks: with bigL the big elements left of pL and smallR the small ones
+// from pL on, a big q < pL with m = |bigL below q| goes to n - 1 (m = 0) or one before the
+// (m - 1)-th element of smallR counted from the top; a small p >= pL with r = |smallR above p|
+// goes to the r-th element of bigL; the others stay (q < pL) or move one left (p >= pL).
+template <bool LDS>
+__device__ __forceinline__ void node_small(const Store<LDS>& St, TmpNode* nodes, uint32_t lane, Slot& sl, Level& Lv,
+                                           const Region& rg, uint32_t t, uint32_t b, uint32_t sub, uint32_t n,
+                                           uint32_t first, uint32_t depth) {
+    using P = typename Store<LDS>::P;
+    P* src = b ? St.perm[1] : St.perm[0];
+    P* dst = b ? St.perm[0] : St.perm[1];
+    const uint32_t f0 = first - St.pos0;
+    bool v[2];
+    uint32_t e[2];
+    float c[2][3], lo[2][3], hi[2][3];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t q = lane + 64u * j;
+        v[j] = q < n;
+        e[j] = v[j] ? static_cast<uint32_t>(src[f0 + q]) : 0u;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            c[j][a] = v[j] ? St.c(a, e[j]) : 0.f;
+            lo[j][a] = v[j] ? St.lo(a, e[j]) : 0.f;
+            hi[j][a] = v[j] ? St.hi(a, e[j]) : 0.f;
+        }
+    }
+    if (!(3u * n > 8u)) {   // Subdivide's termination: the range as it is, in both buffers
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (v[j]) dst[f0 + lane + 64u * j] = static_cast<P>(e[j]);
+        return;
+    }
+    // 1. the slot's bins
+    if (lane < 3u * kBins) (&sl.bc[0][0])[lane] = 0u;
+    for (uint32_t i = lane; i < 3u * kBins * 3u; i += 64u) {
+        (&sl.bl[0][0][0])[i] = FLT_MAX;
+        (&sl.bh[0][0][0])[i] = FLT_MIN;
+    }
+    // 2. centroid bounds (DataTypes.h:404-419), order-free
+    float mn3[3], mx3[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        mn3[a] = fminf(v[0] ? c[0][a] : FLT_MAX, v[1] ? c[1][a] : FLT_MAX);
+        mx3[a] = fmaxf(v[0] ? c[0][a] : FLT_MIN, v[1] ? c[1][a] : FLT_MIN);
+    }
+    wred_min(mn3);
+    wred_max(mx3);
+    float minB[3], bd[3], scale[3];
+    bool live[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        minB[a] = mn3[a];
+        bd[a] = mx3[a] - minB[a];                 // boundsDifference
+        live[a] = !(fabsf(bd[a]) < FLT_EPSILON);  // else `continue`
+        scale[a] = kBins / bd[a];
+    }
+    tsync<false>();
+    // 3. bins (DataTypes.h:424-440): LDS atomics per element
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        if (!v[j]) continue;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            if (!live[a]) continue;
+            const float x = (c[j][a] - minB[a]) * scale[a];
+            int bi = x >= 0.f ? static_cast<int>(fminf(x, 2147483520.f)) : 0;
+            bi = kPlanes < bi ? kPlanes : bi;
+            atomicAdd(&sl.bc[a][bi], 3u);
+            atomicMin(&sl.bl[a][bi][0], lo[j][0]); atomicMin(&sl.bl[a][bi][1], lo[j][1]); atomicMin(&sl.bl[a][bi][2], lo[j][2]);
+            atomicMax(&sl.bh[a][bi][0], hi[j][0]); atomicMax(&sl.bh[a][bi][1], hi[j][1]); atomicMax(&sl.bh[a][bi][2], hi[j][2]);
+        }
+    }
+    tsync<false>();
+    // 4. the sweep
+    int axis = 0;
+    float pos = 0.f;
+    const bool split = plane_sweep(sl, lane, live, minB, bd, n, nodes[t], axis, pos);
+    if (!split) {   // a leaf: the range as it is, in both buffers
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (v[j]) dst[f0 + lane + 64u * j] = static_cast<P>(e[j]);
+        return;
+    }
+    // 5. the partition on ballot masks
+    bool sm[2];
+    sm[0] = v[0] && (axis == 0 ? c[0][0] : axis == 1 ? c[0][1] : c[0][2]) < pos;
+    sm[1] = v[1] && (axis == 0 ? c[1][0] : axis == 1 ? c[1][1] : c[1][2]) < pos;
+    const Mask128 small{{__ballot(sm[0]), __ballot(sm[1])}};
+    const Mask128 valid{{__ballot(v[0]), __ballot(v[1])}};
+    const uint32_t S = static_cast<uint32_t>(__popcll(small.w[0]) + __popcll(small.w[1]));
+    const bool smallS = S < n && ((small.w[S >> 6] >> (S & 63u)) & 1ull);
+    const uint32_t pL = S + ((S < n && !smallS) ? 1u : 0u);
+    const unsigned long long lt0 = pL >= 64u ? ~0ull : ((1ull << pL) - 1ull);
+    const unsigned long long lt1 = pL <= 64u ? 0ull : (pL >= 128u ? ~0ull : ((1ull << (pL - 64u)) - 1ull));
+    const Mask128 bigL{{valid.w[0] & ~small.w[0] & lt0, valid.w[1] & ~small.w[1] & lt1}};
+    const Mask128 smallR{{small.w[0] & ~lt0, small.w[1] & ~lt1}};
+    const uint32_t nR = static_cast<uint32_t>(__popcll(smallR.w[0]) + __popcll(smallR.w[1]));
+    const bool kids = S != 0u && S != n;
+    uint32_t dpos[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t q = lane + 64u * j;
+        uint32_t d = q;
+        if (q < pL) {
+            if (v[j] && !sm[j]) {
+                const uint32_t m = pop_below(bigL, q);
+                d = m == 0u ? n - 1u : sel128(smallR, nR - m) - 1u;   // the (m - 1)-th from the top
+            }
+        } else {
+            d = sm[j] ? sel128(bigL, nR - 1u - pop_below(smallR, q)) : q - 1u;   // r = |smallR above q|
+        }
+        d = d < n ? d : n - 1u;   // (the closed form stays in range; a guard for the stores)
+        dpos[j] = d;
+        if (v[j]) {
+            dst[f0 + d] = static_cast<P>(e[j]);
+            if (!kids) src[f0 + d] = static_cast<P>(e[j]);   // leftCount 0 or all: a leaf, both buffers
+        }
+    }
+    if (!kids) return;
+    // 6. UpdateNodeBounds of both children (DataTypes.h:310-321) from the registers
+    BoundAcc A[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        if (!v[j]) continue;
+        const bool right = dpos[j] >= S;
+        const uint32_t r = 1u + (right ? dpos[j] - S : dpos[j]);
+        if (right) A[1].addv(lo[j][0], lo[j][1], lo[j][2], hi[j][0], hi[j][1], hi[j][2], r);
+        else A[0].addv(lo[j][0], lo[j][1], lo[j][2], hi[j][0], hi[j][1], hi[j][2], r);
+    }
+    unsigned long long k[6] = {A[0].k0, A[0].k1, A[0].k2, A[1].k0, A[1].k1, A[1].k2};
+    float m[6] = {A[0].m0, A[0].m1, A[0].m2, A[1].m0, A[1].m1, A[1].m2};
+    wred_min64(k);
+    wred_max(m);
+    if (lane == 0) {
+        const uint32_t cid = atomicAdd(&Lv.ids, 2u);
+        const unsigned long long ki = min_key_init();
+        TmpNode a{}, bb{};
+        for (int q = 0; q < 3; ++q) {
+            a.mn[q] = min_key_value(k[q] < ki ? k[q] : ki); a.mx[q] = m[q];
+            bb.mn[q] = min_key_value(k[3 + q] < ki ? k[3 + q] : ki); bb.mx[q] = m[3 + q];
+        }
+        a.first = first; a.count = S; a.l = -1; a.depth = depth + 1; a.parent = static_cast<int32_t>(t); a.sub = sub;
+        bb.first = first + S; bb.count = n - S; bb.l = -1; bb.depth = depth + 1; bb.parent = static_cast<int32_t>(t);
+        bb.sub = sub;
+        nodes[cid] = a;
+        nodes[cid + 1] = bb;
+        nodes[t].l = static_cast<int32_t>(cid);
+        const uint32_t w = atomicAdd(&Lv.next, 2u);
+        rg.nxt[w] = cid;
+        rg.nxt[w + 1] = cid + 1;
+        atomicMax(&Lv.nmaxn, max(S, n - S));
+    }
+}
+
 // One node (temp id t, or none: `act` false) by one team.  b: the permutation buffer of this
 // level (depth parity); the next level's is b ^ 1.  Children are appended to rg.nxt.
 template <bool MULTI, bool LDS>
@@ -496,6 +759,12 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
         n = __builtin_amdgcn_readfirstlane(nodes[t].count);
         first = __builtin_amdgcn_readfirstlane(nodes[t].first);
         depth = __builtin_amdgcn_readfirstlane(nodes[t].depth);
+    }
+    if constexpr (!MULTI) {
+        if (RTX_ANIM_SMALL && act && n <= 128u) {   // one wave, elements in registers
+            node_small<LDS>(St, nodes, tm.lane, sl, Lv, rg, t, b, sub, n, first, depth);
+            return;
+        }
     }
     const uint32_t f0 = first - St.pos0;
     // Subdivide's termination (idxCount <= 8) and the teams with no node: nothing but the copy
@@ -605,79 +874,11 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
         tsync<true>();
     }
     stp(3);
-    // 4. the plane sweep (DataTypes.h:443-480): lane j < 21 evaluates plane j % 7 of axis j / 7;
-    //    the reference takes the first strictly smaller cost in (axis, plane) order from FLT_MAX
+    // 4. the plane sweep
     int axis = 0;
     float pos = 0.f;
     bool split = false;
-    if (work) {
-        unsigned long long key = ~0ull;
-        const uint32_t j = tm.lane;
-        if (j < 3u * kPlanes) {
-            const int ax = static_cast<int>(j / kPlanes), i = static_cast<int>(j % kPlanes);
-            if (live[ax]) {
-                // all eight bins read at once (a fixed loop, no per-lane trip counts); a bin on
-                // the other side enters as the fold identity (rmin(m, FLT_MAX) = m, and
-                // rmax(m, FLT_MIN) = m for every m >= FLT_MIN, which all maxima are)
-                uint32_t bcq[kBins];
-                float bq[kBins][6];
-#pragma unroll
-                for (int q = 0; q < kBins; ++q) {
-                    bcq[q] = sl.bc[ax][q];
-                    bq[q][0] = sl.bl[ax][q][0]; bq[q][1] = sl.bl[ax][q][1]; bq[q][2] = sl.bl[ax][q][2];
-                    bq[q][3] = sl.bh[ax][q][0]; bq[q][4] = sl.bh[ax][q][1]; bq[q][5] = sl.bh[ax][q][2];
-                }
-                int lc = 0, rc = 0;
-                float l0 = FLT_MAX, l1 = FLT_MAX, l2 = FLT_MAX, h0 = FLT_MIN, h1 = FLT_MIN, h2 = FLT_MIN;
-#pragma unroll
-                for (int q = 0; q < kBins; ++q) {   // leftBox.Grow(bins[q].bounds), q = 0..i
-                    const bool in = q <= i;
-                    lc += in ? static_cast<int>(bcq[q]) : 0;
-                    l0 = rmin(l0, in ? bq[q][0] : FLT_MAX); l1 = rmin(l1, in ? bq[q][1] : FLT_MAX);
-                    l2 = rmin(l2, in ? bq[q][2] : FLT_MAX);
-                    h0 = rmax(h0, in ? bq[q][3] : FLT_MIN); h1 = rmax(h1, in ? bq[q][4] : FLT_MIN);
-                    h2 = rmax(h2, in ? bq[q][5] : FLT_MIN);
-                }
-                const float la = area(l0, l1, l2, h0, h1, h2);
-                l0 = l1 = l2 = FLT_MAX;
-                h0 = h1 = h2 = FLT_MIN;
-#pragma unroll
-                for (int q = kPlanes; q >= 0; --q) {   // rightBox.Grow(bins[q].bounds), q = 7..i+1
-                    const bool in = q > i;
-                    rc += in ? static_cast<int>(bcq[q]) : 0;
-                    l0 = rmin(l0, in ? bq[q][0] : FLT_MAX); l1 = rmin(l1, in ? bq[q][1] : FLT_MAX);
-                    l2 = rmin(l2, in ? bq[q][2] : FLT_MAX);
-                    h0 = rmax(h0, in ? bq[q][3] : FLT_MIN); h1 = rmax(h1, in ? bq[q][4] : FLT_MIN);
-                    h2 = rmax(h2, in ? bq[q][5] : FLT_MIN);
-                }
-                const float ra = area(l0, l1, l2, h0, h1, h2);
-                const float cost = static_cast<float>(lc) * la + static_cast<float>(rc) * ra;
-                // candidates: cost < FLT_MAX (NaN never is); ties keep the earlier (axis, plane)
-                if (cost < FLT_MAX) key = min_key(cost, j) & ~1ull;
-            }
-        }
-        stp(15);
-        {
-            unsigned long long k1[1] = {key};
-            wred_min64(k1);
-            key = k1[0];
-        }
-        stp(16);
-        float bestCost = FLT_MAX;
-        if (key != ~0ull) {
-            const uint32_t jb = static_cast<uint32_t>(key) >> 1;
-            axis = static_cast<int>(jb / kPlanes);
-            const int i = static_cast<int>(jb % kPlanes);
-            const float step = bd[axis] / kBins;
-            pos = minB[axis] + step * static_cast<float>(i + 1);
-            bestCost = min_key_value(key);
-        }
-        const TmpNode& X = nodes[t];
-        auto u = [](float v) { return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(v))); };
-        const float noSplitCost = static_cast<float>(3u * n) * area(u(X.mn[0]), u(X.mn[1]), u(X.mn[2]), u(X.mx[0]),
-                                                                    u(X.mx[1]), u(X.mx[2]));
-        split = !(bestCost >= noSplitCost);   // Subdivide: `if (splitCost >= noSplitCost) return;`
-    }
+    if (work) split = plane_sweep(sl, tm.lane, live, minB, bd, n, nodes[t], axis, pos);
     // 5. the partition: per-wave blocks of positions in order
     const uint32_t per = (n + tm.k - 1u) / tm.k;
     const uint32_t lo = min(n, tm.wt * per), hi = min(n, tm.wt * per + per);
