@@ -1461,6 +1461,7 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
 // + 1 of them) — found from a histogram of counts.  The parts are the unsplit children of the
 // split nodes (the root alone if none), ordered by their root paths read as bit strings.
 // Meshes above Launch::frontier_max (<= kFrontierHistMax) triangles keep the serial greedy over HBM.
+constexpr uint32_t kFrontierBitWords = (2u * kFrontierHistMax + kMaxTop + 31u) / 32u;
 __device__ __forceinline__ void out_frontier(const Launch& L, const MeshDev& M, const uint32_t* s_vbase,
                                              const uint32_t* s_base, const uint32_t* s_rank,
                                              const uint32_t* s_subroot, uint32_t ntop, uint32_t nsub, uint32_t nvirt,
@@ -1491,19 +1492,28 @@ __device__ __forceinline__ void out_frontier(const Launch& L, const MeshDev& M, 
     const uint32_t msplit = cap > 0u ? cap - 1u : 0u;   // splits wanted
     if (T <= min(L.frontier_max, kFrontierHistMax)) {
         __shared__ uint32_t s_hist[kFrontierHistMax + 1];
-        __shared__ uint32_t s_bits[2 * kFrontierHistMax / 32];   // split set by temp id
+        __shared__ uint32_t s_bits[kFrontierBitWords];   // split set by temp id (< kMaxTop + 2 T)
         __shared__ uint32_t s_wsum[kAnimWaves];
         __shared__ uint32_t s_sel[kMaxAnimParts], s_pidx[kMaxAnimParts], s_dep[kMaxAnimParts], s_path[kMaxAnimParts];
         __shared__ int32_t s_sl[kMaxAnimParts];
         __shared__ uint32_t s_tie[2 * kMaxAnimParts][2];
-        __shared__ uint32_t s_nsel, s_ntie, s_cstar, s_take, s_total;
+        __shared__ uint32_t s_nsel, s_ntie, s_cstar, s_take, s_total, s_ncand;
+        __shared__ uint32_t s_cand[kFrontierHistMax];   // the eligible nodes (split ones: fewer than T), temp id
+        __shared__ uint16_t s_ccnt[kFrontierHistMax];   // and count
         for (uint32_t i = tid; i <= T; i += kAnimThreads) s_hist[i] = 0u;
-        for (uint32_t i = tid; i < 2u * kFrontierHistMax / 32u; i += kAnimThreads) s_bits[i] = 0u;
-        if (tid == 0) { s_nsel = 0; s_ntie = 0; s_cstar = ~0u; s_take = 0; s_total = 0; }
+        for (uint32_t i = tid; i < kFrontierBitWords; i += kAnimThreads) s_bits[i] = 0u;
+        if (tid == 0) { s_nsel = 0; s_ntie = 0; s_cstar = ~0u; s_take = 0; s_total = 0; s_ncand = 0; }
         __syncthreads();
         for (uint32_t v = tid; v < nvirt; v += kAnimThreads) {
-            const TmpNode& X = M.tmp[tmap(v)];
-            if (X.l >= 0 && X.depth < 31u) atomicAdd(&s_hist[X.count], 1u);
+            const uint32_t t = tmap(v);
+            const TmpNode& X = M.tmp[t];
+            if (X.l >= 0 && X.depth < 31u) {
+                const uint32_t cnt = X.count;
+                atomicAdd(&s_hist[cnt], 1u);
+                const uint32_t i = atomicAdd(&s_ncand, 1u);
+                s_cand[i] = t;
+                s_ccnt[i] = static_cast<uint16_t>(cnt);
+            }
         }
         __syncthreads();
         // c*: the count where the suffix sums of the histogram reach msplit
@@ -1531,17 +1541,16 @@ __device__ __forceinline__ void out_frontier(const Launch& L, const MeshDev& M, 
         // every eligible node if there are no more than msplit (c* stays ~0u)
         const uint32_t cstar = s_total <= msplit ? 0u : s_cstar;
         const bool all = s_total <= msplit;
-        for (uint32_t v = tid; v < nvirt; v += kAnimThreads) {
-            const uint32_t t = tmap(v);
-            const TmpNode& X = M.tmp[t];
-            if (!(X.l >= 0 && X.depth < 31u)) continue;
-            if (all || X.count > cstar) {
+        const uint32_t ncand = s_ncand;
+        for (uint32_t v = tid; v < ncand; v += kAnimThreads) {
+            const uint32_t t = s_cand[v], cnt = s_ccnt[v];
+            if (all || cnt > cstar) {
                 s_sel[atomicAdd(&s_nsel, 1u)] = t;
                 atomicOr(&s_bits[t >> 5], 1u << (t & 31u));
-            } else if (X.count == cstar) {
+            } else if (cnt == cstar) {
                 const uint32_t i = atomicAdd(&s_ntie, 1u);
                 s_tie[i][0] = t;
-                s_tie[i][1] = rank_abs(t, X);
+                s_tie[i][1] = rank_abs(t, M.tmp[t]);
             }
         }
         __syncthreads();
@@ -1699,44 +1708,77 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
     __shared__ int32_t s_l[kMaxTop];
     __shared__ uint32_t s_split[kMaxTop], s_rank[kMaxTop], s_count[kMaxTop];
     __shared__ uint32_t s_subroot[kMaxSub], s_base[kMaxSub], s_nalloc[kMaxSub], s_smaxd[kMaxSub], s_vbase[kMaxSub + 1];
-    __shared__ uint8_t s_isroot[kMaxTop];
-    __shared__ uint32_t s_maxd;
+    __shared__ uint8_t s_isroot[kMaxTop], s_depth[kMaxTop];
+    __shared__ uint32_t s_maxd, s_dmax;
     if (g == 0 && tid == 0) M.status[kStOut0] = stamp();
     // ---- the task-split nodes' split counts (bottom-up, subtree roots from their builds) and ranks
+    if (tid == 0) { s_maxd = M.status[1]; s_dmax = 0u; }
+    __syncthreads();
     for (uint32_t t = tid; t < ntop; t += kAnimThreads) {
         const TmpNode X = M.tmp[t];
         s_l[t] = X.l;
         s_count[t] = X.count;
         s_isroot[t] = X.sub < static_cast<uint32_t>(kMaxSub) ? 1 : 0;
         s_split[t] = s_isroot[t] ? X.splits : 0u;   // a subtree root: its own build's count
+        const uint32_t d = X.parent == -2 ? 0u : X.depth;   // (an unused reserved id: no depth)
+        s_depth[t] = static_cast<uint8_t>(d);
+        atomicMax(&s_dmax, d);
     }
     for (uint32_t f = tid; f < nsub; f += kAnimThreads) {
-        const SubRec s = M.sub[f];
-        s_subroot[f] = s.root; s_base[f] = s.base; s_nalloc[f] = s.nalloc; s_smaxd[f] = s.maxd;
+        const SubRec sr = M.sub[f];
+        s_subroot[f] = sr.root; s_base[f] = sr.base; s_nalloc[f] = sr.nalloc; s_smaxd[f] = sr.maxd;
+        atomicMax(&s_maxd, sr.maxd);
     }
     __syncthreads();
-    if (tid == 0) {
-        uint32_t maxd = M.status[1];
-        for (uint32_t f = 0; f < nsub; ++f) maxd = max(maxd, s_smaxd[f]);
-        s_maxd = maxd;
-        // task-split ids are allocated after their parents' (parents before children)
-        for (int t = static_cast<int>(ntop) - 1; t >= 0; --t) {
+    // level by level (a task-split node's depth < 256: the build's depth limit)
+    const uint32_t dmax = s_dmax;
+    for (int d = static_cast<int>(dmax); d >= 0; --d) {
+        for (uint32_t t = tid; t < ntop; t += kAnimThreads) {
             const int32_t l = s_l[t];
-            if (!s_isroot[t]) s_split[t] = l >= 0 ? 1u + s_split[l] + s_split[l + 1] : 0u;
+            if (s_depth[t] == static_cast<uint32_t>(d) && !s_isroot[t])
+                s_split[t] = l >= 0 ? 1u + s_split[l] + s_split[l + 1] : 0u;
         }
-        s_rank[0] = 0u;
-        for (uint32_t t = 0; t < ntop; ++t) {
+        __syncthreads();
+    }
+    if (tid == 0) s_rank[0] = 0u;
+    __syncthreads();
+    for (uint32_t d = 0; d <= dmax; ++d) {
+        for (uint32_t t = tid; t < ntop; t += kAnimThreads) {
             const int32_t l = s_l[t];
-            if (l >= 0 && !s_isroot[t]) {   // a subtree root's children are subtree nodes
+            if (s_depth[t] == d && l >= 0 && !s_isroot[t]) {   // a subtree root's children are subtree nodes
                 s_rank[l] = s_rank[t] + 1u;
                 s_rank[l + 1] = s_rank[t] + 1u + s_split[l];
             }
         }
-        s_vbase[0] = ntop;
-        for (uint32_t f = 0; f < nsub; ++f) s_vbase[f + 1] = s_vbase[f] + s_nalloc[f];
-        if (g == kOutGroups) M.status[kStRanks] = stamp();
+        __syncthreads();
+    }
+    // the subtrees' virtual index bases: an exclusive scan of nalloc (one wave, kMaxSub / 64 per lane)
+    if (tid < 64u) {
+        constexpr uint32_t kPer = (kMaxSub + 63) / 64;
+        uint32_t v[kPer], sum = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint32_t f = tid * kPer + i;
+            v[i] = f < nsub ? s_nalloc[f] : 0u;
+            sum += v[i];
+        }
+        uint32_t incl = sum;
+        for (uint32_t o = 1; o < 64u; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (tid >= o) incl += y;
+        }
+        uint32_t base = ntop + incl - sum;
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint32_t f = tid * kPer + i;
+            if (f < nsub) s_vbase[f] = base;
+            base += v[i];
+            if (f + 1u == nsub) s_vbase[nsub] = base;
+        }
+        if (nsub == 0u && tid == 0) s_vbase[0] = ntop;
     }
     __syncthreads();
+    if (g == kOutGroups && tid == 0) M.status[kStRanks] = stamp();
     // absolute DFS rank of a split node (temp id t)
     auto rank_abs = [&](uint32_t t, const TmpNode& X) -> uint32_t {
         return t < ntop ? s_rank[t] : s_rank[s_subroot[X.sub]] + X.rank;
