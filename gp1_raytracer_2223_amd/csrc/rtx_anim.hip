@@ -173,6 +173,9 @@ __device__ __forceinline__ void wred_min64(unsigned long long (&v)[N]) {
 // reductions of 15 steps each.  Lane l ends with the wave's fold of value
 // q = 2 (l & 1) + ((l >> 1) & 1), c = 4 ((l >> 2) & 1) + 2 ((l >> 3) & 1) + ((l >> 4) & 1)
 // (lanes l and l + 32 alike).  Order-free, like the other wave reductions.
+#ifndef RTX_ANIM_BIN_PASSES
+#define RTX_ANIM_BIN_PASSES 1   // register bins: all eight in one pass (1, 512-thread workgroups) or two halves (2)
+#endif
 #ifndef RTX_ANIM_BINS_TRANSPOSE
 #define RTX_ANIM_BINS_TRANSPOSE 1
 #endif
@@ -184,10 +187,11 @@ __device__ __forceinline__ float xchg(float v) {
     const int u = __float_as_int(v);
     if constexpr (X == 1) return __int_as_float(__builtin_amdgcn_mov_dpp(u, 0xB1, 0xf, 0xf, false));   // [1,0,3,2]
     else if constexpr (X == 2) return __int_as_float(__builtin_amdgcn_mov_dpp(u, 0x4E, 0xf, 0xf, false));   // [2,3,0,1]
+    else if constexpr (X == 32) return __shfl_xor(v, 32);
     else return __int_as_float(__builtin_amdgcn_ds_swizzle(u, 0x1F | (X << 10)));   // bitmask mode: and 31, xor X
 }
-template <int X, int N>
-__device__ __forceinline__ void tstep(float (&v)[32], uint32_t lane, uint32_t& cbase) {
+template <int X, int N, int V>
+__device__ __forceinline__ void tstep(float (&v)[V], uint32_t lane, uint32_t& cbase) {
     constexpr int H = N / 2;
     const bool hi = (lane & static_cast<uint32_t>(X)) != 0u;
     float snd[H], kp[H];
@@ -202,17 +206,32 @@ __device__ __forceinline__ void tstep(float (&v)[32], uint32_t lane, uint32_t& c
 #pragma unroll
     for (int i = 0; i < H; ++i) v[i] = fold_c(N > 8 ? static_cast<uint32_t>(i & 7) : cbase + i, kp[i], snd[i]);
 }
-__device__ __forceinline__ float wred_transpose(float (&v)[32], uint32_t lane, uint32_t& q, uint32_t& c) {
+// V = 64 (eight bins): a sixth halving step across the two 32-lane halves instead of the full
+// fold; lane l then holds q = 4 (l & 1) + 2 ((l >> 1) & 1) + ((l >> 2) & 1), c from bits 3-5.
+template <int V>
+__device__ __forceinline__ float wred_transpose(float (&v)[V], uint32_t lane, uint32_t& q, uint32_t& c) {
     uint32_t cb = 0;
-    tstep<1, 32>(v, lane, cb);
-    tstep<2, 16>(v, lane, cb);
-    tstep<4, 8>(v, lane, cb);
-    tstep<8, 4>(v, lane, cb);
-    tstep<16, 2>(v, lane, cb);
-    const float r = fold_c(cb, v[0], __shfl_xor(v[0], 32));
-    q = 2u * (lane & 1u) + ((lane >> 1) & 1u);
-    c = cb;
-    return r;
+    if constexpr (V == 64) {
+        tstep<1, 64>(v, lane, cb);
+        tstep<2, 32>(v, lane, cb);
+        tstep<4, 16>(v, lane, cb);
+        tstep<8, 8>(v, lane, cb);
+        tstep<16, 4>(v, lane, cb);
+        tstep<32, 2>(v, lane, cb);
+        q = 4u * (lane & 1u) + 2u * ((lane >> 1) & 1u) + ((lane >> 2) & 1u);
+        c = cb;
+        return v[0];
+    } else {
+        tstep<1, 32>(v, lane, cb);
+        tstep<2, 16>(v, lane, cb);
+        tstep<4, 8>(v, lane, cb);
+        tstep<8, 4>(v, lane, cb);
+        tstep<16, 2>(v, lane, cb);
+        const float r = fold_c(cb, v[0], __shfl_xor(v[0], 32));
+        q = 2u * (lane & 1u) + ((lane >> 1) & 1u);
+        c = cb;
+        return r;
+    }
 }
 
 // The build records and permutation of a build region.  Records: centroid (v0 + v1 + v2) *
@@ -391,11 +410,11 @@ struct BoundAcc {
     }
 };
 
-template <int Q0, class ST, class PT, class SINK>
+template <int Q0, int H, class ST, class PT, class SINK>
 __device__ __forceinline__ void bins_private_half(const ST& St, const PT* src, uint32_t f0, uint32_t n, uint32_t tl,
                                                   uint32_t nl, uint32_t lane, int ax, float minB, float scale,
                                                   const SINK& sink) {
-    constexpr int H = kBins / 2;   // bins Q0 .. Q0 + 3 (half the registers of all eight)
+    // bins Q0 .. Q0 + H - 1 (H = 4: half the registers of all eight)
     uint32_t bc[H];
     float bl[H][3], bh[H][3];
 #pragma unroll
@@ -424,7 +443,7 @@ __device__ __forceinline__ void bins_private_half(const ST& St, const PT* src, u
         }
     }
 #if RTX_ANIM_BINS_TRANSPOSE
-    float v[32];   // index q * 8 + c: c 0 the count (exact: < 2^24), 1-3 the box minimum, 4-6 its maximum
+    float v[8 * H];   // index q * 8 + c: c 0 the count (exact: < 2^24), 1-3 the box minimum, 4-6 its maximum
 #pragma unroll
     for (int q = 0; q < H; ++q) {
         v[q * 8] = static_cast<float>(bc[q]);
@@ -433,8 +452,8 @@ __device__ __forceinline__ void bins_private_half(const ST& St, const PT* src, u
         v[q * 8 + 7] = 0.f;
     }
     uint32_t q, c;
-    const float r = wred_transpose(v, lane, q, c);
-    if (lane < 32u && c < 7u) sink.put1(ax, Q0 + static_cast<int>(q), c, r);
+    const float r = wred_transpose<8 * H>(v, lane, q, c);
+    if ((H == 8 || lane < 32u) && c < 7u) sink.put1(ax, Q0 + static_cast<int>(q), c, r);
 #else
     wred_sum(bc);
     wred_min(reinterpret_cast<float(&)[3 * H]>(bl));
@@ -448,8 +467,8 @@ __device__ __forceinline__ void bins_private_half(const ST& St, const PT* src, u
 // registers (branch-free: the other bins see their fold identity), then over the wave (DPP),
 // then into the slot: atomics (several waves) or plain stores (one wave).  Order-free (see
 // the header); used where lanes hold several elements, LDS atomics per element otherwise.
-// Two passes of four bins each keep the accumulators within the 128-VGPR budget of a
-// 1,024-thread workgroup.
+// All eight bins in one pass (the 256-VGPR budget of a 512-thread workgroup; two passes of four
+// bins with RTX_ANIM_BIN_PASSES=2: the root's bins 26 -> 23 us).
 // Sink of a wave's bins: a slot's bins (the team's, or the wave's own partial record that is
 // folded over the team's waves after a barrier — same-address LDS atomics from every wave of a
 // team serialised: 40 us a level).
@@ -471,8 +490,12 @@ template <class ST, class PT, class SINK>
 __device__ __forceinline__ void bins_private(const ST& St, const PT* src, uint32_t f0, uint32_t n, uint32_t tl,
                                              uint32_t nl, uint32_t lane, int ax, float minB, float scale,
                                              const SINK& sink) {
-    bins_private_half<0>(St, src, f0, n, tl, nl, lane, ax, minB, scale, sink);
-    bins_private_half<kBins / 2>(St, src, f0, n, tl, nl, lane, ax, minB, scale, sink);
+#if RTX_ANIM_BIN_PASSES == 1 && RTX_ANIM_BINS_TRANSPOSE
+    bins_private_half<0, kBins>(St, src, f0, n, tl, nl, lane, ax, minB, scale, sink);
+#else
+    bins_private_half<0, kBins / 2>(St, src, f0, n, tl, nl, lane, ax, minB, scale, sink);
+    bins_private_half<kBins / 2, kBins / 2>(St, src, f0, n, tl, nl, lane, ax, minB, scale, sink);
+#endif
 }
 
 // 4. the plane sweep (DataTypes.h:443-480) over the bins in the slot: lane j < 21 evaluates
