@@ -173,6 +173,9 @@ __device__ __forceinline__ void wred_min64(unsigned long long (&v)[N]) {
 // reductions of 15 steps each.  Lane l ends with the wave's fold of value
 // q = 2 (l & 1) + ((l >> 1) & 1), c = 4 ((l >> 2) & 1) + 2 ((l >> 3) & 1) + ((l >> 4) & 1)
 // (lanes l and l + 32 alike).  Order-free, like the other wave reductions.
+#ifndef RTX_ANIM_PRIV_MULTI
+#define RTX_ANIM_PRIV_MULTI 128   // (64ths of an element per lane: 128 = two elements per lane)
+#endif
 #ifndef RTX_ANIM_BIN_PASSES
 #define RTX_ANIM_BIN_PASSES 1   // register bins: all eight in one pass (1, 512-thread workgroups) or two halves (2)
 #endif
@@ -775,7 +778,9 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
     P* src = b ? St.perm[1] : St.perm[0];   // (selects: a dynamic index would put St in scratch)
     P* dst = b ? St.perm[0] : St.perm[1];
     const uint32_t nl = 64u * tm.k;
-    const uint32_t priv_min = 2u * nl;   // register bins when lanes hold several elements
+    // register bins when lanes hold several elements (several waves: from RTX_ANIM_PRIV_MULTI
+    // elements per 64 lanes, their LDS atomics on one slot serialise)
+    const uint32_t priv_min = MULTI ? (nl * RTX_ANIM_PRIV_MULTI) / 64u : 2u * nl;
     // the node's fields are wave-uniform: scalar registers (the VGPRs are the build's budget)
     uint32_t n = 0, first = 0, depth = 0;
     if (act) {
