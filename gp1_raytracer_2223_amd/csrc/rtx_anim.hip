@@ -698,7 +698,7 @@ __device__ __forceinline__ void node_small(const Store<LDS>& St, TmpNode* nodes,
     const Mask128 bigL{{valid.w[0] & ~small.w[0] & lt0, valid.w[1] & ~small.w[1] & lt1}};
     const Mask128 smallR{{small.w[0] & ~lt0, small.w[1] & ~lt1}};
     const uint32_t nR = static_cast<uint32_t>(__popcll(smallR.w[0]) + __popcll(smallR.w[1]));
-    const bool kids = S != 0u && S != n;
+    const bool kids = S != 0u && S < n;   // (S <= n always; < n also keeps a child count from wrapping)
     uint32_t dpos[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -965,7 +965,7 @@ __device__ __forceinline__ void node_process(const MeshDev& M, const Store<LDS>&
     tsync<MULTI>();
     stp(7);
     // leftCount 0 or all: a leaf with the permutation applied (both buffers)
-    const bool kids = split && S != 0u && S != n;
+    const bool kids = split && S != 0u && S < n;   // (S <= n always; < n also keeps a child count from wrapping)
     if (split && !kids)
         for (uint32_t q = tm.tl; q < n; q += nl) src[f0 + q] = dst[f0 + q];
     // 6. UpdateNodeBounds of both children (DataTypes.h:310-321), positions in the new order
@@ -1759,7 +1759,7 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
     }
     __syncthreads();
     // level by level (a task-split node's depth < 256: the build's depth limit)
-    const uint32_t dmax = s_dmax;
+    const uint32_t dmax = min(s_dmax, 255u);   // (s_depth is 8-bit: task-split nodes are < 256 levels deep)
     for (int d = static_cast<int>(dmax); d >= 0; --d) {
         for (uint32_t t = tid; t < ntop; t += kAnimThreads) {
             const int32_t l = s_l[t];
