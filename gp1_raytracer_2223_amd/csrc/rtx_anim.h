@@ -61,7 +61,7 @@ struct alignas(16) TmpNode {
     uint32_t pad[2];
 };
 
-// Per-subtree record written by the top phase and completed by the subtree build.
+// Per-subtree record written when a node becomes a subtree (make_subtree) and completed by its build.
 struct SubRec {
     uint32_t root;               // temp id of the subtree root (a child of a task-split node, or the root)
     uint32_t base;               // first temp id of its descendants (2 n - 2 slots reserved, from kMaxTop on)

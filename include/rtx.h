@@ -299,18 +299,19 @@ void rtx_anim_destroy(rtx_anim* anim);
 /* Reason for the anim's last error; with NULL, why this thread's last create failed. */
 const char* rtx_anim_last_error(const rtx_anim* anim);
 /* One Update: registered mesh i gets finalTransform = transforms[16 i .. 16 i + 15] (the
- * reference's Matrix, data[0..3] row-major).  Queued on ctx's stream after the previous
- * update (whichever context on the anim's device ran it); frames rendered on ctx
- * afterwards see the new geometry.  Build errors are reported by rtx_anim_status. */
+ * reference's Matrix, data[0..3] row-major).  Runs on the anim's own stream after the
+ * previous update (whichever context on the anim's device ran it); ctx's stream waits for it,
+ * so frames rendered on ctx afterwards see the new geometry.  Build errors are reported by
+ * rtx_anim_status. */
 int rtx_anim_update(rtx_anim* anim, rtx_ctx* ctx, const float* transforms);
 /* Waits for the last update.  status = {error bits (1: NaN vertex, 2: BVH too deep for the
- * render stack, 4: a subtree workgroup timed out waiting for the top levels; the frames
+ * render stack, 4: a build workgroup timed out waiting for a queue task; the frames
  * rendered from it are invalid), deepest level, nodesUsed, frontier parts}; returns
  * RTX_E_UNSUPPORTED when error bits are set. */
 int rtx_anim_status(rtx_anim* anim, uint32_t i, uint32_t status[4]);
 /* Diagnostics: 128 status words of the last update of registered mesh i (0-3 as above,
- * 4-6 subtrees / top-phase nodes / top-phase levels, 8-16 phase stamps of the device build at
- * 100 MHz; csrc/rtx_anim.h). */
+ * 4-6 subtrees / task-split ids / nodes split as tasks, 8-27 phase stamps of the device build
+ * at 100 MHz; csrc/rtx_anim.h). */
 int rtx_anim_stamps(rtx_anim* anim, uint32_t i, uint32_t out[128]);
 /* Waits for the last update and copies registered mesh i's state in the reference's own
  * form: transformedPositions (3V), indices (3T), normals (object space, 3T),
