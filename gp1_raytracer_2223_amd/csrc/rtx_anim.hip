@@ -81,47 +81,56 @@ __device__ __forceinline__ float min_key_value(unsigned long long k) {
 }
 __device__ __forceinline__ unsigned long long min_key_init() { return min_key(FLT_MAX, 0u); }
 
-// Order-free wave reductions through DPP row shifts (lanes outside the row keep the identity)
-// and the four row results read back (values only, see the header).
+// Order-free wave reductions through DPP row shifts (lanes outside the row keep the identity),
+// then the rows combined: DPP row broadcasts (lane 15 of rows 0 / 2 into rows 1 / 3, lane 31
+// into rows 2 and 3) and lane 63 read back, or (RTX_ANIM_DPP_BCAST=0) the four row results read
+// back (values only, see the header).
+#ifndef RTX_ANIM_DPP_BCAST
+#define RTX_ANIM_DPP_BCAST 1
+#endif
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp_ctl(uint32_t v, uint32_t identity) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(identity), static_cast<int>(v), CTRL,
+                                                             ROWS, 0xf, false));
+}
 template <int N>
 __device__ __forceinline__ uint32_t dpp_shr(uint32_t v, uint32_t identity) {
-    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(identity), static_cast<int>(v),
-                                                             0x110 + N, 0xf, 0xf, false));
+    return dpp_ctl<0x110 + N>(v, identity);
 }
 // Batched forms: N independent values per lane reduced together, one DPP step for all of them
 // at a time (back-to-back independent DPP moves need no hazard waits; a chain per value did:
-// ~7 us per axis of the root's bins), then the four row results read back.  Order-free.
-template <int SH, int N>
+// ~7 us per axis of the root's bins).  Order-free.
+template <int CTRL, int ROWS, int N>
 __device__ __forceinline__ void wred_step_min(float (&v)[N]) {
     float t[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) t[i] = __uint_as_float(dpp_shr<SH>(__float_as_uint(v[i]), __float_as_uint(FLT_MAX)));
+    for (int i = 0; i < N; ++i) t[i] = __uint_as_float(dpp_ctl<CTRL, ROWS>(__float_as_uint(v[i]), __float_as_uint(FLT_MAX)));
 #pragma unroll
     for (int i = 0; i < N; ++i) v[i] = fminf(v[i], t[i]);
 }
-template <int SH, int N>
+template <int CTRL, int ROWS, int N>
 __device__ __forceinline__ void wred_step_max(float (&v)[N]) {
     float t[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) t[i] = __uint_as_float(dpp_shr<SH>(__float_as_uint(v[i]), __float_as_uint(FLT_MIN)));
+    for (int i = 0; i < N; ++i) t[i] = __uint_as_float(dpp_ctl<CTRL, ROWS>(__float_as_uint(v[i]), __float_as_uint(FLT_MIN)));
 #pragma unroll
     for (int i = 0; i < N; ++i) v[i] = fmaxf(v[i], t[i]);
 }
-template <int SH, int N>
+template <int CTRL, int ROWS, int N>
 __device__ __forceinline__ void wred_step_sum(uint32_t (&v)[N]) {
     uint32_t t[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) t[i] = dpp_shr<SH>(v[i], 0u);
+    for (int i = 0; i < N; ++i) t[i] = dpp_ctl<CTRL, ROWS>(v[i], 0u);
 #pragma unroll
     for (int i = 0; i < N; ++i) v[i] += t[i];
 }
-template <int SH, int N>
+template <int CTRL, int ROWS, int N>
 __device__ __forceinline__ void wred_step_min64(unsigned long long (&v)[N]) {
     uint32_t lo[N], hi[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        lo[i] = dpp_shr<SH>(static_cast<uint32_t>(v[i]), ~0u);
-        hi[i] = dpp_shr<SH>(static_cast<uint32_t>(v[i] >> 32), ~0u);
+        lo[i] = dpp_ctl<CTRL, ROWS>(static_cast<uint32_t>(v[i]), ~0u);
+        hi[i] = dpp_ctl<CTRL, ROWS>(static_cast<uint32_t>(v[i] >> 32), ~0u);
     }
 #pragma unroll
     for (int i = 0; i < N; ++i) {
@@ -129,26 +138,47 @@ __device__ __forceinline__ void wred_step_min64(unsigned long long (&v)[N]) {
         v[i] = w < v[i] ? w : v[i];
     }
 }
+// the four row steps (lane 15 of each row then holds the row's fold), then the rows
+#define RTX_WRED_ROWS(step, v) step<0x111, 0xf>(v); step<0x112, 0xf>(v); step<0x114, 0xf>(v); step<0x118, 0xf>(v)
+#define RTX_WRED_BCAST(step, v) step<0x142, 0xa>(v); step<0x143, 0xc>(v)
 __device__ __forceinline__ float rl(float v, int l) { return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), l)); }
 template <int N>
 __device__ __forceinline__ void wred_min(float (&v)[N]) {
-    wred_step_min<1>(v); wred_step_min<2>(v); wred_step_min<4>(v); wred_step_min<8>(v);
+    RTX_WRED_ROWS(wred_step_min, v);
+#if RTX_ANIM_DPP_BCAST
+    RTX_WRED_BCAST(wred_step_min, v);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = rl(v[i], 63);
+#else
 #pragma unroll
     for (int i = 0; i < N; ++i) v[i] = fminf(fminf(rl(v[i], 15), rl(v[i], 31)), fminf(rl(v[i], 47), rl(v[i], 63)));
+#endif
 }
 template <int N>
 __device__ __forceinline__ void wred_max(float (&v)[N]) {
-    wred_step_max<1>(v); wred_step_max<2>(v); wred_step_max<4>(v); wred_step_max<8>(v);
+    RTX_WRED_ROWS(wred_step_max, v);
+#if RTX_ANIM_DPP_BCAST
+    RTX_WRED_BCAST(wred_step_max, v);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = rl(v[i], 63);
+#else
 #pragma unroll
     for (int i = 0; i < N; ++i) v[i] = fmaxf(fmaxf(rl(v[i], 15), rl(v[i], 31)), fmaxf(rl(v[i], 47), rl(v[i], 63)));
+#endif
 }
 template <int N>
 __device__ __forceinline__ void wred_sum(uint32_t (&v)[N]) {
-    wred_step_sum<1>(v); wred_step_sum<2>(v); wred_step_sum<4>(v); wred_step_sum<8>(v);
+    RTX_WRED_ROWS(wred_step_sum, v);
+#if RTX_ANIM_DPP_BCAST
+    RTX_WRED_BCAST(wred_step_sum, v);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = __builtin_amdgcn_readlane(v[i], 63);
+#else
 #pragma unroll
     for (int i = 0; i < N; ++i)
         v[i] = __builtin_amdgcn_readlane(v[i], 15) + __builtin_amdgcn_readlane(v[i], 31) +
                __builtin_amdgcn_readlane(v[i], 47) + __builtin_amdgcn_readlane(v[i], 63);
+#endif
 }
 __device__ __forceinline__ unsigned long long rl64(unsigned long long v, int l) {
     return (static_cast<unsigned long long>(__builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), l)) << 32) |
@@ -156,13 +186,19 @@ __device__ __forceinline__ unsigned long long rl64(unsigned long long v, int l) 
 }
 template <int N>
 __device__ __forceinline__ void wred_min64(unsigned long long (&v)[N]) {
-    wred_step_min64<1>(v); wred_step_min64<2>(v); wred_step_min64<4>(v); wred_step_min64<8>(v);
+    RTX_WRED_ROWS(wred_step_min64, v);
+#if RTX_ANIM_DPP_BCAST
+    RTX_WRED_BCAST(wred_step_min64, v);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = rl64(v[i], 63);
+#else
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const unsigned long long r0 = rl64(v[i], 15), r1 = rl64(v[i], 31), r2 = rl64(v[i], 47), r3 = rl64(v[i], 63);
         const unsigned long long a = r0 < r1 ? r0 : r1, b = r2 < r3 ? r2 : r3;
         v[i] = a < b ? a : b;
     }
+#endif
 }
 
 // Transposing wave reduction of 32 values per lane, index q * 8 + c (c 0: a sum, 1-3: a
