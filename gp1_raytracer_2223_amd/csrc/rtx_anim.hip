@@ -1193,36 +1193,66 @@ __device__ __forceinline__ void top_phase(const Launch& L, const MeshDev& M, Lev
     }
     float* rec = const_cast<float*>(St.rec);
     // ---- UpdateTransforms (DataTypes.h:210-230)
-    for (uint32_t v = tid; v < V; v += kAnimThreads) {
-        const float4 p = M.pos[v];
-        const float3 t = xform_point(mat, p.x, p.y, p.z);
-        M.tpos[v] = make_float4(t.x, t.y, t.z, 0.f);
+    for (uint32_t v0 = tid; v0 < V; v0 += 4u * kAnimThreads) {   // (four vertices per thread at a time)
+        float4 p[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) {
+            const uint32_t v = v0 + j * kAnimThreads;
+            p[j] = v < V ? M.pos[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) {
+            const uint32_t v = v0 + j * kAnimThreads;
+            if (v >= V) continue;
+            const float3 t = xform_point(mat, p[j].x, p[j].y, p[j].z);
+            M.tpos[v] = make_float4(t.x, t.y, t.z, 0.f);
+        }
     }
     __syncthreads();
     // per triangle: transformed normal (input order), centroid, box; the identity permutation;
     // the root's bounds over the input order (BuildBVH, DataTypes.h:294-308)
+    // (four triangles per thread at a time: their index and vertex loads issued together)
     BoundAcc A;
-    for (uint32_t k = tid; k < T; k += kAnimThreads) {
-        const float4 n = nrm[k];
-        const float3 tn = normalized(xform_vector(mat, n.x, n.y, n.z));
-        M.tnrm[k] = make_float4(tn.x, tn.y, tn.z, 0.f);
-        const int4 i = idx[k];
-        const float4 v0 = M.tpos[i.x], v1 = M.tpos[i.y], v2 = M.tpos[i.z];
-        if (v0.x != v0.x || v0.y != v0.y || v0.z != v0.z || v1.x != v1.x || v1.y != v1.y || v1.z != v1.z ||
-            v2.x != v2.x || v2.y != v2.y || v2.z != v2.z)
-            atomicOr(&Lv.err, kErrNaN);
-        // (v0 + v1 + v2) * 0.3333f, the reference's centroid (DataTypes.h:348, 411-415, 435)
-        const float r9[9] = {((v0.x + v1.x) + v2.x) * 0.3333f, ((v0.y + v1.y) + v2.y) * 0.3333f,
-                             ((v0.z + v1.z) + v2.z) * 0.3333f,
-                             rmin(rmin(v0.x, v1.x), v2.x), rmin(rmin(v0.y, v1.y), v2.y), rmin(rmin(v0.z, v1.z), v2.z),
-                             rmax(rmax(v0.x, v1.x), v2.x), rmax(rmax(v0.y, v1.y), v2.y), rmax(rmax(v0.z, v1.z), v2.z)};
+    constexpr uint32_t kB = 4;
+    for (uint32_t k0 = tid; k0 < T; k0 += kB * kAnimThreads) {
+        int4 ii[kB];
+        float4 nn[kB], v[kB][3];
 #pragma unroll
-        for (int c = 0; c < 9; ++c) {
-            soa[c * T + k] = r9[c];
-            if (LDS) rec[c * T + k] = r9[c];
+        for (uint32_t j = 0; j < kB; ++j) {
+            const uint32_t k = k0 + j * kAnimThreads;
+            ii[j] = k < T ? idx[k] : make_int4(0, 0, 0, 0);
+            nn[j] = k < T ? nrm[k] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        St.perm[0][k] = static_cast<typename Store<LDS>::P>(k);
-        A.add(St, k, 1u + k);
+#pragma unroll
+        for (uint32_t j = 0; j < kB; ++j) {
+            const bool in = k0 + j * kAnimThreads < T;
+            v[j][0] = in ? M.tpos[ii[j].x] : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[j][1] = in ? M.tpos[ii[j].y] : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[j][2] = in ? M.tpos[ii[j].z] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kB; ++j) {
+            const uint32_t k = k0 + j * kAnimThreads;
+            if (k >= T) continue;
+            const float3 tn = normalized(xform_vector(mat, nn[j].x, nn[j].y, nn[j].z));
+            M.tnrm[k] = make_float4(tn.x, tn.y, tn.z, 0.f);
+            const float4 v0 = v[j][0], v1 = v[j][1], v2 = v[j][2];
+            if (v0.x != v0.x || v0.y != v0.y || v0.z != v0.z || v1.x != v1.x || v1.y != v1.y || v1.z != v1.z ||
+                v2.x != v2.x || v2.y != v2.y || v2.z != v2.z)
+                atomicOr(&Lv.err, kErrNaN);
+            // (v0 + v1 + v2) * 0.3333f, the reference's centroid (DataTypes.h:348, 411-415, 435)
+            const float r9[9] = {((v0.x + v1.x) + v2.x) * 0.3333f, ((v0.y + v1.y) + v2.y) * 0.3333f,
+                                 ((v0.z + v1.z) + v2.z) * 0.3333f,
+                                 rmin(rmin(v0.x, v1.x), v2.x), rmin(rmin(v0.y, v1.y), v2.y), rmin(rmin(v0.z, v1.z), v2.z),
+                                 rmax(rmax(v0.x, v1.x), v2.x), rmax(rmax(v0.y, v1.y), v2.y), rmax(rmax(v0.z, v1.z), v2.z)};
+#pragma unroll
+            for (int c = 0; c < 9; ++c) {
+                soa[c * T + k] = r9[c];
+                if (LDS) rec[c * T + k] = r9[c];
+            }
+            St.perm[0][k] = static_cast<typename Store<LDS>::P>(k);
+            A.addv(r9[3], r9[4], r9[5], r9[6], r9[7], r9[8], 1u + k);
+        }
     }
     A.wave();
     Slot& s0 = slots[0];
