@@ -2618,7 +2618,7 @@ extern "C" int rtx_debug_stamps(rtx_ctx* c, const rtx_camera* cam, const rtx_ren
 // triangle records, node pairs (+ octant copies) and frontier parts.
 // Device Update: nodes above this many triangles are split by a whole workgroup as queue
 // tasks, smaller ones built as subtrees by one workgroup each (rtx_anim.h)
-constexpr uint32_t kAnimCut = 128;
+constexpr uint32_t kAnimCut = 96;
 
 struct rtx_anim {
     int device = 0;
