@@ -2635,9 +2635,10 @@ struct rtx_anim {
     float room_p0[5] = {};   // rtx_ctx::room_p0 of the registration upload
     std::string sig;
     hipEvent_t ev = nullptr;              // the last update
-    // The updates' own stream, high priority (RTX_ANIM_SAME_STREAM=1: the context's stream): an
-    // update then runs beside the render of the previous frame (another context's stream)
-    // instead of queueing behind its workgroups; the context's next render waits for it.
+    // RTX_ANIM_OWN_STREAM=1: the updates run on the anim's own stream (high priority;
+    // RTX_ANIM_STREAM_PRIO=normal: default priority) beside the previous frame's render, the
+    // context's next render waiting for its event; default: on the context's stream, which
+    // measured faster in 4 of 6 animated-loop cases (profiles/r03/anim_benchmark_update_stream.log)
     hipStream_t stream = nullptr;
     bool built = false;
     uint32_t cur = 0;                     // state buffer of the current order
@@ -2757,10 +2758,12 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
     } while (0)
     ANIM_CREATE_TRY(hipSetDevice(c->device));
     ANIM_CREATE_TRY(hipEventCreateWithFlags(&a->ev, hipEventDisableTiming));
-    if (!std::getenv("RTX_ANIM_SAME_STREAM")) {
+    if (std::getenv("RTX_ANIM_OWN_STREAM") && !std::getenv("RTX_ANIM_SAME_STREAM")) {
         int lo_prio = 0, hi_prio = 0;
         ANIM_CREATE_TRY(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
-        ANIM_CREATE_TRY(hipStreamCreateWithPriority(&a->stream, hipStreamNonBlocking, hi_prio));
+        const char* pr = std::getenv("RTX_ANIM_STREAM_PRIO");   // "normal": the default priority (tests)
+        ANIM_CREATE_TRY(hipStreamCreateWithPriority(&a->stream, hipStreamNonBlocking,
+                                                    pr && std::string(pr) == "normal" ? lo_prio : hi_prio));
     }
     a->total = lay.total;
     a->tri_off = lay.tri_off; a->node_off = lay.node_off; a->part_off = lay.part_off; a->mesh_off = lay.mesh_off;

@@ -299,10 +299,9 @@ void rtx_anim_destroy(rtx_anim* anim);
 /* Reason for the anim's last error; with NULL, why this thread's last create failed. */
 const char* rtx_anim_last_error(const rtx_anim* anim);
 /* One Update: registered mesh i gets finalTransform = transforms[16 i .. 16 i + 15] (the
- * reference's Matrix, data[0..3] row-major).  Runs on the anim's own stream after the
- * previous update (whichever context on the anim's device ran it); ctx's stream waits for it,
- * so frames rendered on ctx afterwards see the new geometry.  Build errors are reported by
- * rtx_anim_status. */
+ * reference's Matrix, data[0..3] row-major).  Queued on ctx's stream after the previous
+ * update (whichever context on the anim's device ran it); frames rendered on ctx afterwards
+ * see the new geometry.  Build errors are reported by rtx_anim_status. */
 int rtx_anim_update(rtx_anim* anim, rtx_ctx* ctx, const float* transforms);
 /* Waits for the last update.  status = {error bits (1: NaN vertex, 2: BVH too deep for the
  * render stack, 4: a build workgroup timed out waiting for a queue task; the frames

@@ -113,9 +113,14 @@ def test_device_update_matches_oracle_full_resolution(name):
     ctx.close()
 
 
-def test_device_update_frames_in_flight_two_contexts():
+@pytest.mark.parametrize("own_stream", [False, True], ids=["context_stream", "own_stream"])
+def test_device_update_frames_in_flight_two_contexts(own_stream, monkeypatch):
     """Updates alternate between two contexts (frames in flight): each context's image holds
-    the Update it was given, and the permutation chain runs through both."""
+    the Update it was given, and the permutation chain runs through both — with the updates on
+    the contexts' streams or on the anim's own stream (RTX_ANIM_OWN_STREAM=1, read at
+    rtx_anim_create)."""
+    if own_stream:
+        monkeypatch.setenv("RTX_ANIM_OWN_STREAM", "1")
     dev_scene, host_scene = _scene("W4_Optional"), _scene("W4_Optional")
     a, b, ref = DeviceContext(0), DeviceContext(0), DeviceContext(0)
     anim = DeviceAnimation(dev_scene, a)
