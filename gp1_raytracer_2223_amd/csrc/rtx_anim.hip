@@ -212,6 +212,9 @@ __device__ __forceinline__ void wred_min64(unsigned long long (&v)[N]) {
 #ifndef RTX_ANIM_PRIV_MULTI
 #define RTX_ANIM_PRIV_MULTI 128   // (64ths of an element per lane: 128 = two elements per lane)
 #endif
+#ifndef RTX_ANIM_KEEP_CHILD
+#define RTX_ANIM_KEEP_CHILD 1   // a split task goes on with its larger child instead of queueing it
+#endif
 #ifndef RTX_ANIM_BIN_PASSES
 #define RTX_ANIM_BIN_PASSES 1   // register bins: all eight in one pass (1, 512-thread workgroups) or two halves (2)
 #endif
@@ -1136,8 +1139,10 @@ __device__ __forceinline__ void make_subtree(const Launch& L, const MeshDev& M, 
 // A child of 3 n <= 8 indices is a leaf (Subdivide returns at once), a child above the cut a
 // split task (ids for its children reserved now), any other a subtree.  `done` counts the
 // triangles whose leaves are final: the workers stop when it reaches T.
+// keep (optional): the larger child that is itself a split is not queued but returned in
+// keep[0] (its reserved ids in keep[1]; ~0u: none) for the calling workgroup to split next.
 __device__ __forceinline__ void dispatch_children(const Launch& L, const MeshDev& M, uint32_t n, uint32_t d, uint32_t K,
-                                                  uint32_t c0, uint32_t t_start) {
+                                                  uint32_t c0, uint32_t t_start, uint32_t* keep = nullptr) {
     __threadfence();
     const uint32_t k = atomicAdd(&M.status[6], 1u);
     if (k < 4u) {   // diagnostics: the first four splits' size, start and end
@@ -1151,6 +1156,7 @@ __device__ __forceinline__ void dispatch_children(const Launch& L, const MeshDev
         return;
     }
     atomicMax(&M.status[1], d + 1u);
+    const uint32_t kc = M.tmp[c0].count >= M.tmp[c0 + 1u].count ? c0 : c0 + 1u;   // the larger child
     for (uint32_t c = c0; c < c0 + 2u; ++c) {
         const uint32_t nc = M.tmp[c].count;
         if (3u * nc <= 8u) {
@@ -1161,6 +1167,11 @@ __device__ __forceinline__ void dispatch_children(const Launch& L, const MeshDev
             const uint32_t r = atomicAdd(&M.q[kQTop], 2u);
             reserve_ids(M, r);
             if (r + 2u <= static_cast<uint32_t>(kMaxTop)) {
+                if (keep && c == kc) {
+                    keep[0] = c;
+                    keep[1] = r;
+                    continue;
+                }
                 __threadfence();
                 push_task(L, M, 0x80000000u | c, r);
                 continue;
@@ -1387,17 +1398,43 @@ __device__ __forceinline__ void run_task(const Launch& L, const MeshDev& M, uint
                                             split ? nullptr : lvl_base, kSubLevels,
                                             (!split && f == 0) ? M.status + 32 : nullptr, 8u);
     if (split) {
-        // the node's range in its new order into both buffers (a leaf child's range is final)
-        const P* dst = b ? St.perm[0] : St.perm[1];
-        uint32_t* hdst = M.perm[b ^ 1u];
-        for (uint32_t q = tid; q < n; q += kAnimThreads) {
-            const uint32_t v = LDS ? gmap[dst[q]] : hdst[first + q];
-            if (LDS) hdst[first + q] = v;
-            M.perm[b][first + q] = v;
+        // Split, then keep splitting the larger child in this workgroup while it is a split task
+        // (its records are staged here already: positions relative to St.pos0), the other child
+        // queued; each node's range in its new order into both buffers (a leaf child's range is
+        // final; the next level rewrites the kept child's).
+        uint32_t tc = t, nc = n, dc = D, fc = first, ts = t_start;
+        uint32_t* keep = s_list + 4;
+        for (;;) {
+            const uint32_t bc = dc & 1u, f0c = fc - St.pos0;
+            const P* dst = bc ? St.perm[0] : St.perm[1];
+            uint32_t* hdst = M.perm[bc ^ 1u];
+            for (uint32_t q = tid; q < nc; q += kAnimThreads) {
+                const uint32_t v = LDS ? gmap[dst[f0c + q]] : hdst[fc + q];
+                if (LDS) hdst[fc + q] = v;
+                M.perm[bc][fc + q] = v;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                keep[0] = ~0u;
+                dispatch_children(L, M, nc, dc, Lv.K, rg.cur[0], ts, RTX_ANIM_KEEP_CHILD ? keep : nullptr);
+            }
+            __syncthreads();
+            const uint32_t kt = keep[0], kid = keep[1];
+            if (!RTX_ANIM_KEEP_CHILD || kt == ~0u) return;
+            tc = kt;
+            dc += 1u;
+            nc = M.tmp[tc].count;
+            fc = M.tmp[tc].first;
+            ts = stamp();
+            __syncthreads();   // (everyone has read keep[] and the node)
+            if (tid == 0) {
+                Lv.K = 1; Lv.next = 0; Lv.take = 0; Lv.maxn = nc; Lv.nmaxn = 0; Lv.ids = kid; Lv.err = 0;
+                s_list[0] = tc;
+            }
+            __syncthreads();
+            rg = Region{s_list, s_list + 2};
+            build_levels<LDS>(M, St, M.tmp, Lv, slots, rg, dc, 1u, kMaxSub, nullptr, 0u);
         }
-        __syncthreads();
-        if (tid == 0) dispatch_children(L, M, n, D, Lv.K, rg.cur[0], t_start);
-        return;
     }
     if (f == 0 && tid == 0) M.status[30] = stamp();   // subtree 0: levels done
     if (LDS)   // the final order (every leaf range is current in both buffers) as triangle ids
@@ -1485,7 +1522,7 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
     __shared__ Level Lv;
     __shared__ Slot slots[kAnimWaves];
     __shared__ uint32_t lvl_base[kSubLevels + 1];
-    __shared__ uint32_t s_list[4];
+    __shared__ uint32_t s_list[8];   // level lists of a split task (4) and its kept child (2)
     __shared__ uint32_t s_task[3];
     const uint32_t tid = threadIdx.x;
     if (blockIdx.y == 0) {
