@@ -1307,17 +1307,41 @@ __device__ __forceinline__ void top_phase(const Launch& L, const MeshDev& M, Lev
         }
         __syncthreads();
         Region rg{s_list, s_list + 2};
-        if constexpr (LDS) build_levels<LDS>(M, St, M.tmp, Lv, slots, rg, 0u, 1u, kMaxSub, nullptr, 0u);
-        // the new order (triangle ids) into both buffers (a leaf child's range is final)
-        for (uint32_t k = tid; k < T; k += kAnimThreads) {
-            const uint32_t v = LDS ? static_cast<uint32_t>(St.perm[1][k]) : M.perm[1][k];
-            if (LDS) M.perm[1][k] = v;
-            M.perm[0][k] = v;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            M.status[kStTopDone] = stamp();
-            dispatch_children(L, M, T, 0u, Lv.K, rg.cur[0], M.status[kStSetup]);
+        if constexpr (LDS) {
+            // the root, then the larger child while it is a split task, like run_task (records by
+            // triangle id, staged for the whole mesh); each node's range in its new order into both
+            // buffers
+            uint32_t nc = T, dc = 0, fc = 0, ts = M.status[kStSetup];
+            uint32_t* keep = s_list + 4;
+            for (;;) {
+                rg = Region{s_list, s_list + 2};
+                build_levels<LDS>(M, St, M.tmp, Lv, slots, rg, dc, 1u, kMaxSub, nullptr, 0u);
+                const uint32_t bc = dc & 1u;
+                for (uint32_t k = tid; k < nc; k += kAnimThreads) {
+                    const uint32_t v = static_cast<uint32_t>(St.perm[bc ^ 1u][fc + k]);
+                    M.perm[bc ^ 1u][fc + k] = v;
+                    M.perm[bc][fc + k] = v;
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    if (dc == 0) M.status[kStTopDone] = stamp();
+                    keep[0] = ~0u;
+                    dispatch_children(L, M, nc, dc, Lv.K, rg.cur[0], ts, RTX_ANIM_KEEP_CHILD ? keep : nullptr);
+                }
+                __syncthreads();
+                const uint32_t kt = keep[0], kid = keep[1];
+                if (!RTX_ANIM_KEEP_CHILD || kt == ~0u) break;
+                dc += 1u;
+                nc = M.tmp[kt].count;
+                fc = M.tmp[kt].first;
+                ts = stamp();
+                __syncthreads();
+                if (tid == 0) {
+                    Lv.K = 1; Lv.next = 0; Lv.take = 0; Lv.maxn = nc; Lv.nmaxn = 0; Lv.ids = kid; Lv.err = 0;
+                    s_list[0] = kt;
+                }
+                __syncthreads();
+            }
         }
     } else {
         if (LDS)
