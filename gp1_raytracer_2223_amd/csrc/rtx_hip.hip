@@ -897,10 +897,24 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         const uint32_t pos = ((k / kRun) * 8u + x) * kRun + (k % kRun);
         widx = pos * kWavesPerBlock + wave;
     }
+    if (PHASE == 0 && F.band_tiles) {
+        // XCD bands: workgroups go round robin to the 8 XCDs (blockIdx % 8), each with its own
+        // 4 MB L2.  XCD x takes dispatch slots [x, x + 1) * band_tiles, which the schedule fills
+        // with band x of the image (consecutive tiles, heaviest first: rtx_sched_scan), so one
+        // XCD's rays walk the part of the scene its band sees.  A bijection onto [0, n_tiles)
+        // (the host sizes the grid 8 x band_tiles / kWavesPerBlock; the rest return).
+        const uint32_t bpb = F.band_tiles / kWavesPerBlock, k = b >> 3;
+        widx = k < bpb ? ((b & 7u) * bpb + k) * kWavesPerBlock + wave : 8u * F.band_tiles;
+        widx = __builtin_amdgcn_readfirstlane(widx);   // wave-uniform: keep the scalar tile loads
+    }
     uint32_t tile, part = 0, light = 0;
     if (PHASE == 0) {
-        if (widx >= F.n_tiles) return;
-        tile = F.order ? ldc(F.order, widx) : widx;
+        // (XCD bands: slots up to 8 x band_tiles, free ones holding the no-tile marker ~0u)
+        const uint32_t lim = F.band_tiles ? 8u * F.band_tiles : F.n_tiles;
+        const uint32_t w = widx < lim ? widx : 0u;
+        tile = F.order ? ldc(F.order, w) : w;
+        tile = __builtin_amdgcn_readfirstlane(widx < lim ? tile : ~0u);   // wave-uniform
+        if (tile >= F.n_tiles) return;
         if (F.heavy_flag && ldc(F.heavy_flag, tile)) return;   // rendered by the split launches
     } else {
         // grid (heavy tiles / waves per block, parts, lights), tile fastest: every heavy tile's part 0 is
@@ -1387,27 +1401,79 @@ __global__ void __launch_bounds__(kReorderThreads) rtx_sched_count(uint32_t* __r
 
 // Exclusive prefix of hist[class][chunk] in class-major order (in place), the total cost and
 // the heavy threshold; zeroes the heavy counter the scatter appends to.
+// XCD bands (band_tiles != 0, nchunks <= kScanThreads): the chunks (kSchedChunk consecutive
+// tiles: a few image rows) are dealt to the 8 XCDs in snake order of their measured cost
+// (heaviest chunk to XCD 0, the next to XCD 1, ..., the 9th to XCD 7, the 10th to XCD 6, ...),
+// so every XCD gets the same number of chunks and about the same cost.  The prefix then runs
+// band-major (band, class, chunk) and band x's slots start at x * band_tiles; the slots a band
+// leaves free get the no-tile marker ~0u in `order`.
 __global__ void __launch_bounds__(kScanThreads) rtx_sched_scan(uint32_t* __restrict__ hist, uint32_t nchunks,
+                                                               uint32_t band_tiles, uint32_t* __restrict__ order,
                                                                const unsigned long long* __restrict__ csum, uint32_t n,
                                                                uint32_t split_slots, uint32_t split_permille,
                                                                unsigned long long* __restrict__ thr_out,
                                                                uint32_t* __restrict__ heavy_n) {
     __shared__ uint32_t part[kScanThreads];
     __shared__ unsigned long long cpart[kScanThreads];
+    __shared__ uint32_t s_chunk[kScanThreads];   // XCD bands: chunks in (band, round) order
+    __shared__ uint32_t s_nb[8], s_cnt[8], s_fc[8], s_fb[8], s_off[8];
     const uint32_t tid = threadIdx.x;
+    const bool bands = band_tiles != 0u;
+    uint32_t my_band = 0, my_round = 0;
+    if (bands) {
+        if (tid < 8u) { s_nb[tid] = 0u; s_cnt[tid] = 0u; }
+        __syncthreads();
+        if (tid < nchunks) {
+            const unsigned long long my = csum[tid];
+            uint32_t rank = 0;
+            for (uint32_t j = 0; j < nchunks; ++j) {
+                const unsigned long long o = csum[j];
+                rank += (o > my || (o == my && j < tid)) ? 1u : 0u;
+            }
+            my_round = rank >> 3;
+            my_band = (my_round & 1u) ? 7u - (rank & 7u) : (rank & 7u);
+            atomicAdd(&s_nb[my_band], 1u);
+            atomicAdd(&s_cnt[my_band], min(static_cast<uint32_t>(kSchedChunk), n - tid * kSchedChunk));
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t fc = 0, tiles = 0;
+            for (uint32_t x = 0; x < 8u; ++x) {
+                s_fc[x] = fc;
+                s_fb[x] = fc * kCostBuckets;
+                s_off[x] = x * band_tiles - tiles;
+                fc += s_nb[x];
+                tiles += s_cnt[x];
+            }
+        }
+        __syncthreads();
+        if (tid < nchunks) s_chunk[s_fc[my_band] + my_round] = tid;
+        __syncthreads();
+    }
+    // entry i of the scan order -> its hist index and slot offset
+    auto hidx = [&](uint32_t i, uint32_t& off) -> uint32_t {
+        off = 0;
+        if (!bands) return i;
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t y = 1; y < 8u; ++y) x += i >= s_fb[y] ? 1u : 0u;
+        const uint32_t r = i - s_fb[x], nb = s_nb[x], cls = r / nb;
+        off = s_off[x];
+        return cls * nchunks + s_chunk[s_fc[x] + (r - cls * nb)];
+    };
     const uint32_t len = kCostBuckets * nchunks;
     const uint32_t per = (len + kScanThreads - 1) / kScanThreads;
     const uint32_t lo = tid * per, hi = (lo + per < len) ? lo + per : len;
-    uint32_t s = 0;
-    for (uint32_t i = lo; i < hi; ++i) s += hist[i];
+    uint32_t s = 0, off = 0;
+    for (uint32_t i = lo; i < hi; ++i) s += hist[hidx(i, off)];
     unsigned long long cs = 0;
     for (uint32_t i = tid; i < nchunks; i += kScanThreads) cs += csum[i];
     part[tid] = s;
     cpart[tid] = cs;
     __syncthreads();
-    for (uint32_t off = 1; off < kScanThreads; off <<= 1) {   // inclusive Hillis-Steele scan
-        const uint32_t v = tid >= off ? part[tid - off] : 0u;
-        const unsigned long long w = tid >= off ? cpart[tid - off] : 0ull;
+    for (uint32_t o = 1; o < kScanThreads; o <<= 1) {   // inclusive Hillis-Steele scan
+        const uint32_t v = tid >= o ? part[tid - o] : 0u;
+        const unsigned long long w = tid >= o ? cpart[tid - o] : 0ull;
         __syncthreads();
         part[tid] += v;
         cpart[tid] += w;
@@ -1415,10 +1481,13 @@ __global__ void __launch_bounds__(kScanThreads) rtx_sched_scan(uint32_t* __restr
     }
     uint32_t acc = part[tid] - s;   // exclusive
     for (uint32_t i = lo; i < hi; ++i) {
-        const uint32_t v = hist[i];
-        hist[i] = acc;
+        const uint32_t h = hidx(i, off), v = hist[h];
+        hist[h] = acc + off;
         acc += v;
     }
+    if (bands)
+        for (uint32_t x = 0; x < 8u; ++x)
+            for (uint32_t k = s_cnt[x] + tid; k < band_tiles; k += kScanThreads) order[x * band_tiles + k] = ~0u;
     if (tid == 0) {
         const unsigned long long total = cpart[kScanThreads - 1];
         const bool force = split_slots == 0xffffffffu;
@@ -1531,9 +1600,11 @@ struct rtx_ctx {
     unsigned long long* d_csum = nullptr;   // per chunk cost sums
     unsigned long long* d_thr = nullptr;    // heavy threshold of the measured frame
     uint32_t sched_cap = 0;
+    uint32_t order_cap = 0;          // slots of d_order (XCD bands pad them to 8 x band_tiles)
     std::string sched_key;
     bool sched_ready = false;
     bool sched_enabled = true;
+    bool xcd_bands = false;          // RTX_XCD_BANDS=1: band x of the image on XCD x (see the kernel)
     uint64_t sched_frame = 0;
     uint64_t scene_gen = 0;
     // split rendering of heavy tiles: double-buffered flag/list sets (the reorder kernel
@@ -1688,6 +1759,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     // RTX_TILE_ORDER=0 disables cost-ordered tile dispatch (identity order every frame)
     if (const char* e = std::getenv("RTX_TILE_ORDER")) c->sched_enabled = std::strcmp(e, "0") != 0;
     // RTX_SPLIT=0 renders heavy tiles in one piece; RTX_SPLIT=force splits every tile
+    if (const char* e = std::getenv("RTX_XCD_BANDS")) c->xcd_bands = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_NO_SPEC")) c->no_spec = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_SPLIT")) c->split_mode = std::strcmp(e, "0") == 0 ? 0u : (std::strcmp(e, "force") == 0 ? 2u : 1u);
     if (const char* e = std::getenv("RTX_SPLIT_PARTS")) {
@@ -2179,9 +2251,18 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     F.n_tiles = ntiles;
     uint32_t nblocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
     if (RTX_XCD_RUN > 1) nblocks = (nblocks + 8 * RTX_XCD_RUN - 1) / (8 * RTX_XCD_RUN) * (8 * RTX_XCD_RUN);
+    F.band_tiles = 0;
+    const uint32_t nch_all = (ntiles + kSchedChunk - 1) / kSchedChunk;
+    if (c->xcd_bands && RTX_XCD_RUN <= 1 && nch_all <= static_cast<uint32_t>(kScanThreads)) {
+        // XCD bands (the kernel, rtx_sched_scan): the same number of whole scheduling chunks
+        // per XCD, band x's slots from x * band_tiles
+        F.band_tiles = (nch_all + 7u) / 8u * kSchedChunk;
+        nblocks = 8u * (F.band_tiles / kWavesPerBlock);
+    }
+    const uint32_t order_slots = F.band_tiles ? 8u * F.band_tiles : ntiles;
     grid = dim3(nblocks, 1, 1);
     // Cost-ordered dispatch (see the kernel): keep one order/cost pair per launch shape.
-    if (ntiles > c->sched_cap) {
+    if (ntiles > c->sched_cap || order_slots > c->order_cap) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         (void)hipFree(c->d_order);
         (void)hipFree(c->d_cost);
@@ -2195,7 +2276,9 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         c->d_order = nullptr;
         c->d_cost = nullptr;
         c->sched_cap = 0;
-        HIP_TRY(c, hipMalloc(&c->d_order, ntiles * 4));
+        c->order_cap = 0;
+        HIP_TRY(c, hipMalloc(&c->d_order, static_cast<size_t>(std::max(ntiles, order_slots)) * 4));
+        c->order_cap = std::max(ntiles, order_slots);
         HIP_TRY(c, hipMalloc(&c->d_cost, ntiles * 4));
         for (int k = 0; k < 2; ++k) HIP_TRY(c, hipMalloc(&c->d_heavy_flag[k], ntiles * 4));
         HIP_TRY(c, hipMalloc(&c->d_saved_cost, ntiles * 4));
@@ -2358,7 +2441,8 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         hipLaunchKernelGGL(rtx_sched_count, dim3(nch), dim3(kReorderThreads), 0, c->stream, F.cost, F.n_tiles,
                            F.heavy_flag, c->d_saved_cost, c->d_hist, c->d_csum, nch);
         HIP_TRY(c, hipGetLastError());
-        hipLaunchKernelGGL(rtx_sched_scan, dim3(1), dim3(kScanThreads), 0, c->stream, c->d_hist, nch, c->d_csum,
+        hipLaunchKernelGGL(rtx_sched_scan, dim3(1), dim3(kScanThreads), 0, c->stream, c->d_hist, nch,
+                           F.band_tiles, c->d_order, c->d_csum,
                            F.n_tiles, slots, c->split_permille, c->d_thr, c->d_heavy_n);
         HIP_TRY(c, hipGetLastError());
         hipLaunchKernelGGL(rtx_sched_scatter, dim3(nch), dim3(kReorderThreads), 0, c->stream, F.cost, c->d_order,
