@@ -824,6 +824,12 @@ __device__ __forceinline__ uint32_t q8(float c) {
 #ifndef RTX_MIN_WAVES_PER_EU
 #define RTX_MIN_WAVES_PER_EU 1
 #endif
+// XCD bands (experiment build, tools/xcd_bands_ab.sh; RTX_XCD_BANDS=1 in the environment then
+// turns them on): band x of the image on XCD x.  Off in the product build: the band-aware tile
+// fetch alone costs 3-4 % (profiles/r03/ab_xcd_bands.txt) and the bands gain no time.
+#ifndef RTX_XCD_BANDS
+#define RTX_XCD_BANDS 0
+#endif
 // XCD-aware dispatch: runs of this many consecutive dispatch-order entries per XCD (0/1: off)
 #ifndef RTX_XCD_RUN
 #define RTX_XCD_RUN 0
@@ -897,6 +903,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         const uint32_t pos = ((k / kRun) * 8u + x) * kRun + (k % kRun);
         widx = pos * kWavesPerBlock + wave;
     }
+#if RTX_XCD_BANDS
     if (PHASE == 0 && F.band_tiles) {
         // XCD bands: workgroups go round robin to the 8 XCDs (blockIdx % 8), each with its own
         // 4 MB L2.  XCD x takes dispatch slots [x, x + 1) * band_tiles, which the schedule fills
@@ -907,14 +914,20 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         widx = k < bpb ? ((b & 7u) * bpb + k) * kWavesPerBlock + wave : 8u * F.band_tiles;
         widx = __builtin_amdgcn_readfirstlane(widx);   // wave-uniform: keep the scalar tile loads
     }
+#endif
     uint32_t tile, part = 0, light = 0;
     if (PHASE == 0) {
+#if RTX_XCD_BANDS
         // (XCD bands: slots up to 8 x band_tiles, free ones holding the no-tile marker ~0u)
         const uint32_t lim = F.band_tiles ? 8u * F.band_tiles : F.n_tiles;
         const uint32_t w = widx < lim ? widx : 0u;
         tile = F.order ? ldc(F.order, w) : w;
         tile = __builtin_amdgcn_readfirstlane(widx < lim ? tile : ~0u);   // wave-uniform
         if (tile >= F.n_tiles) return;
+#else
+        if (widx >= F.n_tiles) return;
+        tile = F.order ? ldc(F.order, widx) : widx;
+#endif
         if (F.heavy_flag && ldc(F.heavy_flag, tile)) return;   // rendered by the split launches
     } else {
         // grid (heavy tiles / waves per block, parts, lights), tile fastest: every heavy tile's part 0 is
@@ -2253,7 +2266,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     if (RTX_XCD_RUN > 1) nblocks = (nblocks + 8 * RTX_XCD_RUN - 1) / (8 * RTX_XCD_RUN) * (8 * RTX_XCD_RUN);
     F.band_tiles = 0;
     const uint32_t nch_all = (ntiles + kSchedChunk - 1) / kSchedChunk;
-    if (c->xcd_bands && RTX_XCD_RUN <= 1 && nch_all <= static_cast<uint32_t>(kScanThreads)) {
+    if (RTX_XCD_BANDS && c->xcd_bands && RTX_XCD_RUN <= 1 && nch_all <= static_cast<uint32_t>(kScanThreads)) {
         // XCD bands (the kernel, rtx_sched_scan): the same number of whole scheduling chunks
         // per XCD, band x's slots from x * band_tiles
         F.band_tiles = (nch_all + 7u) / 8u * kSchedChunk;

@@ -111,7 +111,10 @@ def test_headline_config_many_frames(fresh_ctx):
 def test_xcd_bands_full_resolution(monkeypatch, name, W, H, exact):
     """RTX_XCD_BANDS=1 (band x of the image on XCD x, the chunks dealt by measured cost,
     rtx_sched_scan): the padded grid and the no-tile slots change which wave renders a tile,
-    never a pixel — every frame is still the reference's."""
+    never a pixel — every frame is still the reference's.  The bands are compiled only into
+    the experiment build (-DRTX_XCD_BANDS=1, tools/xcd_bands_ab.sh sets RTX_TEST_XCD_BANDS)."""
+    if os.environ.get("RTX_TEST_XCD_BANDS") != "1":
+        pytest.skip("XCD bands are an experiment build (tools/xcd_bands_ab.sh)")
     from gp1_raytracer_2223_amd.renderer import DeviceContext
     monkeypatch.setenv("RTX_XCD_BANDS", "1")
     ctx = DeviceContext(int(os.environ.get("RTX_TEST_DEVICE", "0")))

@@ -1,12 +1,15 @@
 #!/bin/bash
-# XCD bands (RTX_XCD_BANDS=1: band x of the image on XCD x) against the default dispatch:
+# XCD bands (RTX_XCD_BANDS=1: band x of the image on XCD x) against the default dispatch, both
+# in the experiment build:
 # full-size parity of every config with bands on, kernel time A/B in alternating rounds, and
 # FETCH_SIZE of Synthetic100k both ways (run on the GPU box).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/xcd_bands
 mkdir -p $OUT
-RTX_XCD_BANDS=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -x -q --timeout 300 \
+# the experiment build (on the CPU beforehand): python tools/build_variant.py bands -DRTX_XCD_BANDS=1
+export RTX_HIP_LIB=gp1_raytracer_2223_amd/lib/exp/librtx_hip_bands.so
+RTX_TEST_XCD_BANDS=1 RTX_XCD_BANDS=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -x -q --timeout 300 \
   --timeout-method thread > $OUT/parity_bands.log 2>&1 || { tail -20 $OUT/parity_bands.log; exit 1; }
 tail -2 $OUT/parity_bands.log
 for r in 1 2; do
