@@ -24,12 +24,19 @@
 #include <string>
 #include <vector>
 
+#include <sys/resource.h>
+
 #include "rtx_renderer.hpp"
 
 namespace {
 
 using Clock = std::chrono::steady_clock;
 double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+double cpu_secs() {   // the process's CPU time, every thread (user + system)
+    rusage u{};
+    getrusage(RUSAGE_SELF, &u);
+    return double(u.ru_utime.tv_sec + u.ru_stime.tv_sec) + 1e-6 * double(u.ru_utime.tv_usec + u.ru_stime.tv_usec);
+}
 
 // Timer::StartBenchmark / Update FPS logic (Timer.cpp:44-131), same float arithmetic.
 struct Benchmark {
@@ -92,6 +99,7 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
     long frames = 0, queued = 0;
     int rc = 0, last = -1;
     const Clock::time_point start = Clock::now();
+    const double cpu0 = cpu_secs();
     Clock::time_point prev = start;
     rtx_scene s;
     rtx_camera cam;
@@ -202,10 +210,13 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
     out << "LOW = " << b.low << std::endl;
     out << "AVG = " << b.avg << std::endl;
     const double n = static_cast<double>(queued);
+    // host CPU use of the loop: process CPU time (the build pool's spinning workers included) over
+    // wall time, in cores
+    const double cores = (cpu_secs() - cpu0) / std::max(1e-9, secs(start, Clock::now()));
     std::printf("frames %ld%s%s, %d in flight: per frame update %.3f ms, upload %.3f ms, queue %.3f ms, "
-                "wait for GPU %.3f ms\n", frames, animated ? " (animated)" : "", device_update ? " device Update" : "",
-                inflight, t_update / n * 1e3,
-                t_upload / n * 1e3, t_queue / n * 1e3, t_wait / std::max(1.0, double(frames)) * 1e3);
+                "wait for GPU %.3f ms, host CPU %.2f cores\n", frames, animated ? " (animated)" : "",
+                device_update ? " device Update" : "", inflight, t_update / n * 1e3,
+                t_upload / n * 1e3, t_queue / n * 1e3, t_wait / std::max(1.0, double(frames)) * 1e3, cores);
     return 0;
 }
 
