@@ -299,7 +299,7 @@ constexpr uint32_t kLdsBytesSub = 50;    // + the element's triangle id
 constexpr uint32_t kSubLdsMax = 2816;    // subtrees up to this size build from LDS
 
 #ifndef RTX_ANIM_TEAM_ELEMS
-#define RTX_ANIM_TEAM_ELEMS 96u   // a team gets another wave only for this many elements per wave
+#define RTX_ANIM_TEAM_ELEMS 64u   // a team gets another wave only for this many elements per wave (96: +13 us of timeline, profiles/r03/anim_exp_team*)
 #endif
 #ifndef RTX_ANIM_SMALL
 #define RTX_ANIM_SMALL 1   // one-wave nodes of up to 128 elements by node_small (0: node_process for all)
