@@ -91,6 +91,7 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
         ctx.push_back(c);
     }
     std::vector<std::vector<uint32_t>> buf(inflight, std::vector<uint32_t>(npx));
+    std::vector<char> upd_ok(inflight, 1);   // --sequence: the device Update of the frame in buf[f] succeeded
     for (int f = 0; f < inflight; ++f) rtx_host_register(ctx[f], buf[f].data(), npx * 4);   // async D2H
     const rtx_render_params p = r.Params();
     Benchmark b(windows);
@@ -127,7 +128,7 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
     if (device_update && animated) {
         std::vector<int32_t> ids(64);
         const int ns = rtx_host_scene_spinning(hs, ids.data(), static_cast<uint32_t>(ids.size()));
-        if (ns > static_cast<int>(ids.size())) {   // rtx_anim_create takes at most 8 anyway
+        if (ns > static_cast<int>(ids.size())) {   // rtx_anim_create takes at most 32 anyway
             std::fprintf(stderr, "--device-update: %d turning meshes, more than %zu\n", ns, ids.size());
             for (size_t i = 1; i < ctx.size(); ++i) rtx_destroy(ctx[i]);
             return 1;
@@ -155,7 +156,7 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
             const float elapsed = static_cast<float>(secs(prev, w1));                  // Timer::Update
             prev = w1;
             if (seq) {
-                if (anim && !anim_ok()) { rc = 1; break; }   // never write a frame of a failed Update
+                if (anim && !upd_ok[f]) { rc = 1; break; }   // never write a frame of a failed Update
                 r.Pixels() = buf[f];
                 if (!r.SaveBufferToImage(stem + "_" + std::to_string(frames - 1) + ".bmp")) { rc = 1; break; }
                 if (frames == static_cast<long>(seq->size())) break;
@@ -179,6 +180,10 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
                 rc = 1;
                 break;
             }
+            // --sequence: this Update's own status, read now (the status words are the newest
+            // Update's, so with frames in flight a later one would overwrite a failure); the
+            // frame is written only if it is clean.  The benchmark loop checks once at the end.
+            if (seq) upd_ok[f] = anim_ok();
         } else if ((animated || queued < inflight) && !ok(rtx_upload_scene(ctx[f], &s), "rtx_upload_scene", ctx[f])) {
             break;
         }

@@ -96,7 +96,8 @@ struct MeshDev {
 };
 
 // status words: 0 error bits, 1 deepest level, 2 nodesUsed, 3 frontier parts, 4 subtrees,
-// 5 task-split ids (output launch), 6 tasks split, 7 -; 8.. phase stamps (s_memrealtime, 100 MHz, low 32 bits):
+// 5 task-split ids (output launch), 6 tasks split, 7 sticky kErrTimeout / kErrCapacity of an earlier
+// update (the mesh stays disabled); 8.. phase stamps (s_memrealtime, 100 MHz, low 32 bits):
 // 8 build start, 9 set-up done, 10 root split, 11 first subtree start, 12 last subtree end,
 // 13 output start, 14 numbering known (frontier workgroup), 15 frontier done; 16-19 the first
 // four task splits' sizes, 20-27 their start / end
@@ -126,11 +127,17 @@ struct Launch {
     uint32_t epoch;              // this update's number (> 0): tags the queue entries it publishes
     uint32_t cut;                // nodes above this many triangles are split as tasks, smaller ones are subtrees
     uint32_t frontier_max;       // meshes up to this many triangles select the frontier in parallel (else serially)
+    uint64_t wait_ticks;         // a worker's wait for a queue entry, s_memrealtime ticks (100 MHz): 200 ms; tests lower it
 };
 constexpr uint32_t kTopLdsTris = 3136;   // the largest top_lds (rtx_anim.hip's LDS budget)
 constexpr uint32_t kFrontierHistMax = 4096;   // the largest frontier_max (the count histogram's bins)
 
-enum : uint32_t { kErrNaN = 1u, kErrDepth = 2u, kErrTimeout = 4u };
+// kErrTimeout: a worker gave up waiting for a queue entry (Launch::wait_ticks); kErrCapacity: a
+// task-queue or subtree-table guard fired.  Both leave the tree incomplete: the output launch then
+// writes none of it and disables the mesh in the image (no frontier parts, node count 0), as for
+// kErrDepth.
+enum : uint32_t { kErrNaN = 1u, kErrDepth = 2u, kErrTimeout = 4u, kErrCapacity = 8u };
+constexpr uint64_t kWaitTicks = 20000000ull;   // Launch::wait_ticks' default: 200 ms at 100 MHz
 
 hipError_t launch_build(const Launch& L, hipStream_t stream);
 

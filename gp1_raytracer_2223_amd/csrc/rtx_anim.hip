@@ -1110,7 +1110,7 @@ __device__ __forceinline__ uint32_t build_levels(const MeshDev& M, const Store<L
 // (the writes of the whole workgroup before the barrier become visible with it).
 __device__ __forceinline__ void push_task(const Launch& L, const MeshDev& M, uint32_t what, uint32_t ids) {
     const uint32_t j = atomicAdd(&M.q[kQHead], 1u);
-    if (j >= kQCap) { atomicOr(&M.status[0], kErrTimeout); return; }   // (cannot happen: kQCap bounds the tasks)
+    if (j >= kQCap) { atomicOr(&M.status[0], kErrCapacity); return; }   // (cannot happen: kQCap bounds the tasks)
     uint32_t* e = M.q + kQEntries + 4u * j;
     e[0] = what;
     e[1] = ids;
@@ -1129,7 +1129,7 @@ __device__ __forceinline__ void reserve_ids(const MeshDev& M, uint32_t r) {
 // Node t (n triangles, depth d) becomes subtree f: its descendants get 2 n - 2 temp ids
 __device__ __forceinline__ void make_subtree(const Launch& L, const MeshDev& M, uint32_t t, uint32_t n, uint32_t d) {
     const uint32_t f = atomicAdd(&M.status[4], 1u);   // < kMaxSub: every subtree root is a distinct id < kMaxTop
-    if (f >= static_cast<uint32_t>(kMaxSub)) { atomicOr(&M.status[0], kErrTimeout); return; }   // (guard only)
+    if (f >= static_cast<uint32_t>(kMaxSub)) { atomicOr(&M.status[0], kErrCapacity); return; }   // (guard only)
     const uint32_t base = atomicAdd(&M.q[kQSubIds], n > 1u ? 2u * n - 2u : 0u);
     M.sub[f] = SubRec{t, base, 0u, d};
     M.tmp[t].sub = f;
@@ -1536,7 +1536,9 @@ __device__ __forceinline__ void run_task(const Launch& L, const MeshDev& M, uint
 // has a running producer (the producers of all meshes come first in dispatch order,
 // blockIdx.x fastest).  One launch with the waits in it instead of a kernel per level: a kernel
 // boundary cost ~100 us before the next workgroups ran (the idle XCDs' start-up, profiles/r03).
-constexpr uint64_t kWaitTicks = 20000000ull;   // 200 ms of s_memrealtime: a stuck build reports, never hangs
+// A waiting worker gives up after Launch::wait_ticks (kWaitTicks = 200 ms of s_memrealtime by
+// default, rtx_anim.h): a stuck build reports, never hangs.  (A worker that gives up leaves the entry it claimed unbuilt, so the tree is
+// incomplete: kErrTimeout, and the output launch disables the mesh, see rtx_anim_out)
 #ifndef RTX_ANIM_POLL_SLEEP
 #define RTX_ANIM_POLL_SLEEP 8   // s_sleep units (64 clocks) between a waiting worker's polls
 #endif
@@ -1549,6 +1551,14 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
     __shared__ uint32_t s_list[8];   // level lists of a split task (4) and its kept child (2)
     __shared__ uint32_t s_task[3];
     const uint32_t tid = threadIdx.x;
+    if (M.status[7]) {
+        // An earlier update left this mesh's tree incomplete (status word 7, sticky): its order of
+        // triangles is no longer the reference's (each build permutes the previous order,
+        // DataTypes.h:335-363), so no later update can be exact.  Build nothing; the output launch
+        // keeps the mesh disabled and every update reports the error (re-register to recover).
+        if (blockIdx.y == 0 && tid == 0) M.status[0] = M.status[7];
+        return;
+    }
     if (blockIdx.y == 0) {
         if (tid == 0) {
             M.status[kStTop0] = stamp();
@@ -1580,7 +1590,7 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
                 }
                 if (__hip_atomic_load(&M.q[kQDone], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= M.T) break;
                 __builtin_amdgcn_s_sleep(RTX_ANIM_POLL_SLEEP);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > L.wait_ticks) {
                     atomicOr(&M.status[0], kErrTimeout);
                     break;
                 }
@@ -1859,6 +1869,26 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
     const MeshDev& M = L.meshes[blockIdx.y];
     const uint32_t g = blockIdx.x, tid = threadIdx.x;
     const uint32_t T = M.T;
+    if (M.status[0] & (kErrTimeout | kErrCapacity)) {
+        // The build left the tree incomplete (an entry claimed by a worker that gave up, or a
+        // capacity guard): none of its numbering, records or frontier is written — their inputs
+        // may be stale — and the mesh is disabled in the image (the update's template copy leaves
+        // its node region empty): no frontier parts, node count 0, so the render kernel skips it.
+        if (g == kOutGroups) {
+            for (uint32_t k = tid; k < M.part_cap; k += kAnimThreads) L.img.parts[M.part0 + k] = make_int4(-1, 0, 0, 0);
+            if (tid == 0) {
+                L.img.meshes[M.mesh].y = 0;
+                M.status[7] |= M.status[0] & (kErrTimeout | kErrCapacity);   // sticky: see rtx_anim_build
+                M.status[1] = 0u;
+                M.status[2] = 0u;
+                M.status[3] = 0u;
+                M.q[kQHead] = 0u;
+                M.q[kQTail] = 0u;
+                M.q[kQDone] = 0u;
+            }
+        }
+        return;
+    }
     const uint32_t nsub = M.status[4], ntop = min(M.q[kQTop], static_cast<uint32_t>(kMaxTop));
     __shared__ int32_t s_l[kMaxTop];
     __shared__ uint32_t s_split[kMaxTop], s_rank[kMaxTop], s_count[kMaxTop];

@@ -29,6 +29,7 @@
 
 #include "rtx.h"
 #include "rtx_anim.h"
+#include "rtx_cull.h"
 #include "rtx_fastdiv.h"
 #include "rtx_kernels.h"
 
@@ -95,6 +96,7 @@ __device__ __forceinline__ int4 ldc(const int4* base, uint32_t i) {
 __device__ __forceinline__ uint32_t ldc(const uint32_t* base, uint32_t i) {
     return ((const RTX_CONST uint32_t*)base)[i];
 }
+__device__ __forceinline__ float ldc(const float* base, uint32_t i) { return ((const RTX_CONST float*)base)[i]; }
 typedef float cf8 __attribute__((ext_vector_type(8)));
 // A wave-uniform value the optimiser cannot see through: a loop counter passed through it
 // stays a 32-bit SGPR offset instead of being widened into a 64-bit pointer induction
@@ -363,6 +365,40 @@ __device__ __forceinline__ unsigned long long slab_mask(const float4 a, const fl
     return ballot(tMax > 0) & ballot(tMax >= tMin);
 }
 
+// Exact cull (rtx_cull.h): a node the reference's slab test passes is skipped for
+// a lane whose LINE misses the node's tight box widened by the margin rtx_cull.h proves for the
+// ray's anchor (view camera / light) — no triangle below can then pass HitTest_Triangle for that
+// ray, so the visit would change nothing.  Record per node slot (same byte offset as the node):
+// {c.x, c.y, c.z, E.x}, {E.y, E.z, -, -}, box = c +- E (E includes the margin and the padding
+// 16u (E + |c|) that covers this test's own rounding).  `k` = 16u |o| |inv| per axis covers the
+// rounding of (c - o) * inv, or +inf for a lane outside the bound's domain (it then always
+// passes).  Lanes of a FAST batch only (finite non-zero inverse directions, |inv| <= 2^64).
+// NaN-safe: max/min ignore a NaN operand, so a NaN term drops its axis (never culls wrongly).
+struct CullRay {
+    const float4* base;   // the anchor's records (null: no cull)
+    float kx, ky, kz;
+};
+__device__ __forceinline__ unsigned long long cull_mask(const float4 a, const float4 b, const Ray& r, const CullRay& q) {
+    const float tx = (a.x - r.ox) * r.ix, ty = (a.y - r.oy) * r.iy, tz = (a.z - r.oz) * r.iz;
+    const float hx = fmaf(a.w, fabsf(r.ix), q.kx), hy = fmaf(b.x, fabsf(r.iy), q.ky), hz = fmaf(b.y, fabsf(r.iz), q.kz);
+    const float n = fmaxf(fmaxf(tx - hx, ty - hy), tz - hz);
+    const float f = fminf(fminf(tx + hx, ty + hy), tz + hz);
+    return ballot(!(n > f));
+}
+// 16u |o_k| |inv_k| per axis, or +inf (always pass) for a lane outside the bound's domain:
+// |o_k| <= 2^40, |inv_k| <= 2^64 and `ok` (the caller's conditions on the direction and tmax)
+__device__ __forceinline__ CullRay cull_ray(const float4* base, const Ray& r, bool ok) {
+    CullRay q;
+    q.base = base;
+    ok = ok && fabsf(r.ox) <= 0x1p40f && fabsf(r.oy) <= 0x1p40f && fabsf(r.oz) <= 0x1p40f &&
+         fabsf(r.ix) <= 0x1p64f && fabsf(r.iy) <= 0x1p64f && fabsf(r.iz) <= 0x1p64f;
+    constexpr float k16u = 0x1p-20f;
+    q.kx = ok ? (k16u * fabsf(r.ox)) * fabsf(r.ix) : INFINITY;
+    q.ky = ok ? (k16u * fabsf(r.oy)) * fabsf(r.iy) : INFINITY;
+    q.kz = ok ? (k16u * fabsf(r.oz)) * fabsf(r.iz) : INFINITY;
+    return q;
+}
+
 // Octant of a FAST ray batch (every live inverse direction finite and non-zero): bit k set
 // when axis k's inverse direction is negative for every lane in `mask` (non-empty), -1
 // when the lanes disagree on some axis.  One code per lane from the sign bits, compared
@@ -550,11 +586,12 @@ __device__ __forceinline__ void touch_wait(uint32_t a, uint32_t b) {
 // VGPR boolean or a lane-mask flow variable), a dead end leaves it as an empty "leaf", and
 // the pop loop is the only other path.  Same visits, tests and order as bvh_walk.
 // `nb` is the node copy the slab form reads (the octant's (near, far) copy for kSlabOct).
-template <bool ANY, int SLAB, bool CB = false>
+// CULL: a child is entered only by the lanes whose line also meets its cull box (cull_mask).
+template <bool ANY, int SLAB, bool CB = false, bool CULL = false>
 __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, const Ray& r, uint32_t link,
                               uint32_t ntri, unsigned long long m, unsigned long long mask, uint32_t lane, uint4* stk,
                               float& sc_t, uint32_t& sc_tri, unsigned long long& live, const uint32_t* occ_word,
-                              uint32_t occ_bit) {
+                              uint32_t occ_bit, const CullRay& cq = CullRay{}) {
     constexpr bool FAST = SLAB != kSlabExact;
     uint32_t sp = 0;
     [[maybe_unused]] uint32_t pf0 = 0, pf1 = 0;
@@ -570,8 +607,18 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                 pf1 = touch_ld(nr ? static_cast<const void*>(S.tris) : nb, __float_as_uint(P.r1.z));
             }
 #endif
-            const unsigned long long ml = slab_mask<SLAB>(P.l0, P.l1, r) & m;
-            const unsigned long long mr = slab_mask<SLAB>(P.r0, P.r1, r) & m;
+            unsigned long long ml = slab_mask<SLAB>(P.l0, P.l1, r) & m;
+            unsigned long long mr = slab_mask<SLAB>(P.r0, P.r1, r) & m;
+            if (CULL) {
+                NodePair Q;
+                ldcb64(cq.base, link, Q.l0, Q.l1, Q.r0, Q.r1);
+                // only pairs whose records are flagged worth testing (cull_write), and only when
+                // some lane entered a child
+                if ((__float_as_uint(Q.l1.w) | __float_as_uint(Q.r1.w)) && (ml | mr)) {
+                    ml &= cull_mask(Q.l0, Q.l1, r, cq);
+                    mr &= cull_mask(Q.r0, Q.r1, r, cq);
+                }
+            }
 #if RTX_ASM_SELECT
             // next (link, ntri): left, else right, else a dead end taken as an empty leaf
             // (ntri = 1 with m = 0); `both` = mr if the left child is taken too (the right
@@ -653,10 +700,13 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
 }
 
 // SLAB = kSlabOct: `oct` is the batch's octant (batch_octant), else ignored.
-template <bool ANY, int SLAB, bool COUNT, bool CB = false>
+// CULL (SLAB != kSlabExact, !COUNT): the exact cull of the anchor `cq` (cull_mask) beside every
+// slab test, the root's included.
+template <bool ANY, int SLAB, bool COUNT, bool CB = false, bool CULL = false>
 __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int oct, unsigned long long mask,
                               uint32_t lane, uint4* stk, unsigned long long* sT, float& sc_t, uint32_t& sc_tri,
-                              unsigned long long& live, Counts& cnt) {
+                              unsigned long long& live, Counts& cnt, const CullRay& cq = CullRay{}) {
+    static_assert(!CULL || (SLAB != kSlabExact && !COUNT), "the cull runs in FAST batches of the lean walk only");
     constexpr bool FAST = SLAB != kSlabExact;
     if (M.y == 0) return;
     const bool OCT = SLAB == kSlabOct && !COUNT && !RTX_STAMPS_WALK;
@@ -667,13 +717,18 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
     float4 b0, b1;
     ldcb32(nb, static_cast<uint32_t>(M.x), b0, b1);   // M.x: the root's byte offset
     if (COUNT && ((mask >> lane) & 1ull)) cnt.c[kSlab]++;
-    const unsigned long long m =
+    unsigned long long m =
         (OCT ? slab_mask<kSlabOct>(b0, b1, r) : slab_mask<FAST ? kSlabFast : kSlabExact>(b0, b1, r)) & mask;
+    if (CULL && m) {
+        float4 c0, c1;
+        ldcb32(cq.base, static_cast<uint32_t>(M.x), c0, c1);
+        if (__float_as_uint(c1.w)) m &= cull_mask(c0, c1, r, cq);
+    }
     if (m == 0) return;
     if (RTX_LEAN_WALK && !COUNT && !RTX_STAMPS_WALK)
-        bvh_walk_lean<ANY, OCT ? kSlabOct : (FAST ? kSlabFast : kSlabExact), CB>(
+        bvh_walk_lean<ANY, OCT ? kSlabOct : (FAST ? kSlabFast : kSlabExact), CB, CULL>(
             S, nb, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask, lane, stk, sc_t,
-            sc_tri, live, nullptr, 0u);
+            sc_tri, live, nullptr, 0u, cq);
     else
         bvh_walk<ANY, FAST, COUNT>(S, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask,
                                    lane, stk, sT, sc_t, sc_tri, live, cnt);
@@ -687,10 +742,13 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
 // the reference's first-found, strict-< winner — and occlusion is the OR of the parts.
 // SLAB = kSlabOct: `oct` is the batch's octant (batch_octant) and the part walks that copy.
 // CB: kSpecCullBack (tri_t_wave).
-template <bool ANY, int SLAB, bool CB = false>
+// CULL: as mesh_traverse, on the part's path and below it.
+template <bool ANY, int SLAB, bool CB = false, bool CULL = false>
 __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int oct, unsigned long long mask,
                               uint32_t lane, uint4* stk, float& sc_t, uint32_t& sc_tri, unsigned long long& live,
-                              Counts& cnt, const uint32_t* occ_word = nullptr, uint32_t occ_bit = 0) {
+                              Counts& cnt, const uint32_t* occ_word = nullptr, uint32_t occ_bit = 0,
+                              const CullRay& cq = CullRay{}) {
+    static_assert(!CULL || SLAB != kSlabExact, "the cull runs in FAST batches only");
     constexpr bool FAST = SLAB != kSlabExact;
     if (E.x < 0) return;   // unused entry of a device-animated mesh's reserved frontier
     const int4 M = ldcb16i(S.meshes, static_cast<uint32_t>(E.x) * 16u);
@@ -700,6 +758,11 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int
     float4 b0, b1;
     ldcb32(nb, static_cast<uint32_t>(M.x), b0, b1);   // M.x: the root's byte offset
     unsigned long long m = slab_mask<SLAB>(b0, b1, r) & mask;
+    if (CULL && m) {
+        float4 q0, q1;
+        ldcb32(cq.base, static_cast<uint32_t>(M.x), q0, q1);
+        if (__float_as_uint(q1.w)) m &= cull_mask(q0, q1, r, cq);
+    }
     uint32_t link = __float_as_uint(b1.z), ntri = __float_as_uint(b1.w);
     const uint32_t path = static_cast<uint32_t>(E.z);
     for (int d = 0; d < E.w && m; ++d) {
@@ -708,13 +771,18 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int
         const bool right = (path >> d) & 1u;
         const float4 c0 = right ? P.r0 : P.l0, c1 = right ? P.r1 : P.l1;
         m &= slab_mask<SLAB>(c0, c1, r);
+        if (CULL) {
+            float4 q0, q1;
+            ldcb32(cq.base, link + (right ? 32u : 0u), q0, q1);
+            if (__float_as_uint(q1.w)) m &= cull_mask(q0, q1, r, cq);
+        }
         link = __float_as_uint(c1.z);
         ntri = __float_as_uint(c1.w);
     }
     if (m == 0) return;
     if (RTX_LEAN_WALK && !RTX_STAMPS_WALK)
-        bvh_walk_lean<ANY, SLAB, CB>(S, nb, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, sc_t, sc_tri,
-                                     live, occ_word, occ_bit);
+        bvh_walk_lean<ANY, SLAB, CB, CULL>(S, nb, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, sc_t,
+                                           sc_tri, live, occ_word, occ_bit, cq);
     else
         bvh_walk<ANY, FAST, false>(S, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, nullptr, sc_t, sc_tri,
                                    live, cnt, occ_word, occ_bit);
@@ -853,7 +921,9 @@ __device__ __forceinline__ uint32_t q8(float c) {
 #ifndef RTX_SPEC_WAVES_PARTIAL
 #define RTX_SPEC_WAVES_PARTIAL 7
 #endif
-template <bool COUNT, int PHASE, bool DEEP = false, int SPEC = 0, bool HSTK = false>
+// CULLK: the variant with the exact cull (DevScene::cull; launched only for scenes that have the
+// records — the code of the cull paths costs the kernel without them registers and 8 %).
+template <bool COUNT, int PHASE, bool DEEP = false, int SPEC = 0, bool HSTK = false, bool CULLK = false>
 __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                                                   : ((SPEC & (kSpecOneMesh | kSpecNoMesh))
                                                          ? RTX_SPEC_WAVES
@@ -985,6 +1055,13 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
     const bool fast = (active & vslow) == 0 && S.tri_fast;
     // octant of the wave's primary rays (-1: mixed signs, or no octant copies)
     const int poct = (RTX_OCTANT && fast && S.oct_bytes && PHASE == 0) ? batch_octant(vr, active) : -1;
+    // exact cull of the view's camera anchor (FAST waves; a direction normalised from a magnitude
+    // of at least 2^-30 has |d| = 1 +- 3u, which the bound assumes)
+    constexpr bool kCull = CULLK && !COUNT && !RTX_STAMPS_WALK;
+    const bool pcull = kCull && S.cull_stride && fast && (PHASE == 0 || PHASE == 1);
+    CullRay pq{};
+    if (pcull)
+        pq = cull_ray(S.cull + static_cast<size_t>(uni(view)) * (S.cull_stride / 16u), vr, dm >= 0x1p-30f);
 
     // ---- Scene::GetClosestHit (Scene.cpp:29-66)
     float best_t = FLT_MAX, sc_t = FLT_MAX;
@@ -1054,9 +1131,15 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
             const int4 M = ldcb16i(S.meshes, opaque(mi * 16u));
             uint32_t sc_tri = 0;
             unsigned long long unused = 0;
-            if (poct >= 0)
+            if (poct >= 0 && pcull)
+                mesh_traverse<false, kSlabOct, COUNT, kCullBack, kCull>(S, M, vr, poct, active, lane, stk, sT, sc_t,
+                                                                        sc_tri, unused, cnt, pq);
+            else if (poct >= 0)
                 mesh_traverse<false, kSlabOct, COUNT, kCullBack>(S, M, vr, poct, active, lane, stk, sT, sc_t, sc_tri,
                                                                  unused, cnt);
+            else if (fast && pcull)
+                mesh_traverse<false, kSlabFast, COUNT, kCullBack, kCull>(S, M, vr, 0, active, lane, stk, sT, sc_t,
+                                                                         sc_tri, unused, cnt, pq);
             else if (fast)
                 mesh_traverse<false, kSlabFast, COUNT, kCullBack>(S, M, vr, 0, active, lane, stk, sT, sc_t, sc_tri,
                                                                   unused, cnt);
@@ -1072,8 +1155,14 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         uint32_t sc_tri = 0;
         unsigned long long unused = 0;
         const int oct = (RTX_OCTANT && fast && S.oct_bytes) ? batch_octant(vr, active) : -1;
-        if (oct >= 0)
+        if (oct >= 0 && pcull)
+            part_traverse<false, kSlabOct, kCullBack, kCull>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri, unused,
+                                                             cnt, nullptr, 0u, pq);
+        else if (oct >= 0)
             part_traverse<false, kSlabOct, kCullBack>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri, unused, cnt);
+        else if (fast && pcull)
+            part_traverse<false, kSlabFast, kCullBack, kCull>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused,
+                                                              cnt, nullptr, 0u, pq);
         else if (fast)
             part_traverse<false, kSlabFast, kCullBack>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused, cnt);
         else
@@ -1145,6 +1234,13 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                 const bool sfast = (hitmask & sslow) == 0 && S.tri_fast;
                 const int soct =
                     (RTX_OCTANT && sfast && S.oct_bytes && PHASE == 0 && n_mesh) ? batch_octant(sr, hitmask) : -1;
+                // exact cull of the light's anchor: lanes with mag <= cull_T[li] (and a direction
+                // normalised from at least 2^-30)
+                const bool scull = kCull && S.cull_stride && sfast && (PHASE == 0 || PHASE == 2) && n_mesh;
+                CullRay sq{};
+                if (scull)
+                    sq = cull_ray(S.cull + static_cast<size_t>(kMaxViews + li) * (S.cull_stride / 16u), sr,
+                                  mag >= 0x1p-30f && mag <= ldc(S.cull_T, li));
                 if (COUNT && did) cnt.c[kShadow]++;
                 // (single-condition loops with a separate exit test: a `&& live` loop
                 // condition is carried as a VGPR boolean by the compiler)
@@ -1207,9 +1303,15 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                     float st = 0.f;
                     uint32_t stri = 0;
                     const int4 M = ldcb16i(S.meshes, opaque(mi * 16u));
-                    if (soct >= 0)
+                    if (soct >= 0 && scull)
+                        mesh_traverse<true, kSlabOct, COUNT, kCullBack, kCull>(S, M, sr, soct, live, lane, stk, sT, st,
+                                                                               stri, live, cnt, sq);
+                    else if (soct >= 0)
                         mesh_traverse<true, kSlabOct, COUNT, kCullBack>(S, M, sr, soct, live, lane, stk, sT, st, stri,
                                                                         live, cnt);
+                    else if (sfast && scull)
+                        mesh_traverse<true, kSlabFast, COUNT, kCullBack, kCull>(S, M, sr, 0, live, lane, stk, sT, st,
+                                                                                stri, live, cnt, sq);
                     else if (sfast)
                         mesh_traverse<true, kSlabFast, COUNT, kCullBack>(S, M, sr, 0, live, lane, stk, sT, st, stri,
                                                                          live, cnt);
@@ -1222,9 +1324,15 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                     float st = 0.f;
                     uint32_t stri = 0;
                     const int poct2 = (RTX_OCTANT && sfast && S.oct_bytes) ? batch_octant(sr, hitmask) : -1;
-                    if (poct2 >= 0)
+                    if (poct2 >= 0 && scull)
+                        part_traverse<true, kSlabOct, kCullBack, kCull>(S, E, sr, poct2, live, lane, stk, st, stri, live,
+                                                                        cnt, &F.occ_bits[slot], 1u << li, sq);
+                    else if (poct2 >= 0)
                         part_traverse<true, kSlabOct, kCullBack>(S, E, sr, poct2, live, lane, stk, st, stri, live, cnt,
                                                                  &F.occ_bits[slot], 1u << li);
+                    else if (sfast && scull)
+                        part_traverse<true, kSlabFast, kCullBack, kCull>(S, E, sr, 0, live, lane, stk, st, stri, live,
+                                                                         cnt, &F.occ_bits[slot], 1u << li, sq);
                     else if (sfast)
                         part_traverse<true, kSlabFast, kCullBack>(S, E, sr, 0, live, lane, stk, st, stri, live, cnt,
                                                                   &F.occ_bits[slot], 1u << li);
@@ -1340,6 +1448,22 @@ template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[1]>(co
 template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[2]>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[3]>(const DevScene, const FrameArgs);
 template __global__ void rtx_render_kernel<false, 0, false, kSpecVariants[4]>(const DevScene, const FrameArgs);
+// the exact-cull variants (CULLK): the generic kernel and the mesh variants, all phases
+#define RTX_CULL_VARIANTS(P)                                                                                    \
+    template __global__ void rtx_render_kernel<false, P, false, 0, false, true>(const DevScene, const FrameArgs); \
+    template __global__ void rtx_render_kernel<false, P, false, kSpecVariants[0], false, true>(const DevScene,   \
+                                                                                               const FrameArgs); \
+    template __global__ void rtx_render_kernel<false, P, false, kSpecVariants[1], false, true>(const DevScene,   \
+                                                                                               const FrameArgs); \
+    template __global__ void rtx_render_kernel<false, P, false, kSpecVariants[3], false, true>(const DevScene,   \
+                                                                                               const FrameArgs); \
+    template __global__ void rtx_render_kernel<false, P, false, kSpecVariants[4], false, true>(const DevScene,   \
+                                                                                               const FrameArgs);
+RTX_CULL_VARIANTS(0)
+RTX_CULL_VARIANTS(1)
+RTX_CULL_VARIANTS(2)
+RTX_CULL_VARIANTS(3)
+#undef RTX_CULL_VARIANTS
 
 // Octant copies 1..7 of an uploaded node array from copy 0 (blockIdx.y + 1 = octant k):
 // copy k stores (hi, lo) on the axes set in k, the same swap the host applies for small
@@ -1354,6 +1478,168 @@ __global__ void __launch_bounds__(256) rtx_octant_expand(float4* __restrict__ no
     float4* dst = nodes + static_cast<size_t>(k) * stride;
     dst[2u * i] = make_float4(mx ? a.y : a.x, mx ? a.x : a.y, my ? a.w : a.z, my ? a.z : a.w);
     dst[2u * i + 1u] = make_float4(mz ? b.y : b.x, mz ? b.x : b.y, b.z, b.w);
+}
+
+// ---------------------------------------------------------------- exact cull records
+// (rtx_cull.h; DevScene::cull).  Three launches derive them from the uploaded
+// triangle records, all on the context stream before the frames that read them:
+//   rtx_cull_tri_box     per triangle: the box of (v0, v0 + E1, v0 + E2), rounded outward
+//   rtx_cull_tri_margin  per (anchor, triangle): rtx_cull.h's margin, rounded up
+//   rtx_cull_nodes_*     per node slot: the box over its subtree's triangle range (contiguous in
+//                        leaf order; a superset range is merely looser) widened by the range's
+//                        largest margin and the kernel test's own padding -> the record
+// Light anchors at upload; a view's camera anchor when a frame's view origin is not the one its
+// records were made for.  A NaN, infinite or huge (> 2^40) coordinate anywhere gives +inf (the
+// record then always passes: the bound's finite-arithmetic domain, rtx_cull.h).
+struct CullAnchors {
+    float p[kMaxViews + kMaxCullLights][4];   // xyz: the anchor point; w = 0: camera origin, > 0: light with tmax <= w
+    uint32_t idx[kMaxViews + kMaxCullLights]; // record copy the anchor writes
+    uint32_t n;
+};
+
+__device__ __forceinline__ float f_rd(double x) {   // largest float <= x (NaN stays NaN)
+    float f = static_cast<float>(x);
+    if (static_cast<double>(f) > x) f = nextafterf(f, -INFINITY);
+    return f;
+}
+__device__ __forceinline__ float f_ru(double x) {   // smallest float >= x
+    float f = static_cast<float>(x);
+    if (static_cast<double>(f) < x) f = nextafterf(f, INFINITY);
+    return f;
+}
+__device__ __forceinline__ bool cull_domain(float x) { return fabsf(x) <= 0x1p40f; }   // false for NaN / inf
+
+__global__ void __launch_bounds__(256) rtx_cull_tri_box(const Tri* __restrict__ tris, uint32_t n, float4* __restrict__ box) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const float4 a = tris[i].a, b = tris[i].b, c = tris[i].c;
+    const float v0[3] = {a.x, a.y, a.z}, e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
+    float lo[3], hi[3];
+    bool ok = true;
+    for (int k = 0; k < 3; ++k) {
+        ok = ok && cull_domain(v0[k]) && cull_domain(e1[k]) && cull_domain(e2[k]);
+        const double p = v0[k], q = p + static_cast<double>(e1[k]), r = p + static_cast<double>(e2[k]);
+        const double mn = fmin(p, fmin(q, r)), mx = fmax(p, fmax(q, r));
+        // the double sums are exact unless the exponents differ by > 29: widen by 2^-40 anyway
+        lo[k] = f_rd(mn - fabs(mn) * 0x1p-40);
+        hi[k] = f_ru(mx + fabs(mx) * 0x1p-40);
+    }
+    const float bad = ok ? 0.f : 1.f;   // out of the domain: the node records pass every ray
+    box[2u * i] = make_float4(lo[0], lo[1], lo[2], bad);
+    box[2u * i + 1u] = make_float4(hi[0], hi[1], hi[2], 0.f);
+}
+
+__global__ void __launch_bounds__(256) rtx_cull_tri_margin(const Tri* __restrict__ tris, uint32_t n, const CullAnchors A,
+                                                         float* __restrict__ marg) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x, j = blockIdx.y;
+    if (i >= n || j >= A.n) return;
+    const float4 a = tris[i].a, b = tris[i].b, c = tris[i].c;
+    const float v0[3] = {a.x, a.y, a.z}, e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
+    rtx_cull_tri T;
+    rtx_cull_tri_setup(&T, v0, e1, e2);
+    const float* p = A.p[j];
+    const double m = p[3] > 0.f ? rtx_cull_margin_light(&T, p, p[3]) : rtx_cull_margin_point(&T, p);
+    marg[static_cast<size_t>(j) * n + i] = (m >= 0.0 && m < 0x1p100) ? f_ru(m) : INFINITY;   // NaN -> inf
+}
+
+// Which records the walk tests (CullParams): a box some axis of which the reference's box (node
+// copy 0) exceeds `ratio` times — the reference's FLT_MIN-inflated boxes, DataTypes.h:315 — and,
+// with `leaves`, only leaf nodes.  Unflagged records are loaded but cost no vector work.
+struct CullParams {
+    const float4* nodes;   // node copy 0 (reference boxes, {min.x, max.x, min.y, max.y}, {min.z, max.z, link, ntri})
+    float ratio;
+    uint32_t leaves;
+};
+// the record of `slot` for anchor copy `a`: tight box [lo, hi] widened by `m` and the padding
+// 16u (E + |c|) of cull_mask's rounding (2^-20 = 16u); w of its second half = the test flag
+__device__ __forceinline__ void cull_write(float4* __restrict__ cull, uint32_t stride4, uint32_t a, uint32_t slot,
+                                           const float* lo, const float* hi, bool bad, float m, const CullParams& P) {
+    float cf[3], Ef[3];
+    for (int k = 0; k < 3; ++k) {
+        const double c = 0.5 * (static_cast<double>(lo[k]) + hi[k]);
+        cf[k] = static_cast<float>(c);
+        double E = 0.5 * (static_cast<double>(hi[k]) - lo[k]) + fabs(c - cf[k]) + static_cast<double>(m);
+        E = (E + 0x1p-20 * (E + fabs(static_cast<double>(cf[k])))) * (1.0 + 0x1p-40) +
+            0x1p-50 * (fabs(static_cast<double>(lo[k])) + fabs(static_cast<double>(hi[k])));
+        Ef[k] = (!bad && E < 0x1p100) ? f_ru(E) : INFINITY;   // NaN and empty boxes pass every ray
+        if (bad || !(E < 0x1p100)) cf[k] = 0.f;
+    }
+    const float4 n0 = P.nodes[2u * slot], n1 = P.nodes[2u * slot + 1u];
+    const float ref[3] = {n0.y - n0.x, n0.w - n0.z, n1.y - n1.x};
+    bool worth = false;
+    for (int k = 0; k < 3; ++k) worth = worth || ref[k] > P.ratio * 2.f * Ef[k];   // false for inf / NaN
+    if (P.leaves && __float_as_uint(n1.w) == 0u) worth = false;
+    float4* r = cull + static_cast<size_t>(a) * stride4 + 2u * slot;
+    r[0] = make_float4(cf[0], cf[1], cf[2], Ef[0]);
+    r[1] = make_float4(Ef[1], Ef[2], 0.f, __uint_as_float(worth ? 1u : 0u));
+}
+
+// node slots whose triangle range holds at most kCullBigTris triangles, one thread each
+__global__ void __launch_bounds__(256) rtx_cull_nodes_small(const uint2* __restrict__ rng, uint32_t nslots,
+                                                           const float4* __restrict__ box, const float* __restrict__ marg,
+                                                           uint32_t ntris, const CullAnchors A, float4* __restrict__ cull,
+                                                           uint32_t stride4, const CullParams P) {
+    const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+    if (s >= nslots) return;
+    const uint2 r = rng[s];
+    if (r.y - r.x > kCullBigTris) return;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    bool bad = r.y <= r.x || r.y > ntris;   // empty range (padding slot): pass
+    for (uint32_t t = r.x; !bad && t < r.y; ++t) {
+        const float4 l = box[2u * t], h = box[2u * t + 1u];
+        bad = bad || l.w != 0.f;
+        lo[0] = fminf(lo[0], l.x); lo[1] = fminf(lo[1], l.y); lo[2] = fminf(lo[2], l.z);
+        hi[0] = fmaxf(hi[0], h.x); hi[1] = fmaxf(hi[1], h.y); hi[2] = fmaxf(hi[2], h.z);
+    }
+    for (uint32_t j = 0; j < A.n; ++j) {
+        float m = 0.f;
+        for (uint32_t t = r.x; !bad && t < r.y; ++t) {
+            const float x = marg[static_cast<size_t>(j) * ntris + t];
+            m = (x > m || x != x) ? x : m;   // NaN sticks (then +inf below)
+        }
+        cull_write(cull, stride4, A.idx[j], s, lo, hi, bad, m, P);
+    }
+}
+
+__device__ __forceinline__ float wave_min(float x) {
+    for (int o = 32; o > 0; o >>= 1) x = fminf(x, __shfl_xor(x, o, 64));
+    return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+    for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
+    return x;
+}
+
+// the listed node slots (ranges above kCullBigTris), one wave each
+__global__ void __launch_bounds__(64) rtx_cull_nodes_big(const uint32_t* __restrict__ big, const uint2* __restrict__ rng,
+                                                        const float4* __restrict__ box, const float* __restrict__ marg,
+                                                        uint32_t ntris, const CullAnchors A, float4* __restrict__ cull,
+                                                        uint32_t stride4, const CullParams P) {
+    const uint32_t s = big[blockIdx.x], lane = threadIdx.x;
+    const uint2 r = rng[s];
+    const bool empty = r.y <= r.x || r.y > ntris;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    uint32_t badl = empty ? 1u : 0u;
+    for (uint32_t t = r.x + lane; !empty && t < r.y; t += 64u) {
+        const float4 l = box[2u * t], h = box[2u * t + 1u];
+        badl |= l.w != 0.f ? 1u : 0u;
+        lo[0] = fminf(lo[0], l.x); lo[1] = fminf(lo[1], l.y); lo[2] = fminf(lo[2], l.z);
+        hi[0] = fmaxf(hi[0], h.x); hi[1] = fmaxf(hi[1], h.y); hi[2] = fmaxf(hi[2], h.z);
+    }
+    const bool bad = __builtin_amdgcn_ballot_w64(badl != 0u) != 0ull;
+    for (int k = 0; k < 3; ++k) { lo[k] = wave_min(lo[k]); hi[k] = wave_max(hi[k]); }
+    for (uint32_t j = 0; j < A.n; ++j) {
+        float m = 0.f;
+        uint32_t nanl = 0u;
+        for (uint32_t t = r.x + lane; !empty && t < r.y; t += 64u) {
+            const float x = marg[static_cast<size_t>(j) * ntris + t];
+            nanl |= x != x ? 1u : 0u;
+            m = fmaxf(m, x);
+        }
+        m = wave_max(m);
+        if (__builtin_amdgcn_ballot_w64(nanl != 0u)) m = INFINITY;
+        if (lane == 0) cull_write(cull, stride4, A.idx[j], s, lo, hi, bad, m, P);
+    }
 }
 
 // Next frames' dispatch order from this frame's per-tile cost: heaviest first, STABLE
@@ -1592,6 +1878,8 @@ struct rtx_ctx {
         size_t cap = 0;
         hipEvent_t done = nullptr;   // recorded after the last frame that reads this image
         bool pending = false;
+        float4* cull = nullptr;      // the image's cull records (DevScene::cull), device only
+        size_t cull_cap = 0;
     };
     SceneBuf sb[2];
     int sb_cur = -1;
@@ -1648,6 +1936,22 @@ struct rtx_ctx {
     bool no_spec = false;            // RTX_NO_SPEC=1: always the generic kernel (tests)
     unsigned long long* d_hit_key = nullptr;
     uint32_t* d_occ = nullptr;
+    // exact cull (DevScene::cull): on for host uploads (RTX_NO_CULL=1: off); the
+    // scratch of its record launches (per-triangle boxes and margins) and the node-slot ranges
+    // and big-node list in the current image
+    bool no_cull = false;
+    float cull_ratio = 1.5f;              // CullParams (RTX_CULL_RATIO, RTX_CULL_LEAVES: tuning)
+    double cull_min_sa = 1.5;             // upload_scene's worth test (RTX_CULL_MIN_SA)
+    bool cull_leaves = false;
+    float4* d_cull_box = nullptr;
+    float* d_cull_marg = nullptr;
+    size_t cull_box_cap = 0, cull_marg_cap = 0;
+    const uint2* cull_rng = nullptr;
+    const uint32_t* cull_big = nullptr;
+    uint32_t cull_nslots = 0, cull_nbig = 0, cull_ntris = 0;
+    float cull_view[kMaxViews][3] = {};   // camera origin each view's records of the current image were made for
+    uint32_t cull_view_valid = 0;         // bit v: view v's records are current
+    uint64_t cull_updates = 0;            // camera-anchor record launches so far (rtx_cull_info)
     rtx_render_params last{};
     int last_views = 1;
     bool last_valid = false, last_rgb = false;
@@ -1774,6 +2078,16 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     // RTX_SPLIT=0 renders heavy tiles in one piece; RTX_SPLIT=force splits every tile
     if (const char* e = std::getenv("RTX_XCD_BANDS")) c->xcd_bands = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_NO_SPEC")) c->no_spec = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RTX_NO_CULL")) c->no_cull = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RTX_CULL_RATIO")) {
+        const double v = std::atof(e);
+        if (v >= 0.0 && v < 1e30) c->cull_ratio = static_cast<float>(v);
+    }
+    if (const char* e = std::getenv("RTX_CULL_LEAVES")) c->cull_leaves = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RTX_CULL_MIN_SA")) {
+        const double v = std::atof(e);
+        if (v >= 0.0 && v < 1e30) c->cull_min_sa = v;
+    }
     if (const char* e = std::getenv("RTX_SPLIT")) c->split_mode = std::strcmp(e, "0") == 0 ? 0u : (std::strcmp(e, "force") == 0 ? 2u : 1u);
     if (const char* e = std::getenv("RTX_SPLIT_PARTS")) {
         const int v = std::atoi(e);
@@ -1829,6 +2143,7 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& B : c->sb) {
         (void)hipFree(B.d);
+        (void)hipFree(B.cull);
         if (B.h) (void)hipHostFree(B.h);
         if (B.done) (void)hipEventDestroy(B.done);
     }
@@ -1848,6 +2163,8 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     (void)hipFree(c->d_occ);
     (void)hipFree(c->d_hstk);
     (void)hipFree(c->d_hstkT);
+    (void)hipFree(c->d_cull_box);
+    (void)hipFree(c->d_cull_marg);
     if (c->ev_heavy) (void)hipEventDestroy(c->ev_heavy);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -1886,6 +2203,77 @@ struct UploadLayout {
 };
 
 int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay);
+
+// Queue the record launches of the anchors in A (rtx_cull_tri_margin + rtx_cull_nodes_*) on the
+// context stream, the per-triangle boxes first when `boxes`.  Grows the scratch (after a stream
+// sync: queued launches may still read the old buffers).
+int cull_launch(rtx_ctx* c, const CullAnchors& A, bool boxes) {
+    const uint32_t nt = c->cull_ntris;
+    const size_t marg_need = static_cast<size_t>(kMaxViews > kMaxCullLights ? kMaxViews : kMaxCullLights) * nt;
+    if (2 * static_cast<size_t>(nt) > c->cull_box_cap || marg_need > c->cull_marg_cap) {
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_cull_box);
+        (void)hipFree(c->d_cull_marg);
+        c->d_cull_box = nullptr;
+        c->d_cull_marg = nullptr;
+        c->cull_box_cap = c->cull_marg_cap = 0;
+        HIP_TRY(c, hipMalloc(&c->d_cull_box, 2 * static_cast<size_t>(nt) * sizeof(float4)));
+        HIP_TRY(c, hipMalloc(&c->d_cull_marg, marg_need * sizeof(float)));
+        c->cull_box_cap = 2 * static_cast<size_t>(nt);
+        c->cull_marg_cap = marg_need;
+    }
+    const uint32_t tb = (nt + 255u) / 256u;
+    if (boxes) {
+        hipLaunchKernelGGL(rtx_cull_tri_box, dim3(tb), dim3(256), 0, c->stream, c->dev.tris, nt, c->d_cull_box);
+        HIP_TRY(c, hipGetLastError());
+    }
+    if (A.n == 0) return RTX_OK;
+    float4* rec = const_cast<float4*>(c->dev.cull);
+    const uint32_t stride4 = c->dev.cull_stride / 16u;
+    const CullParams P{c->dev.nodes, c->cull_ratio, c->cull_leaves ? 1u : 0u};
+    hipLaunchKernelGGL(rtx_cull_tri_margin, dim3(tb, A.n), dim3(256), 0, c->stream, c->dev.tris, nt, A, c->d_cull_marg);
+    HIP_TRY(c, hipGetLastError());
+    hipLaunchKernelGGL(rtx_cull_nodes_small, dim3((c->cull_nslots + 255u) / 256u), dim3(256), 0, c->stream, c->cull_rng,
+                       c->cull_nslots, c->d_cull_box, c->d_cull_marg, nt, A, rec, stride4, P);
+    HIP_TRY(c, hipGetLastError());
+    if (c->cull_nbig) {
+        hipLaunchKernelGGL(rtx_cull_nodes_big, dim3(c->cull_nbig), dim3(64), 0, c->stream, c->cull_big, c->cull_rng,
+                           c->d_cull_box, c->d_cull_marg, nt, A, rec, stride4, P);
+        HIP_TRY(c, hipGetLastError());
+    }
+    return RTX_OK;
+}
+
+// At upload: the per-triangle boxes and every light's records (tmax bound T[l]).
+int cull_records(rtx_ctx* c, const std::vector<float>& T, const rtx_light* lights, uint32_t n_lights, bool boxes) {
+    CullAnchors A{};
+    for (uint32_t l = 0; l < n_lights; ++l) {
+        for (int k = 0; k < 3; ++k) A.p[A.n][k] = lights[l].origin[k];
+        A.p[A.n][3] = T[l] > 0.f ? T[l] : 1.f;   // T = 0: never culled (cull_ray), any bound will do
+        A.idx[A.n] = static_cast<uint32_t>(kMaxViews) + l;
+        ++A.n;
+    }
+    return cull_launch(c, A, boxes);
+}
+
+// Before a frame: the records of every view whose camera origin is not the one its records of
+// the current image were made for (bitwise).
+int cull_views(rtx_ctx* c, const FrameArgs& F) {
+    CullAnchors A{};
+    for (uint32_t v = 0; v < F.n_views && v < static_cast<uint32_t>(kMaxViews); ++v) {
+        const float* o = F.cam[v].origin;
+        if ((c->cull_view_valid >> v) & 1u && std::memcmp(c->cull_view[v], o, 12) == 0) continue;
+        std::memcpy(c->cull_view[v], o, 12);
+        c->cull_view_valid |= 1u << v;
+        for (int k = 0; k < 3; ++k) A.p[A.n][k] = o[k];
+        A.p[A.n][3] = 0.f;
+        A.idx[A.n] = v;
+        ++A.n;
+    }
+    if (A.n == 0) return RTX_OK;
+    ++c->cull_updates;
+    return cull_launch(c, A, false);
+}
 }  // namespace
 
 extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) { return upload_scene(c, s, nullptr); }
@@ -1908,6 +2296,12 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         nodes.reserve(2 * nn + 4 * s->n_meshes + 4);
     }
     bool split_ok = s->n_lights <= static_cast<uint32_t>(kMaxSplitLights);
+    // exact cull (DevScene::cull): host uploads (a device-animated image is rebuilt in place and
+    // carries no records), at most kMaxCullLights lights
+    bool cull_on = !lay && !c->no_cull && s->n_lights <= static_cast<uint32_t>(kMaxCullLights);
+    double bmin[3] = {INFINITY, INFINITY, INFINITY}, bmax[3] = {-INFINITY, -INFINITY, -INFINITY};   // mesh vertices
+    std::vector<std::pair<uint32_t, uint32_t>> mesh_slots;   // node slots [first, end) of each mesh's tree
+    std::vector<float> tbox;   // per triangle (lo, hi) per axis: the cull's worth estimate below
     double max_ee = 0.0;   // max |e1| * |e2| over the triangles (DevScene::tri_fast)
     int max_depth = 0;     // deepest BVH node over the meshes (stack variant)
     for (uint32_t i = 0; i < s->n_spheres; ++i) {
@@ -1949,6 +2343,12 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
                               std::sqrt(double(e2.x) * e2.x + double(e2.y) * e2.y + double(e2.z) * e2.z);
             max_ee = (ee > max_ee || ee != ee) ? ee : max_ee;   // NaN sticks
             tri.push_back(f4(bits(m.material), 0.f, 0.f, 0.f));
+            for (int a = 0; a < 3; ++a) {
+                const float lo = std::fmin(v0[a], std::fmin(v1[a], v2[a])), hi = std::fmax(v0[a], std::fmax(v1[a], v2[a]));
+                bmin[a] = std::fmin(bmin[a], lo);
+                bmax[a] = std::fmax(bmax[a], hi);
+                if (cull_on) { tbox.push_back(lo); tbox.push_back(hi); }
+            }
         }
         uint32_t root = 0;
         if (m.n_nodes) {
@@ -1987,6 +2387,7 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
                 nodes[2 * dst] = f4(nd.min[0], nd.max[0], nd.min[1], nd.max[1]);
                 nodes[2 * dst + 1] = f4(nd.min[2], nd.max[2], bits(link), bits(cnt));
             }
+            mesh_slots.push_back({root, static_cast<uint32_t>(nodes.size() / 2)});
             if (lay && lay->reserve[mi]) {   // slots root .. root + 2T - 1 belong to this mesh
                 const size_t want = 2 * (static_cast<size_t>(root) + 2 * static_cast<size_t>(ntri));
                 if (nodes.size() < want) nodes.resize(want + (want / 2) % 2 * 2, f4(0, 0, 0, 0));
@@ -2009,6 +2410,68 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
     }
     if (parts.size() > static_cast<size_t>(kMaxParts)) split_ok = false;
     if (!split_ok) parts.clear();
+    // Cull records' inputs: per node slot the range of device triangles under it (leaf order is
+    // contiguous within a subtree; children's slots follow their parent's, so one backward sweep),
+    // the slots whose range a wave reduces (rtx_cull_nodes_big), and per light the tmax up to which
+    // its shadow rays are culled: 4x the farthest mesh-box corner + 1 (longer rays pass).
+    std::vector<uint2> cull_rng;
+    std::vector<uint32_t> cull_big;
+    std::vector<float> cull_T;
+    if (cull_on) {
+        cull_on = !tri.empty() && !mesh_slots.empty();
+        for (int a = 0; a < 3; ++a) cull_on = cull_on && std::isfinite(bmin[a]) && std::isfinite(bmax[a]);
+    }
+    if (cull_on) {
+        // Worth it?  The surface areas of the reference's boxes over those of the tight boxes,
+        // summed over the nodes (the SAH estimate of how many more slab tests the reference's
+        // boxes pass): below c->cull_min_sa the records cost more than they save (measured: W4_Bunny
+        // 1.19, -11 %; W4_Optional 2.40, +48 %; Synthetic100k 9.26, +182 %; profiles/r04).
+        cull_rng.assign(nodes.size() / 2, make_uint2(0u, 0u));
+        std::vector<float> nb(6 * (nodes.size() / 2));
+        double sa_ref = 0.0, sa_tight = 0.0;
+        auto sa = [](double x, double y, double z) { return 2.0 * (x * y + y * z + z * x); };
+        for (const auto& [r0, r1] : mesh_slots)
+            for (uint32_t sl = r1; sl-- > r0;) {
+                uint32_t link, cnt;
+                std::memcpy(&link, &nodes[2 * sl + 1].z, 4);
+                std::memcpy(&cnt, &nodes[2 * sl + 1].w, 4);
+                float* b = &nb[6 * sl];
+                if (cnt) {
+                    cull_rng[sl] = make_uint2(link, link + cnt);
+                    for (int a = 0; a < 3; ++a) { b[2 * a] = INFINITY; b[2 * a + 1] = -INFINITY; }
+                    for (uint32_t t = link; t < link + cnt && t < tbox.size() / 6; ++t)
+                        for (int a = 0; a < 3; ++a) {
+                            b[2 * a] = std::fmin(b[2 * a], tbox[6 * t + 2 * a]);
+                            b[2 * a + 1] = std::fmax(b[2 * a + 1], tbox[6 * t + 2 * a + 1]);
+                        }
+                } else {
+                    cull_rng[sl] = make_uint2(std::min(cull_rng[link].x, cull_rng[link + 1].x),
+                                              std::max(cull_rng[link].y, cull_rng[link + 1].y));
+                    for (int a = 0; a < 3; ++a) {
+                        b[2 * a] = std::fmin(nb[6 * link + 2 * a], nb[6 * (link + 1) + 2 * a]);
+                        b[2 * a + 1] = std::fmax(nb[6 * link + 2 * a + 1], nb[6 * (link + 1) + 2 * a + 1]);
+                    }
+                }
+                if (cull_rng[sl].y - cull_rng[sl].x > kCullBigTris) cull_big.push_back(sl);
+                const float4 r0v = nodes[2 * sl], r1v = nodes[2 * sl + 1];
+                sa_ref += sa(double(r0v.y) - r0v.x, double(r0v.w) - r0v.z, double(r1v.y) - r1v.x);
+                sa_tight += sa(std::fmax(double(b[1]) - b[0], 0.0), std::fmax(double(b[3]) - b[2], 0.0),
+                               std::fmax(double(b[5]) - b[4], 0.0));
+            }
+        cull_on = sa_ref >= c->cull_min_sa * sa_tight;   // false for NaN
+        for (uint32_t i = 0; i < s->n_lights; ++i) {
+            double R = 0.0;
+            for (int k = 0; k < 8; ++k) {
+                const double cx = (k & 1) ? bmax[0] : bmin[0], cy = (k & 2) ? bmax[1] : bmin[1],
+                             cz = (k & 4) ? bmax[2] : bmin[2];
+                const double dx = s->lights[i].origin[0] - cx, dy = s->lights[i].origin[1] - cy,
+                             dz = s->lights[i].origin[2] - cz;
+                R = std::fmax(R, std::sqrt(dx * dx + dy * dy + dz * dz));
+            }
+            const double T = 4.0 * R + 1.0;
+            cull_T.push_back(std::isfinite(T) && T < 0x1p60 ? static_cast<float>(T) : 0.f);   // 0: never culled
+        }
+    }
     // Device links are byte offsets (s_load with an SGPR offset, no address arithmetic):
     // inner node -> its child pair (2 slots x 32 B), leaf -> its first 64-B triangle.
     if (tri.size() * 16 >= (1ull << 32) || nodes.size() * 16 >= (1ull << 32) || sph.size() * 16 >= (1ull << 32) ||
@@ -2051,7 +2514,9 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
                   {pl.data(), pl.size() * 16, 0},         {tri.data(), tri.size() * 16, 0},
                   {nullptr, node_sec, 0},
                   {meshes.data(), meshes.size() * 16, 0}, {lights.data(), lights.size() * 16, 0},
-                  {mats.data(), mats.size() * 16, 0},     {parts.data(), parts.size() * 16, 0}};
+                  {mats.data(), mats.size() * 16, 0},     {parts.data(), parts.size() * 16, 0},
+                  {cull_rng.data(), cull_rng.size() * 8, 0}, {cull_big.data(), cull_big.size() * 4, 0},
+                  {cull_T.data(), cull_T.size() * 4, 0}};
     size_t total = 0;
     for (auto& x : secs) { x.off = total; total += align256(x.n ? x.n : 16); }
     HIP_TRY(c, hipSetDevice(c->device));
@@ -2070,6 +2535,17 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         HIP_TRY(c, hipMalloc(&B.d, total));
         HIP_TRY(c, hipHostMalloc(&B.h, total));
         B.cap = total;
+    }
+    // cull records: one copy of the node slots per anchor (kMaxViews cameras, then the lights)
+    const size_t cull_stride = align256(nodes.size() * 16);
+    const size_t cull_bytes = cull_on ? (kMaxViews + static_cast<size_t>(s->n_lights)) * cull_stride : 0;
+    if (cull_on && (cull_stride >= (1ull << 32) || 2 * tri.size() >= (1ull << 32))) cull_on = false;
+    if (cull_on && cull_bytes > B.cull_cap) {
+        (void)hipFree(B.cull);
+        B.cull = nullptr;
+        B.cull_cap = 0;
+        HIP_TRY(c, hipMalloc(&B.cull, cull_bytes));
+        B.cull_cap = cull_bytes;
     }
     // Large node arrays send copy 0 only and the device writes copies 1..7 (rtx_octant_expand):
     // 1/8 of the node bytes over PCIe and of the host's staging writes (an upload per animated
@@ -2132,7 +2608,22 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
     d.tri_fast = max_ee <= 0x1p56 ? 1u : 0u;
     d.oct_bytes = (RTX_OCTANT && oct_ok && !std::getenv("RTX_NO_OCTANT")) ? static_cast<uint32_t>(node_bytes) : 0u;
     d.n_tris = static_cast<uint32_t>(tri.size() / 4); d.n_nodes = static_cast<uint32_t>(nodes.size() / 2);
+    if (cull_on) {
+        d.cull = B.cull;
+        d.cull_T = reinterpret_cast<const float*>(base + secs[11].off);
+        d.cull_stride = static_cast<uint32_t>(cull_stride);
+        c->cull_rng = reinterpret_cast<const uint2*>(base + secs[9].off);
+        c->cull_big = reinterpret_cast<const uint32_t*>(base + secs[10].off);
+        c->cull_nslots = d.n_nodes;
+        c->cull_nbig = static_cast<uint32_t>(cull_big.size());
+        c->cull_ntris = d.n_tris;
+    }
+    c->cull_view_valid = 0;
     c->dev = d;
+    if (cull_on) {   // per-triangle boxes, then the lights' records (cameras: at their first frame)
+        const int rc = cull_records(c, cull_T, s->lights, s->n_lights, true);
+        if (rc != RTX_OK) return rc;
+    }
     // a BVH kStackDepth or more levels deep renders with the deep-stack variant, unsplit;
     // kStackDepthDeep or more with its stacks in HBM
     c->deep_stack = max_depth >= kStackDepth;
@@ -2238,6 +2729,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
             F.cam[v].room_fast = ok ? 1u : 0u;
         }
     }
+    F.n_views = static_cast<uint32_t>(n_views);
     F.aspect = static_cast<int>(p->width) / static_cast<float>(static_cast<int>(p->height));  // Renderer.cpp:30
     F.inv_width = 1.f / static_cast<float>(static_cast<int>(p->width));
     F.inv_height = 1.f / static_cast<float>(static_cast<int>(p->height));
@@ -2346,15 +2838,23 @@ int spec_variant(int facts) {
 }
 
 // The split launches of a frame (PHASE 1-3) in the frame's specialised variant v (-1: generic).
+template <int P, bool CU>
+void launch_phase_v(int v, dim3 g, hipStream_t s, const DevScene& d, const FrameArgs& F) {
+    switch (v) {
+    case 0: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[0], false, CU>), g, dim3(kBlockThreads), 0, s, d, F); break;
+    case 1: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[1], false, CU>), g, dim3(kBlockThreads), 0, s, d, F); break;
+    case 2: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[2]>), g, dim3(kBlockThreads), 0, s, d, F); break;   // (no mesh: nothing to cull)
+    case 3: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[3], false, CU>), g, dim3(kBlockThreads), 0, s, d, F); break;
+    case 4: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[4], false, CU>), g, dim3(kBlockThreads), 0, s, d, F); break;
+    default: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, 0, false, CU>), g, dim3(kBlockThreads), 0, s, d, F); break;
+    }
+}
+// PHASE P of a frame in the frame's specialised variant v (-1: generic), with the cull variant
+// when the scene has cull records
 template <int P>
 void launch_phase(int v, dim3 g, hipStream_t s, const DevScene& d, const FrameArgs& F) {
-    switch (v) {
-    case 0: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[0]>), g, dim3(kBlockThreads), 0, s, d, F); break;
-    case 1: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[1]>), g, dim3(kBlockThreads), 0, s, d, F); break;
-    case 3: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[3]>), g, dim3(kBlockThreads), 0, s, d, F); break;
-    case 4: hipLaunchKernelGGL((rtx_render_kernel<false, P, false, kSpecVariants[4]>), g, dim3(kBlockThreads), 0, s, d, F); break;
-    default: hipLaunchKernelGGL((rtx_render_kernel<false, P>), g, dim3(kBlockThreads), 0, s, d, F); break;   // (2: no mesh, never split)
-    }
+    if (d.cull_stride) launch_phase_v<P, true>(v, g, s, d, F);
+    else launch_phase_v<P, false>(v, g, s, d, F);
 }
 
 // The HBM stacks of the HSTK variant: max_depth + 1 entries for each wave of a launch of
@@ -2401,6 +2901,10 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         HIP_TRY(c, hipGetLastError());
         return RTX_OK;
     }
+    if (c->dev.cull_stride) {   // the views' camera-anchor cull records, when a camera moved
+        const int rc = cull_views(c, F);
+        if (rc != RTX_OK) return rc;
+    }
     // the first specialised variant whose facts the scene and frame satisfy (kSpecVariants;
     // RTX_NO_SPEC=1 forces the generic kernel); the split launches take it too
     const int facts = c->scene_spec | ((F.mode == RTX_MODE_COMBINED && F.shadows) ? kSpecCombShadows : 0);
@@ -2423,27 +2927,12 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(c->ev_join, s2));
     }
-    if (c->hbm_stack)
+    if (c->hbm_stack)   // (the deep variants walk without the cull)
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, true, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
     else if (c->deep_stack)
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
-    else if (v == 0)
-        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecVariants[0]>), grid, dim3(kBlockThreads), 0,
-                           c->stream, c->dev, F);
-    else if (v == 1)
-        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecVariants[1]>), grid, dim3(kBlockThreads), 0,
-                           c->stream, c->dev, F);
-    else if (v == 2)
-        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecVariants[2]>), grid, dim3(kBlockThreads), 0,
-                           c->stream, c->dev, F);
-    else if (v == 3)
-        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecVariants[3]>), grid, dim3(kBlockThreads), 0,
-                           c->stream, c->dev, F);
-    else if (v == 4)
-        hipLaunchKernelGGL((rtx_render_kernel<false, 0, false, kSpecVariants[4]>), grid, dim3(kBlockThreads), 0,
-                           c->stream, c->dev, F);
     else
-        hipLaunchKernelGGL((rtx_render_kernel<false, 0>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
+        launch_phase<0>(v, grid, c->stream, c->dev, F);
     HIP_TRY(c, hipGetLastError());
     if (F.heavy_flag) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     if (F.cost) {
@@ -2667,6 +3156,13 @@ extern "C" int rtx_schedule_state(rtx_ctx* c, uint32_t* order, uint32_t* cost, u
     return RTX_OK;
 }
 
+extern "C" int rtx_cull_info(rtx_ctx* c, uint32_t* enabled, uint64_t* camera_updates) {
+    if (!c) return RTX_E_INVALID;
+    if (enabled) *enabled = c->dev.cull_stride ? 1u : 0u;
+    if (camera_updates) *camera_updates = c->cull_updates;
+    return RTX_OK;
+}
+
 extern "C" int rtx_split_info(rtx_ctx* c, uint32_t* heavy_tiles, uint32_t* parts) {
     if (!c) return RTX_E_INVALID;
     if (c->heavy_pending) {   // a measured frame is in flight: report the set it selects
@@ -2747,6 +3243,7 @@ struct rtx_anim {
     bool serial_frontier = false;         // RTX_ANIM_SERIAL_FRONTIER=1: the frontier's serial greedy for every mesh (tests)
     uint32_t cut = kAnimCut;              // RTX_ANIM_CUT: nodes above this many triangles split as queue tasks
     uint32_t epoch = 0;                   // updates so far (the build's publication flag)
+    uint64_t wait_ticks = rtxa::kWaitTicks;   // rtxa::Launch::wait_ticks (RTX_ANIM_WAIT_TICKS: tests of the timeout path)
     std::vector<double> obj_radius;       // per registered mesh: max |object-space position|
 };
 
@@ -2842,6 +3339,10 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
     if (const char* e = std::getenv("RTX_ANIM_CUT")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 8 && v < (1l << 30)) a->cut = static_cast<uint32_t>(v);
+    }
+    if (const char* e = std::getenv("RTX_ANIM_WAIT_TICKS")) {
+        const long long v = std::strtoll(e, nullptr, 10);
+        if (v >= 0) a->wait_ticks = static_cast<uint64_t>(v);
     }
     if (const char* e = std::getenv("RTX_ANIM_DEPTH_LIMIT")) {
         const int v = std::atoi(e);
@@ -2995,6 +3496,7 @@ extern "C" int rtx_anim_update(rtx_anim* a, rtx_ctx* c, const float* transforms)
     L.sub_lds = a->hbm_only ? 0u : 1u;
     L.frontier_max = a->serial_frontier ? 0u : rtxa::kFrontierHistMax;
     L.cut = a->cut;
+    L.wait_ticks = a->wait_ticks;
     L.epoch = ++a->epoch;
     ANIM_TRY(a, rtxa::launch_build(L, s));
     ANIM_TRY(a, hipEventRecord(a->ev, s));
@@ -3043,9 +3545,11 @@ extern "C" int rtx_anim_status(rtx_anim* a, uint32_t i, uint32_t status[4]) {
     if (a->built) ANIM_TRY(a, hipEventSynchronize(a->ev));
     ANIM_TRY(a, hipMemcpy(status, a->mesh[i].status, 16, hipMemcpyDeviceToHost));
     if (status[0])
-        return afail(a, RTX_E_UNSUPPORTED, status[0] & rtxa::kErrNaN       ? "NaN vertex in an animated mesh"
-                                           : status[0] & rtxa::kErrTimeout ? "device build timed out waiting for its top phase"
-                                                                            : "animated BVH too deep for the render stack");
+        return afail(a, RTX_E_UNSUPPORTED,
+                     status[0] & rtxa::kErrNaN        ? "NaN vertex in an animated mesh"
+                     : status[0] & rtxa::kErrTimeout  ? "device build: a worker timed out waiting for a queue entry (mesh disabled)"
+                     : status[0] & rtxa::kErrCapacity ? "device build: task queue or subtree table capacity exceeded (mesh disabled)"
+                                                      : "animated BVH too deep for the render stack (mesh disabled)");
     return RTX_OK;
 }
 

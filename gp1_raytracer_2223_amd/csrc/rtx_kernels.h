@@ -121,6 +121,13 @@ struct DevScene {
     uint4* hstk;
     unsigned long long* hstkT;   // the instrumented variant's tested-lane masks
     uint32_t hstk_depth;
+    // Exact cull (rtx_cull.h): per anchor a copy of cull_stride bytes of records at
+    // the node slots' byte offsets ({c, E.x}, {E.y, E.z, -, -}: box c +- E); anchor v < kMaxViews =
+    // view v's camera, kMaxViews + l = light l, whose shadow rays are culled only up to tmax
+    // cull_T[l].  cull_stride 0: off.
+    const float4* __restrict__ cull;
+    const float* __restrict__ cull_T;
+    uint32_t cull_stride;
 };
 
 #ifndef RTX_OCT_MAX_BYTES
@@ -129,6 +136,8 @@ struct DevScene {
 constexpr size_t kOctantMaxNodeBytes = RTX_OCT_MAX_BYTES;   // octant node copies only below this (per copy)
 constexpr size_t kOctantDeviceMinBytes = size_t(64) << 10;   // from this size copies 1..7 are written on the device
 constexpr int kMaxViews = 8;   // views (camera positions) rendered by one launch
+constexpr int kMaxCullLights = 32;   // lights with a cull anchor (more: the scene renders without the cull)
+constexpr uint32_t kCullBigTris = 64;   // node ranges above this many triangles reduce with a wave (rtx_cull_nodes_big)
 
 struct ViewCam {
     float origin[3];
@@ -144,7 +153,8 @@ struct ViewCam {
 };
 
 struct FrameArgs {
-    ViewCam cam[kMaxViews];       // blockIdx.z selects the view
+    ViewCam cam[kMaxViews];       // the tile's view selects the camera
+    uint32_t n_views;             // views in the launch
     float aspect;                 // (float)W / (float)H  (Renderer.cpp:30)
     float inv_width, inv_height;  // RN(1/W), RN(1/H): IEEE divisions on the host
     uint32_t width, height;

@@ -94,6 +94,12 @@ class DeviceContext:
         abi.check(self.lib.rtx_split_info(self.h, C.byref(h), C.byref(p)), "rtx_split_info", self.h)
         return h.value, p.value
 
+    def cull_info(self) -> tuple[bool, int]:
+        """(the uploaded scene renders with the exact cull, camera-record rebuilds so far)."""
+        on, n = C.c_uint32(), C.c_uint64()
+        abi.check(self.lib.rtx_cull_info(self.h, C.byref(on), C.byref(n)), "rtx_cull_info", self.h)
+        return bool(on.value), n.value
+
     def count_work(self, cam, params) -> np.ndarray:
         out = (C.c_uint64 * 12)()
         abi.check(self.lib.rtx_count_work(self.h, C.byref(cam), C.byref(params), out), "rtx_count_work", self.h)

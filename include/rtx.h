@@ -242,6 +242,12 @@ int rtx_count_work_ex(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_para
  * and the frontier size of the uploaded scene (0 = the scene is rendered unsplit).
  * Environment: RTX_SPLIT=0 disables, RTX_SPLIT=force splits every tile (tests). */
 int rtx_split_info(rtx_ctx* ctx, uint32_t* heavy_tiles, uint32_t* parts);
+/* Exact cull (no reference counterpart: a pruning of the reference's own BVH walk that never
+ * changes a pixel).  Reports whether the uploaded scene renders with it (on for
+ * host uploads whose reference boxes are inflated enough to pay, see upload_scene) and how
+ * many times a camera's records were (re)built.  Environment: RTX_NO_CULL=1 disables;
+ * RTX_CULL_MIN_SA, RTX_CULL_RATIO tune the enabling test and the per-node flag (tests). */
+int rtx_cull_info(rtx_ctx* ctx, uint32_t* enabled, uint64_t* camera_updates);
 /* Diagnostics of the cost-ordered dispatch (tests): after a measured frame, the dispatch
  * permutation of the first n tiles' slots (`order`) and the one-piece tile costs it was
  * sorted by (`cost`).  *n_tiles = tiles of the current schedule (0 = none measured yet;

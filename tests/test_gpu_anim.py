@@ -168,8 +168,8 @@ def test_device_update_task_cut_extremes(gpu_ctx, cut, monkeypatch):
         for t in TIMES[:3]:
             anim.update(t, gpu_ctx)
             host_scene.update(t)
-            assert list(anim.status(0)[:1]) == [0]
-            for k in range(len(anim.mesh_ids)):
+            for k in range(len(anim.mesh_ids)):   # every registered mesh's error bits, not only mesh 0's
+                assert list(anim.status(k)[:1]) == [0], (name, t, k)
                 _compare_state(anim, host_scene, k)
         anim.close()
 
@@ -245,6 +245,43 @@ def test_device_update_too_deep_tree_is_disabled_not_rendered(monkeypatch):
         apx, _ = a.render(cam, p)
         bpx, _ = b.render(cam, p)
         assert np.array_equal(apx, bpx)
+    anim.close()
+    a.close()
+    b.close()
+
+
+def test_device_update_timeout_disables_the_mesh(monkeypatch):
+    """A worker that gives up waiting for a queue entry (Launch::wait_ticks) leaves the entry it
+    claimed unbuilt: the tree is incomplete.  The output launch must then write none of it and
+    disable the mesh (node count 0, no frontier parts), and the update report kErrTimeout.  Forced
+    with a zero wait (RTX_ANIM_WAIT_TICKS=0, read at rtx_anim_create): W4_Optional's 65 workers
+    mostly claim entries not published yet and give up at once.  Either outcome is checked: if no
+    worker timed out, the build is complete and the frames equal the host Update's.  The error is
+    sticky: an incomplete build breaks the chain of permutations every later Update starts from,
+    so once it happened every later Update reports it and keeps the mesh disabled."""
+    monkeypatch.setenv("RTX_ANIM_WAIT_TICKS", "0")
+    dev_scene, host_scene = _scene("W4_Optional"), _scene("W4_Optional")
+    a, b = DeviceContext(0), DeviceContext(0)
+    anim = DeviceAnimation(dev_scene, a)
+    timed_out = 0
+    for t in TIMES[:3]:
+        anim.update(t, a)
+        host_scene.update(t)
+        s, cam = host_scene.view()
+        try:
+            anim.status(0)
+            assert timed_out == 0, "the error must be sticky"
+        except RuntimeError as e:
+            assert "timed out" in str(e), e
+            timed_out += 1
+            s.meshes[0].n_nodes = 0   # the disabled mesh: triangles present, no tree to walk
+        b.upload(s)
+        p = abi.make_params(320, 180)
+        for _ in range(3):
+            apx, _ = a.render(cam, p)
+            bpx, _ = b.render(cam, p)
+            assert np.array_equal(apx, bpx), (t, timed_out)
+    assert timed_out > 0, "a zero wait should make some worker give up"
     anim.close()
     a.close()
     b.close()

@@ -1,0 +1,193 @@
+"""The exact cull (rtx_cull.h): nodes skipped because the ray's line misses their
+tight box widened by the proven Möller–Trumbore margin.  A skipped node must never change a pixel:
+every frame here is compared bit for bit with a context created under RTX_NO_CULL=1 (the
+reference's traversal, unpruned) and with the oracle.  Cameras are chosen to stress the bound:
+in the plane of a triangle (its margin is then infinite), at a vertex, inside and under the
+height field, far away, several views per launch with different anchors, and a camera that
+moves between frames of one context (the anchor's records are rebuilt)."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import oracle_bind
+from gp1_raytracer_2223_amd import abi
+from gp1_raytracer_2223_amd.renderer import DeviceContext
+from gp1_raytracer_2223_amd.scene import HostScene
+
+pytestmark = pytest.mark.gpu
+
+MESH_SCENES = ["W4_Bunny", "W4_Reference", "W4_Optional", "Synthetic100k", "Bunny8Lights"]
+POW_FREE = {"W4_Bunny", "Synthetic100k", "Bunny8Lights"}
+
+
+def _ctx_env(**env):
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return DeviceContext(int(os.environ.get("RTX_TEST_DEVICE", "0")))
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def cull_ctx():
+    """A context that culls every scene (the product enables the cull only where the SAH estimate
+    says it pays, RTX_CULL_MIN_SA) and tests every record (RTX_CULL_RATIO=0)."""
+    ctx = _ctx_env(RTX_CULL_MIN_SA="0", RTX_CULL_RATIO="0")
+    yield ctx
+    ctx.close()
+
+
+@pytest.fixture(scope="module")
+def plain_ctx():
+    """A context without the cull: the reference's full traversal."""
+    ctx = _ctx_env(RTX_NO_CULL="1")
+    yield ctx
+    ctx.close()
+
+
+def _same(a, b, what):
+    assert np.array_equal(a[0], b[0]), f"{what}: {(a[0] != b[0]).sum()} pixels differ"
+    assert np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32)), f"{what}: colour planes differ"
+
+
+def _check(gpu_ctx, plain_ctx, s, cam, p, what, exact_oracle):
+    gpu_ctx.upload(s)
+    plain_ctx.upload(s)
+    for _ in range(3):   # the cost-ordered / split frames too
+        g = gpu_ctx.render(cam, p)
+    q = plain_ctx.render(cam, p)
+    _same(g, q, f"{what} cull vs no cull")
+    r = oracle_bind.render(s, cam, p)
+    d = float(np.abs(g[1] - r[1]).max(initial=0.0))
+    assert d <= 1e-4, f"{what}: max-abs {d} vs the oracle"
+    if exact_oracle:
+        _same(g, r, f"{what} vs oracle")
+
+
+@pytest.mark.parametrize("name", MESH_SCENES)
+@pytest.mark.parametrize("t", [-1.0, 1.3])
+@pytest.mark.parametrize("mode,shadows", [(3, 1), (0, 1), (3, 0)])
+def test_cull_equals_full_traversal(cull_ctx, gpu_ctx, plain_ctx, name, t, mode, shadows):
+    hs = HostScene(name)
+    if t >= 0:
+        hs.update(t)
+    s, cam = hs.view()
+    for ctx in (cull_ctx, gpu_ctx):   # forced on, and the product's choice
+        _check(ctx, plain_ctx, s, cam, abi.make_params(320, 180, mode, shadows), f"{name}@{t}/m{mode}s{shadows}",
+               name in POW_FREE or mode in (0, 1))
+
+
+def _synthetic_triangle(hs, k):
+    a = hs.arrays()["meshes"][0]
+    P = a["tpositions"].reshape(-1, 3)
+    I = a["indices"].reshape(-1, 3)
+    return P[I[k, 0]], P[I[k, 1]], P[I[k, 2]]
+
+
+def _cameras():
+    hs = HostScene("Synthetic100k")
+    v0, v1, v2 = _synthetic_triangle(hs, 777)
+    e1, e2 = (v1 - v0).astype(np.float32), (v2 - v0).astype(np.float32)
+    in_plane = (v0 + np.float32(3.0) * e1 - np.float32(2.0) * e2).astype(np.float32)
+    w0, w1, _ = _synthetic_triangle(hs, 40000)
+    far_in_plane = (w0 + np.float32(40.0) * (w1 - w0)).astype(np.float32)
+    return [
+        ("reference", (0.0, 3.0, -9.0), 45.0, 0.0, 0.0),
+        ("in_a_triangle_plane", tuple(float(x) for x in in_plane), 60.0, -0.5, 0.3),
+        ("in_a_plane_far", tuple(float(x) for x in far_in_plane), 45.0, -0.3, 0.0),
+        ("at_a_vertex", tuple(float(x) for x in v0), 70.0, -0.4, 0.8),
+        ("inside_the_field", (0.01, 0.55, 1.0), 90.0, 0.0, 0.0),
+        ("under_the_field", (0.5, 0.1, 0.5), 90.0, 0.6, 0.2),
+        ("grazing_the_top", (-2.9, 0.81, -1.5), 50.0, -0.02, 0.0),
+        ("far_away", (30.0, 40.0, -60.0), 20.0, -0.55, -0.45),
+    ]
+
+
+@pytest.mark.parametrize("cam_case", _cameras(), ids=lambda c: c[0])
+def test_cull_adversarial_cameras(cull_ctx, plain_ctx, cam_case):
+    what, origin, fov, pitch, yaw = cam_case
+    hs = HostScene("Synthetic100k")
+    hs.set_camera(origin, fov, pitch, yaw)
+    s, cam = hs.view()
+    _check(cull_ctx, plain_ctx, s, cam, abi.make_params(240, 160), what, True)
+
+
+def test_cull_views_with_different_anchors(cull_ctx, plain_ctx):
+    """One launch, several views: each view's rays use that view's camera anchor."""
+    hs = HostScene("Synthetic100k")
+    s, cam = hs.view()
+    W, H, N = 192, 128, 4
+    views = (abi.Camera * N)()
+    for f in range(N):
+        C.memmove(C.byref(views[f]), C.byref(cam), C.sizeof(abi.Camera))
+        views[f].origin[0] = cam.origin[0] + 0.75 * f
+        views[f].origin[1] = cam.origin[1] - 0.4 * f
+    p = abi.make_params(W, H)
+    out = []
+    for ctx in (cull_ctx, plain_ctx):
+        ctx.upload(s)
+        for _ in range(2):
+            abi.check(ctx.lib.rtx_render_views_async(ctx.h, views, N, C.byref(p), 1), "views", ctx.h)
+        abi.check(ctx.lib.rtx_synchronize(ctx.h), "sync", ctx.h)
+        px = np.zeros(N * W * H, np.uint32)
+        rgb = np.zeros(3 * N * W * H, np.float32)
+        abi.check(ctx.lib.rtx_download(ctx.h, px.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                       rgb.ctypes.data_as(C.POINTER(C.c_float))), "dl", ctx.h)
+        out.append((px, rgb))
+    _same(out[0], out[1], "views")
+    for f in range(N):
+        r = oracle_bind.render(s, views[f], p)
+        g = (out[0][0][f * W * H:(f + 1) * W * H], out[0][1][3 * f * W * H:3 * (f + 1) * W * H])
+        _same(g, r, f"view {f} vs oracle")
+
+
+def test_cull_camera_moves_between_frames(cull_ctx):
+    """One context, the camera moved between frames (and back): the anchor's records follow."""
+    hs = HostScene("Synthetic100k")
+    s, cam0 = hs.view()
+    p = abi.make_params(200, 120)
+    cull_ctx.upload(s)
+    cams = []
+    for dx in (0.0, 1.5, -2.0, 0.0):
+        c = abi.Camera()
+        C.memmove(C.byref(c), C.byref(cam0), C.sizeof(abi.Camera))
+        c.origin[0] = cam0.origin[0] + dx
+        cams.append(c)
+    for c in cams:
+        g = cull_ctx.render(c, p)
+        _same(g, oracle_bind.render(s, c, p), f"camera x+{c.origin[0] - cam0.origin[0]}")
+
+
+@pytest.mark.parametrize("name,on", [("Synthetic100k", True), ("W4_Optional", True), ("W4_Bunny", False),
+                                     ("Bunny8Lights", False), ("W3", False)])
+def test_cull_enabled_where_it_pays(gpu_ctx, name, on):
+    """The product enables the cull where the reference's boxes are inflated enough (the SAH
+    estimate of upload_scene: W4_Bunny 1.19, W4_Optional 2.40, Synthetic100k 9.26)."""
+    hs = HostScene(name)   # (the scene's arrays live as long as hs)
+    s, cam = hs.view()
+    gpu_ctx.upload(s)
+    assert gpu_ctx.cull_info()[0] == on
+
+
+def test_cull_records_follow_the_camera(cull_ctx):
+    """A view's records are rebuilt only when its camera origin changes."""
+    hs = HostScene("Synthetic100k")
+    s, cam = hs.view()
+    p = abi.make_params(64, 64)
+    cull_ctx.upload(s)
+    n0 = cull_ctx.cull_info()[1]
+    cull_ctx.render(cam, p)
+    cull_ctx.render(cam, p)
+    assert cull_ctx.cull_info()[1] == n0 + 1
+    c = abi.Camera()
+    C.memmove(C.byref(c), C.byref(cam), C.sizeof(abi.Camera))
+    c.origin[2] = cam.origin[2] - 0.5
+    cull_ctx.render(c, p)
+    assert cull_ctx.cull_info()[1] == n0 + 2
