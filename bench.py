@@ -513,6 +513,38 @@ class Workload:
                 "value": self.frame_pixels * steps / elapsed / 1e6, "ms_per_step": elapsed / steps * 1e3}
 
 
+def stripe_predictor(ctx: DeviceContext, wl: "Workload", lib_hash: str, steps=(2, 4, 8), launches: int = 30) -> dict:
+    """One-GPU predictor of strong scaling (N = 1 only): the frame cut into 16-row stripes dealt
+    over s ranks, each rank's share timed alone on this GPU (serialized launches, HIP events,
+    after a warm-up that builds the share's cost order).  The step time at s GPUs is the slowest
+    share's, so efficiency(s) = t_full / (s * max_r t_share(r)); `rank0` uses rank 0's share only.
+    What it leaves out: the host gather and the ranks' clocks (one GPU times every share)."""
+    lib = ctx.lib
+    cam = wl.views
+
+    def t(p):
+        ms = C.c_float()
+        abi.check(lib.rtx_time_views(ctx.h, cam, 1, C.byref(p), 5, C.byref(ms)), "rtx_time_views", ctx.h)
+        best = None
+        for _ in range(2):
+            abi.check(lib.rtx_time_views(ctx.h, cam, 1, C.byref(p), launches, C.byref(ms)), "rtx_time_views", ctx.h)
+            best = ms.value if best is None else min(best, ms.value)
+        return best
+
+    t_full = t(abi.make_params(wl.W, wl.H))
+    out = {"method": f"each share timed alone (rtx_time_views, best of 2 x {launches} launches after 5 warm-up "
+                     "launches); efficiency = t_full / (s * slowest share)", "t_full_ms": round(t_full, 5)}
+    for s_ in steps:
+        shares = [t(abi.make_params(wl.W, wl.H, stripe_rows=16, stripe_first=r, stripe_step=s_)) for r in range(s_)]
+        rec, src = pmc_traffic(wl.scene, wl.W, wl.H, 1, s_, lib_hash)
+        out[f"s{s_}"] = {"share_ms": [round(x, 5) for x in shares],
+                         "efficiency": round(t_full / (s_ * max(shares)), 4),
+                         "efficiency_rank0": round(t_full / (s_ * shares[0]), 4),
+                         "hbm_bytes_per_frame_rank0": rec.get("hbm_bytes_per_frame") if rec else None,
+                         "hbm_source": src}
+    return out
+
+
 def roofline(flop: int, kernel_ms: float, rec: dict | None, src: str | None) -> dict:
     achieved = flop / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
     out = {"bound": "valu", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -628,6 +660,8 @@ def main() -> int:
                                      "equal shares of 16-row stripes)")
             if d.rank == 0:
                 entry["parity"] = parity_report(r["px0"], r["rgb0"], scene, mw, mh, with_fnv=False)
+            if N == 1:
+                entry["strong_scaling_predictor"] = stripe_predictor(ctxs[0], wl, lib_hash)
             multi.append(entry)
 
     # ---- 3. parity of every config at full size (N = 1; one rank per GPU renders stripes at N > 1)

@@ -111,8 +111,8 @@ def build_reference(force: bool = False) -> Path | None:
 def build_all(force: bool = False) -> None:
     build_host(force)
     build_oracle(force)
-    build_reference(force)
     build_hip(force)
+    build_reference(force)   # after librtx_hip.so: oracle/_ref/ref_binding links it
     build_cli(force)
 
 
