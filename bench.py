@@ -322,12 +322,18 @@ def cpu_baseline(ref: CpuReference, scene: str, width: int, height: int, frames:
     if quota is not None and int(quota) < nthreads:
         runs["quota"] = ref.run(scene, width, height, max(1, int(quota)), frames)
     runs["one"] = ref.run(scene, width, height, 1, 1)
-    r = runs["all"]
+    # `value` = the best CPU configuration measured here (the quota-sized run can beat the
+    # oversubscribed hardware_concurrency one), so speedup_vs_cpu is never inflated by a slow run
+    best = "quota" if "quota" in runs and runs["quota"]["mpix_s"] > runs["all"]["mpix_s"] else "all"
+    r = runs[best]
+    used = max(1, int(quota)) if best == "quota" else nthreads
     one = runs["one"]["mpix_s"]
-    out = {"value": round(r["mpix_s"], 4), "unit": "Mpixels/s", "cores": nthreads, "kind": ref.kind,
-           "sample": f"{frames} frames of {scene} {width}x{height}, median of Renderer::Render, {nthreads} threads "
-                     f"(= sched_getaffinity, the reference's hardware_concurrency), {ref.how}",
+    out = {"value": round(r["mpix_s"], 4), "unit": "Mpixels/s", "cores": used, "kind": ref.kind,
+           "sample": f"{frames} frames of {scene} {width}x{height}, median of Renderer::Render, {used} threads "
+                     f"(the faster of sched_getaffinity = {nthreads}, the reference's hardware_concurrency, and the "
+                     f"cgroup quota), {ref.how}",
            "median_s": r["median_s"], "fnv": r.get("fnv"),
+           "all_threads_mpix_s": round(runs["all"]["mpix_s"], 4),
            "single_thread_mpix_s": round(one, 4),
            "full_host_upper_bound_mpix_s": round(one * nthreads, 2),
            "cpu_model": cpu_model(), "nproc": os.cpu_count(), "cgroup_cpu_quota": quota}

@@ -92,21 +92,45 @@ RTX_CULL_HD static inline void rtx_cull_tri_setup(rtx_cull_tri* T, const float* 
     T->nerr = T->lN > 0 ? 0x1p-48 * (T->lE1 * T->lE2 / T->lN + 1.0) : INFINITY;
 }
 
-/* omega for |s~_k| <= sb[k] (+inf for a degenerate triangle) */
-RTX_CULL_HD static inline double rtx_cull_omega(const rtx_cull_tri* T, const double* sb) {
-    if (!(T->lN > 0)) return INFINITY;
-    double sumE1H = 0.0, sumSH = 0.0, sumQ = 0.0;
+/* Both bounds of one (anchor, triangle):
+ *   margin: the line of any accepted ray passes within `margin` of the triangle (above);
+ *   dt:     |t~ - t*| <= dt for any accepted ray whose computed t~ is at most Bt, where t* is the
+ *           line parameter of the point nearest to X: t* - tau~/a~ = Y.d / |d|^2
+ *           with Y = X - o' - (tau~/a~) d, whose components along d x E2 and d x E1 are those of
+ *           w and whose N component is E_tau - (tau~/a~) E_a, so
+ *           |t* - tau~/a~| <= (E_tau + Bt' E_a) / (|N| |d| c) + omega / (|d| c^2),
+ *           and t~ = fl(fl(1/a~) tau~) is tau~/a~ within 2.01 u t~.
+ * Both +inf when no bound closes. */
+typedef struct rtx_cull_bound {
+    double margin, dt;
+} rtx_cull_bound;
+
+RTX_CULL_HD static inline rtx_cull_bound rtx_cull_bounds(const rtx_cull_tri* T, const double* sb, double dist, double R,
+                                                        double Bt) {
+    rtx_cull_bound b = {INFINITY, INFINITY};
+    if (!(T->lN > 0)) return b;
+    double sumE1H = 0.0, sumSH = 0.0, sumQ = 0.0, sumE2Q = 0.0;
     for (int k = 0; k < 3; ++k) {
         const int j = (k + 1) % 3, l = (k + 2) % 3;
         const double H = RTX_CULL_DMAX * (T->n1E2 - fabs(T->E2[k]));
+        const double Q = sb[j] * fabs(T->E1[l]) + sb[l] * fabs(T->E1[j]);
         sumE1H += fabs(T->E1[k]) * H;
         sumSH += sb[k] * H;
-        sumQ += sb[j] * fabs(T->E1[l]) + sb[l] * fabs(T->E1[j]);
+        sumQ += Q;
+        sumE2Q += fabs(T->E2[k]) * Q;
     }
-    const double g5 = rtx_cull_gamma(5), U = RTX_CULL_U;
-    const double ep = g5 * (sumSH + (1 + 4 * U) * sumE1H);            /* |w . (d x E2)| */
+    const double g5 = rtx_cull_gamma(5), U = RTX_CULL_U, dlo = 1.0 - 0x1p-20;
+    const double Ea = g5 * sumE1H;                                      /* |a~ - a| */
+    const double Et = g5 * sumE2Q;                                      /* |tau~ - tau| */
+    const double ep = g5 * (sumSH + (1 + 4 * U) * sumE1H);             /* |w . (d x E2)| */
     const double eg = g5 * ((1 + 4 * U) * sumE1H + RTX_CULL_DMAX * sumQ);   /* |w . (d x E1)| */
-    return (ep * T->lE1 + eg * T->lE2) / T->lN * (1.0 + 1e-9) / (1.0 - 0x1p-20);
+    const double omega = (ep * T->lE1 + eg * T->lE2) / T->lN * (1.0 + 1e-9) / dlo;
+    if (!(dist > omega)) return b;
+    const double c = (dist - omega) / R * (1.0 - 1e-12);               /* |cos| of d to the plane, lower bound */
+    b.margin = (omega + omega * R / (dist - omega)) * (1.0 + 1e-9);
+    const double Btp = Bt * (1.0 + 3 * U);
+    b.dt = (2.01 * U * Bt + (Et + Btp * Ea) / (T->lN * dlo * c) + omega / (dlo * c * c)) * (1.0 + 1e-9);
+    return b;
 }
 
 RTX_CULL_HD static inline double rtx_cull_W(double omega, double dist, double R) {
@@ -114,8 +138,8 @@ RTX_CULL_HD static inline double rtx_cull_W(double omega, double dist, double R)
     return (omega + omega * R / (dist - omega)) * (1.0 + 1e-9);
 }
 
-/* Camera rays: every ray whose origin is exactly o (any direction). */
-RTX_CULL_HD static inline double rtx_cull_margin_point(const rtx_cull_tri* T, const float* o) {
+/* Camera rays: every ray whose origin is exactly o (any direction); dt for t~ <= Bt. */
+RTX_CULL_HD static inline rtx_cull_bound rtx_cull_point_bounds(const rtx_cull_tri* T, const float* o, double Bt) {
     double sb[3], s2 = 0.0, sd = 0.0;
     for (int k = 0; k < 3; ++k) {
         const float sf = o[k] - (float)T->v0[k];   /* fl(o - v0): the test's own s~ */
@@ -126,13 +150,17 @@ RTX_CULL_HD static inline double rtx_cull_margin_point(const rtx_cull_tri* T, co
     const double sn = sqrt(s2) * (1.0 + 1e-12);
     const double dist = fabs(sd) * (1.0 - 1e-12) - sn * T->nerr;
     const double R = (sn + (1.0 + 8 * RTX_CULL_U) * T->lmax) * (1.0 + 1e-12);
-    const double W = rtx_cull_W(rtx_cull_omega(T, sb), dist, R);
-    return (W + 12 * RTX_CULL_U * T->lmax + RTX_CULL_U * sn) * (1.0 + 1e-9);
+    rtx_cull_bound b = rtx_cull_bounds(T, sb, dist, R, Bt);
+    b.margin = (b.margin + 12 * RTX_CULL_U * T->lmax + RTX_CULL_U * sn + 0x1p-100) * (1.0 + 1e-9);
+    return b;
+}
+RTX_CULL_HD static inline double rtx_cull_margin_point(const rtx_cull_tri* T, const float* o) {
+    return rtx_cull_point_bounds(T, o, 0.0).margin;
 }
 
 /* Shadow rays toward a light at L (origin o, direction fl(fl(L - o) / fl(|fl(L - o)|)),
-   Renderer.cpp:130-136) whose tmax = |fl(L - o)| is at most T. */
-RTX_CULL_HD static inline double rtx_cull_margin_light(const rtx_cull_tri* T, const float* L, double Tmax) {
+   Renderer.cpp:130-136) whose tmax = |fl(L - o)| is at most Tmax; dt for t~ <= Tmax. */
+RTX_CULL_HD static inline rtx_cull_bound rtx_cull_light_bounds(const rtx_cull_tri* T, const float* L, double Tmax) {
     const double U = RTX_CULL_U, tp = Tmax * (1.0 + 8 * U);
     double sb[3], s2 = 0.0, lv2 = 0.0, ld = 0.0;
     for (int k = 0; k < 3; ++k) {
@@ -146,8 +174,12 @@ RTX_CULL_HD static inline double rtx_cull_margin_light(const rtx_cull_tri* T, co
     const double eL = 1.01 * rtx_cull_gamma(3) * tp + U * sn;
     const double dist = fabs(ld) * (1.0 - 1e-12) - lvn * T->nerr - eL;
     const double R = (lvn + (1.0 + 8 * U) * T->lmax + eL) * (1.0 + 1e-12);
-    const double W = rtx_cull_W(rtx_cull_omega(T, sb), dist, R);
-    return (W + 12 * U * T->lmax + U * sn) * (1.0 + 1e-9);
+    rtx_cull_bound b = rtx_cull_bounds(T, sb, dist, R, Tmax);
+    b.margin = (b.margin + 12 * U * T->lmax + U * sn + 0x1p-100) * (1.0 + 1e-9);
+    return b;
+}
+RTX_CULL_HD static inline double rtx_cull_margin_light(const rtx_cull_tri* T, const float* L, double Tmax) {
+    return rtx_cull_light_bounds(T, L, Tmax).margin;
 }
 
 #endif /* RTX_CULL_H */

@@ -366,30 +366,53 @@ __device__ __forceinline__ unsigned long long slab_mask(const float4 a, const fl
 }
 
 // Exact cull (rtx_cull.h): a node the reference's slab test passes is skipped for
-// a lane whose LINE misses the node's tight box widened by the margin rtx_cull.h proves for the
-// ray's anchor (view camera / light) — no triangle below can then pass HitTest_Triangle for that
-// ray, so the visit would change nothing.  Record per node slot (same byte offset as the node):
-// {c.x, c.y, c.z, E.x}, {E.y, E.z, -, -}, box = c +- E (E includes the margin and the padding
-// 16u (E + |c|) that covers this test's own rounding).  `k` = 16u |o| |inv| per axis covers the
-// rounding of (c - o) * inv, or +inf for a lane outside the bound's domain (it then always
-// passes).  Lanes of a FAST batch only (finite non-zero inverse directions, |inv| <= 2^64).
-// NaN-safe: max/min ignore a NaN operand, so a NaN term drops its axis (never culls wrongly).
+// a lane when no triangle below can pass HitTest_Triangle for its ray in a way that matters, so
+// the visit would change nothing:
+//   * the ray's LINE misses the node's tight box widened by the margin rtx_cull.h proves for the
+//     ray's anchor (view camera / light): no triangle below can be accepted at all;
+//   * closest hit: the line enters that box at n with n - dt > sc_t (dt: rtx_cull.h's bound on
+//     |t~ - t*| for t~ <= the anchor's bt, valid while sc_t <= bt): every triangle below that
+//     could be accepted has t~ > sc_t, so none replaces the scratch hit (strict <);
+//   * shadow ray: n - dt > tmax or f + dt < tmin (f: where the line leaves the box): no accepted
+//     t~ lies in [tmin, tmax).
+// Record per node slot (same byte offset as the node): {c.x, c.y, c.z, E.x}, {E.y, E.z, dt, flag},
+// box = c +- E (E includes the margin and the padding 16u (E + |c|) that covers this test's own
+// rounding, so n is at most and f at least the exact entry and exit of the widened box; rounding
+// of n - dt etc. is monotone, so each float comparison implies the exact one).  `k` = 16u |o| |inv|
+// per axis covers the rounding of (c - o) * inv, or +inf for a lane outside the bound's domain
+// (n = -inf, f = +inf: it passes every test).  Lanes of a FAST batch only (finite non-zero inverse
+// directions, |inv| <= 2^64).  NaN-safe: max/min ignore a NaN operand (its axis is dropped) and a
+// NaN comparison never culls.
 struct CullRay {
     const float4* base;   // the anchor's records (null: no cull)
     float kx, ky, kz;
+    float bt;             // the anchor's t bound for dt (closest hit: prune only while sc_t <= bt)
 };
-__device__ __forceinline__ unsigned long long cull_mask(const float4 a, const float4 b, const Ray& r, const CullRay& q) {
+__device__ __forceinline__ void cull_nf(const float4 a, const float4 b, const Ray& r, const CullRay& q, float& n,
+                                        float& f) {
     const float tx = (a.x - r.ox) * r.ix, ty = (a.y - r.oy) * r.iy, tz = (a.z - r.oz) * r.iz;
     const float hx = fmaf(a.w, fabsf(r.ix), q.kx), hy = fmaf(b.x, fabsf(r.iy), q.ky), hz = fmaf(b.y, fabsf(r.iz), q.kz);
-    const float n = fmaxf(fmaxf(tx - hx, ty - hy), tz - hz);
-    const float f = fminf(fminf(tx + hx, ty + hy), tz + hz);
-    return ballot(!(n > f));
+    n = fmaxf(fmaxf(tx - hx, ty - hy), tz - hz);
+    f = fminf(fminf(tx + hx, ty + hy), tz + hz);
+}
+// lanes that still have to enter the node whose record is (a, b); n: the entry (child ordering)
+template <bool ANY>
+__device__ __forceinline__ unsigned long long cull_pass(const float4 a, const float4 b, const Ray& r, const CullRay& q,
+                                                        float sc_t, float& n) {
+    float f;
+    cull_nf(a, b, r, q, n, f);
+    const float dt = b.z;
+    bool keep = !(n > f);
+    if (ANY) keep = keep & !(n - dt > r.tmax) & !(f + dt < r.tmin);
+    else keep = keep & !((sc_t <= q.bt) & (n - dt > sc_t));
+    return ballot(keep);
 }
 // 16u |o_k| |inv_k| per axis, or +inf (always pass) for a lane outside the bound's domain:
 // |o_k| <= 2^40, |inv_k| <= 2^64 and `ok` (the caller's conditions on the direction and tmax)
-__device__ __forceinline__ CullRay cull_ray(const float4* base, const Ray& r, bool ok) {
+__device__ __forceinline__ CullRay cull_ray(const float4* base, const Ray& r, bool ok, float bt) {
     CullRay q;
     q.base = base;
+    q.bt = bt;
     ok = ok && fabsf(r.ox) <= 0x1p40f && fabsf(r.oy) <= 0x1p40f && fabsf(r.oz) <= 0x1p40f &&
          fabsf(r.ix) <= 0x1p64f && fabsf(r.iy) <= 0x1p64f && fabsf(r.iz) <= 0x1p64f;
     constexpr float k16u = 0x1p-20f;
@@ -586,13 +609,19 @@ __device__ __forceinline__ void touch_wait(uint32_t a, uint32_t b) {
 // VGPR boolean or a lane-mask flow variable), a dead end leaves it as an empty "leaf", and
 // the pop loop is the only other path.  Same visits, tests and order as bvh_walk.
 // `nb` is the node copy the slab form reads (the octant's (near, far) copy for kSlabOct).
-// CULL: a child is entered only by the lanes whose line also meets its cull box (cull_mask).
+// CULL: a child is entered only by the lanes cull_pass keeps, and a closest-hit walk is ORDERED:
+// the child most lanes enter first is walked first, and the scratch hit is replaced by t < sc_t or,
+// on a tie, by the lower triangle index — the reference's first-found winner whatever the visiting
+// order, because left-then-right DFS order is increasing triangle index (the scene has the cull
+// only when that holds, upload_scene; the split launches' key minimum rests on the same fact) — so
+// nearer subtrees lower sc_t before farther ones are tested and cull_pass prunes those.
 template <bool ANY, int SLAB, bool CB = false, bool CULL = false>
 __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, const Ray& r, uint32_t link,
                               uint32_t ntri, unsigned long long m, unsigned long long mask, uint32_t lane, uint4* stk,
                               float& sc_t, uint32_t& sc_tri, unsigned long long& live, const uint32_t* occ_word,
                               uint32_t occ_bit, const CullRay& cq = CullRay{}) {
     constexpr bool FAST = SLAB != kSlabExact;
+    constexpr bool ORD = CULL && !ANY;
     uint32_t sp = 0;
     [[maybe_unused]] uint32_t pf0 = 0, pf1 = 0;
     for (;;) {
@@ -609,15 +638,29 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
 #endif
             unsigned long long ml = slab_mask<SLAB>(P.l0, P.l1, r) & m;
             unsigned long long mr = slab_mask<SLAB>(P.r0, P.r1, r) & m;
+            [[maybe_unused]] bool rfirst = false;
             if (CULL) {
                 NodePair Q;
                 ldcb64(cq.base, link, Q.l0, Q.l1, Q.r0, Q.r1);
                 // only pairs whose records are flagged worth testing (cull_write), and only when
                 // some lane entered a child
                 if ((__float_as_uint(Q.l1.w) | __float_as_uint(Q.r1.w)) && (ml | mr)) {
-                    ml &= cull_mask(Q.l0, Q.l1, r, cq);
-                    mr &= cull_mask(Q.r0, Q.r1, r, cq);
+                    float nl, nr;
+                    ml &= cull_pass<ANY>(Q.l0, Q.l1, r, cq, sc_t, nl);
+                    mr &= cull_pass<ANY>(Q.r0, Q.r1, r, cq, sc_t, nr);
+                    if (ORD) {   // right first when most lanes that enter both enter it first
+                        const unsigned long long both_m = ml & mr;
+                        rfirst = 2 * __popcll(ballot(nr < nl) & both_m) > __popcll(both_m);
+                    }
                 }
+            }
+            if (ORD && rfirst) {   // walk the right child first: swap the pair's roles
+                const unsigned long long t0 = ml;
+                ml = mr;
+                mr = t0;
+                const float4 t1 = P.l1;
+                P.l1 = P.r1;
+                P.r1 = t1;
             }
 #if RTX_ASM_SELECT
             // next (link, ntri): left, else right, else a dead end taken as an empty leaf
@@ -675,7 +718,8 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                 if (ANY) {
                     live &= ~(ballot(!(rej > 0.f)) & ballot(!(t >= r.tmax)) & m);
                 } else {
-                    const bool u = in & !(rej > 0.f) & !(t >= r.tmax) & (t < sc_t);
+                    const bool better = ORD ? ((t < sc_t) | ((t == sc_t) & (ti < sc_tri))) : (t < sc_t);
+                    const bool u = in & !(rej > 0.f) & !(t >= r.tmax) & better;
                     sc_t = u ? t : sc_t;
                     sc_tri = u ? ti : sc_tri;
                 }
@@ -722,7 +766,8 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
     if (CULL && m) {
         float4 c0, c1;
         ldcb32(cq.base, static_cast<uint32_t>(M.x), c0, c1);
-        if (__float_as_uint(c1.w)) m &= cull_mask(c0, c1, r, cq);
+        float n;
+        if (__float_as_uint(c1.w)) m &= cull_pass<ANY>(c0, c1, r, cq, sc_t, n);
     }
     if (m == 0) return;
     if (RTX_LEAN_WALK && !COUNT && !RTX_STAMPS_WALK)
@@ -761,7 +806,8 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int
     if (CULL && m) {
         float4 q0, q1;
         ldcb32(cq.base, static_cast<uint32_t>(M.x), q0, q1);
-        if (__float_as_uint(q1.w)) m &= cull_mask(q0, q1, r, cq);
+        float n;
+        if (__float_as_uint(q1.w)) m &= cull_pass<ANY>(q0, q1, r, cq, sc_t, n);
     }
     uint32_t link = __float_as_uint(b1.z), ntri = __float_as_uint(b1.w);
     const uint32_t path = static_cast<uint32_t>(E.z);
@@ -774,7 +820,8 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int
         if (CULL) {
             float4 q0, q1;
             ldcb32(cq.base, link + (right ? 32u : 0u), q0, q1);
-            if (__float_as_uint(q1.w)) m &= cull_mask(q0, q1, r, cq);
+            float n;
+            if (__float_as_uint(q1.w)) m &= cull_pass<ANY>(q0, q1, r, cq, sc_t, n);
         }
         link = __float_as_uint(c1.z);
         ntri = __float_as_uint(c1.w);
@@ -1061,7 +1108,8 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
     const bool pcull = kCull && S.cull_stride && fast && (PHASE == 0 || PHASE == 1);
     CullRay pq{};
     if (pcull)
-        pq = cull_ray(S.cull + static_cast<size_t>(uni(view)) * (S.cull_stride / 16u), vr, dm >= 0x1p-30f);
+        pq = cull_ray(S.cull + static_cast<size_t>(uni(view)) * (S.cull_stride / 16u), vr, dm >= 0x1p-30f,
+                      F.cam[uni(view)].cull_bt);
 
     // ---- Scene::GetClosestHit (Scene.cpp:29-66)
     float best_t = FLT_MAX, sc_t = FLT_MAX;
@@ -1240,7 +1288,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                 CullRay sq{};
                 if (scull)
                     sq = cull_ray(S.cull + static_cast<size_t>(kMaxViews + li) * (S.cull_stride / 16u), sr,
-                                  mag >= 0x1p-30f && mag <= ldc(S.cull_T, li));
+                                  mag >= 0x1p-30f && mag <= ldc(S.cull_T, li), ldc(S.cull_T, li));
                 if (COUNT && did) cnt.c[kShadow]++;
                 // (single-condition loops with a separate exit test: a `&& live` loop
                 // condition is carried as a VGPR boolean by the compiler)
@@ -1493,6 +1541,7 @@ __global__ void __launch_bounds__(256) rtx_octant_expand(float4* __restrict__ no
 // record then always passes: the bound's finite-arithmetic domain, rtx_cull.h).
 struct CullAnchors {
     float p[kMaxViews + kMaxCullLights][4];   // xyz: the anchor point; w = 0: camera origin, > 0: light with tmax <= w
+    float bt[kMaxViews + kMaxCullLights];     // the t bound of the records' dt (lights: = w)
     uint32_t idx[kMaxViews + kMaxCullLights]; // record copy the anchor writes
     uint32_t n;
 };
@@ -1538,8 +1587,10 @@ __global__ void __launch_bounds__(256) rtx_cull_tri_margin(const Tri* __restrict
     rtx_cull_tri T;
     rtx_cull_tri_setup(&T, v0, e1, e2);
     const float* p = A.p[j];
-    const double m = p[3] > 0.f ? rtx_cull_margin_light(&T, p, p[3]) : rtx_cull_margin_point(&T, p);
-    marg[static_cast<size_t>(j) * n + i] = (m >= 0.0 && m < 0x1p100) ? f_ru(m) : INFINITY;   // NaN -> inf
+    const rtx_cull_bound bd = p[3] > 0.f ? rtx_cull_light_bounds(&T, p, p[3]) : rtx_cull_point_bounds(&T, p, A.bt[j]);
+    // NaN -> inf; (margin, dt) of anchor j for triangle i
+    marg[2 * (static_cast<size_t>(j) * n + i)] = (bd.margin >= 0.0 && bd.margin < 0x1p100) ? f_ru(bd.margin) : INFINITY;
+    marg[2 * (static_cast<size_t>(j) * n + i) + 1] = (bd.dt >= 0.0 && bd.dt < 0x1p100) ? f_ru(bd.dt) : INFINITY;
 }
 
 // Which records the walk tests (CullParams): a box some axis of which the reference's box (node
@@ -1553,7 +1604,8 @@ struct CullParams {
 // the record of `slot` for anchor copy `a`: tight box [lo, hi] widened by `m` and the padding
 // 16u (E + |c|) of cull_mask's rounding (2^-20 = 16u); w of its second half = the test flag
 __device__ __forceinline__ void cull_write(float4* __restrict__ cull, uint32_t stride4, uint32_t a, uint32_t slot,
-                                           const float* lo, const float* hi, bool bad, float m, const CullParams& P) {
+                                           const float* lo, const float* hi, bool bad, float m, float dt,
+                                           const CullParams& P) {
     float cf[3], Ef[3];
     for (int k = 0; k < 3; ++k) {
         const double c = 0.5 * (static_cast<double>(lo[k]) + hi[k]);
@@ -1571,7 +1623,7 @@ __device__ __forceinline__ void cull_write(float4* __restrict__ cull, uint32_t s
     if (P.leaves && __float_as_uint(n1.w) == 0u) worth = false;
     float4* r = cull + static_cast<size_t>(a) * stride4 + 2u * slot;
     r[0] = make_float4(cf[0], cf[1], cf[2], Ef[0]);
-    r[1] = make_float4(Ef[1], Ef[2], 0.f, __uint_as_float(worth ? 1u : 0u));
+    r[1] = make_float4(Ef[1], Ef[2], (bad || !(dt < 0x1p100f)) ? INFINITY : dt, __uint_as_float(worth ? 1u : 0u));
 }
 
 // node slots whose triangle range holds at most kCullBigTris triangles, one thread each
@@ -1592,12 +1644,13 @@ __global__ void __launch_bounds__(256) rtx_cull_nodes_small(const uint2* __restr
         hi[0] = fmaxf(hi[0], h.x); hi[1] = fmaxf(hi[1], h.y); hi[2] = fmaxf(hi[2], h.z);
     }
     for (uint32_t j = 0; j < A.n; ++j) {
-        float m = 0.f;
+        float m = 0.f, dt = 0.f;
         for (uint32_t t = r.x; !bad && t < r.y; ++t) {
-            const float x = marg[static_cast<size_t>(j) * ntris + t];
-            m = (x > m || x != x) ? x : m;   // NaN sticks (then +inf below)
+            const float x = marg[2 * (static_cast<size_t>(j) * ntris + t)], y = marg[2 * (static_cast<size_t>(j) * ntris + t) + 1];
+            m = (x > m || x != x) ? x : m;   // NaN sticks (then +inf)
+            dt = (y > dt || y != y) ? y : dt;
         }
-        cull_write(cull, stride4, A.idx[j], s, lo, hi, bad, m, P);
+        cull_write(cull, stride4, A.idx[j], s, lo, hi, bad, m, dt, P);
     }
 }
 
@@ -1629,16 +1682,18 @@ __global__ void __launch_bounds__(64) rtx_cull_nodes_big(const uint32_t* __restr
     const bool bad = __builtin_amdgcn_ballot_w64(badl != 0u) != 0ull;
     for (int k = 0; k < 3; ++k) { lo[k] = wave_min(lo[k]); hi[k] = wave_max(hi[k]); }
     for (uint32_t j = 0; j < A.n; ++j) {
-        float m = 0.f;
+        float m = 0.f, dt = 0.f;
         uint32_t nanl = 0u;
         for (uint32_t t = r.x + lane; !empty && t < r.y; t += 64u) {
-            const float x = marg[static_cast<size_t>(j) * ntris + t];
-            nanl |= x != x ? 1u : 0u;
+            const float x = marg[2 * (static_cast<size_t>(j) * ntris + t)], y = marg[2 * (static_cast<size_t>(j) * ntris + t) + 1];
+            nanl |= (x != x || y != y) ? 1u : 0u;
             m = fmaxf(m, x);
+            dt = fmaxf(dt, y);
         }
         m = wave_max(m);
-        if (__builtin_amdgcn_ballot_w64(nanl != 0u)) m = INFINITY;
-        if (lane == 0) cull_write(cull, stride4, A.idx[j], s, lo, hi, bad, m, P);
+        dt = wave_max(dt);
+        if (__builtin_amdgcn_ballot_w64(nanl != 0u)) m = dt = INFINITY;
+        if (lane == 0) cull_write(cull, stride4, A.idx[j], s, lo, hi, bad, m, dt, P);
     }
 }
 
@@ -1951,6 +2006,7 @@ struct rtx_ctx {
     uint32_t cull_nslots = 0, cull_nbig = 0, cull_ntris = 0;
     float cull_view[kMaxViews][3] = {};   // camera origin each view's records of the current image were made for
     uint32_t cull_view_valid = 0;         // bit v: view v's records are current
+    double cull_bmin[3] = {}, cull_bmax[3] = {};   // the meshes' box (a camera anchor's t bound, cull_bt)
     uint64_t cull_updates = 0;            // camera-anchor record launches so far (rtx_cull_info)
     rtx_render_params last{};
     int last_views = 1;
@@ -2209,7 +2265,7 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay);
 // sync: queued launches may still read the old buffers).
 int cull_launch(rtx_ctx* c, const CullAnchors& A, bool boxes) {
     const uint32_t nt = c->cull_ntris;
-    const size_t marg_need = static_cast<size_t>(kMaxViews > kMaxCullLights ? kMaxViews : kMaxCullLights) * nt;
+    const size_t marg_need = 2 * static_cast<size_t>(kMaxViews > kMaxCullLights ? kMaxViews : kMaxCullLights) * nt;
     if (2 * static_cast<size_t>(nt) > c->cull_box_cap || marg_need > c->cull_marg_cap) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         (void)hipFree(c->d_cull_box);
@@ -2250,6 +2306,7 @@ int cull_records(rtx_ctx* c, const std::vector<float>& T, const rtx_light* light
     for (uint32_t l = 0; l < n_lights; ++l) {
         for (int k = 0; k < 3; ++k) A.p[A.n][k] = lights[l].origin[k];
         A.p[A.n][3] = T[l] > 0.f ? T[l] : 1.f;   // T = 0: never culled (cull_ray), any bound will do
+        A.bt[A.n] = A.p[A.n][3];
         A.idx[A.n] = static_cast<uint32_t>(kMaxViews) + l;
         ++A.n;
     }
@@ -2267,6 +2324,7 @@ int cull_views(rtx_ctx* c, const FrameArgs& F) {
         c->cull_view_valid |= 1u << v;
         for (int k = 0; k < 3; ++k) A.p[A.n][k] = o[k];
         A.p[A.n][3] = 0.f;
+        A.bt[A.n] = F.cam[v].cull_bt;
         A.idx[A.n] = v;
         ++A.n;
     }
@@ -2429,6 +2487,7 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         cull_rng.assign(nodes.size() / 2, make_uint2(0u, 0u));
         std::vector<float> nb(6 * (nodes.size() / 2));
         double sa_ref = 0.0, sa_tight = 0.0;
+        bool increasing = true;
         auto sa = [](double x, double y, double z) { return 2.0 * (x * y + y * z + z * x); };
         for (const auto& [r0, r1] : mesh_slots)
             for (uint32_t sl = r1; sl-- > r0;) {
@@ -2445,6 +2504,8 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
                             b[2 * a + 1] = std::fmax(b[2 * a + 1], tbox[6 * t + 2 * a + 1]);
                         }
                 } else {
+                    // the ordered walk needs left-then-right DFS order = increasing triangle index
+                    increasing = increasing && cull_rng[link].y <= cull_rng[link + 1].x;
                     cull_rng[sl] = make_uint2(std::min(cull_rng[link].x, cull_rng[link + 1].x),
                                               std::max(cull_rng[link].y, cull_rng[link + 1].y));
                     for (int a = 0; a < 3; ++a) {
@@ -2458,7 +2519,7 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
                 sa_tight += sa(std::fmax(double(b[1]) - b[0], 0.0), std::fmax(double(b[3]) - b[2], 0.0),
                                std::fmax(double(b[5]) - b[4], 0.0));
             }
-        cull_on = sa_ref >= c->cull_min_sa * sa_tight;   // false for NaN
+        cull_on = increasing && sa_ref >= c->cull_min_sa * sa_tight;   // false for NaN
         for (uint32_t i = 0; i < s->n_lights; ++i) {
             double R = 0.0;
             for (int k = 0; k < 8; ++k) {
@@ -2615,6 +2676,7 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         c->cull_rng = reinterpret_cast<const uint2*>(base + secs[9].off);
         c->cull_big = reinterpret_cast<const uint32_t*>(base + secs[10].off);
         c->cull_nslots = d.n_nodes;
+        for (int a = 0; a < 3; ++a) { c->cull_bmin[a] = bmin[a]; c->cull_bmax[a] = bmax[a]; }
         c->cull_nbig = static_cast<uint32_t>(cull_big.size());
         c->cull_ntris = d.n_tris;
     }
@@ -2718,6 +2780,18 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
             F.cam[v].up[k] = cams[v].up[k]; F.cam[v].forward[k] = cams[v].forward[k];
         }
         F.cam[v].fov = cams[v].fov;
+        // the camera anchor's t bound (CullRay::bt): 4x the farthest corner of the meshes' box + 1
+        if (c->dev.cull_stride) {
+            double R = 0.0;
+            for (int k = 0; k < 8; ++k) {
+                const double dx = cams[v].origin[0] - ((k & 1) ? c->cull_bmax[0] : c->cull_bmin[0]);
+                const double dy = cams[v].origin[1] - ((k & 2) ? c->cull_bmax[1] : c->cull_bmin[1]);
+                const double dz = cams[v].origin[2] - ((k & 4) ? c->cull_bmax[2] : c->cull_bmin[2]);
+                R = std::fmax(R, std::sqrt(dx * dx + dy * dy + dz * dz));
+            }
+            const double bt = 4.0 * R + 1.0;
+            F.cam[v].cull_bt = std::isfinite(bt) && bt < 0x1p60 ? static_cast<float>(bt) : 0.f;   // 0: no pruning
+        }
         if (c->scene_spec & kSpecRoomPlanes) {   // the room planes' camera numerators (ViewCam)
             bool ok = true;
             for (int k = 0; k < 5; ++k) {

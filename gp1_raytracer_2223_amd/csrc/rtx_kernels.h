@@ -149,7 +149,7 @@ struct ViewCam {
     // whether all five are 0 or in [2^-60, 2^60] (div_rn's numerator domain, rtx_fastdiv.h)
     float room_a[5];
     uint32_t room_fast;
-    float _pad[1];
+    float cull_bt;    // the view's camera-anchor cull records: their t bound (CullRay::bt)
 };
 
 struct FrameArgs {

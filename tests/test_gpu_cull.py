@@ -191,3 +191,31 @@ def test_cull_records_follow_the_camera(cull_ctx):
     c.origin[2] = cam.origin[2] - 0.5
     cull_ctx.render(c, p)
     assert cull_ctx.cull_info()[1] == n0 + 2
+
+
+def test_cull_ordered_walk_ties(cull_ctx, plain_ctx, tmp_path):
+    """The ordered walk replaces the scratch hit on a tie of t only by a LOWER triangle index —
+    the reference's first-found winner.  A mesh whose every face appears twice (the copy right
+    after the original, so both land in one leaf or in neighbouring subtrees) makes every hit a
+    tie between two triangles; the frames must equal the unculled walk's and the oracle's."""
+    rng = np.random.default_rng(7)
+    n = 24
+    lines = []
+    for j in range(n + 1):
+        for i in range(n + 1):
+            lines.append(f"v {-2 + 4 * i / n:.6f} {0.2 + 0.6 * rng.random():.6f} {-1 + 3 * j / n:.6f}")
+    for j in range(n):
+        for i in range(n):
+            a, b, c, d = j * (n + 1) + i + 1, j * (n + 1) + i + 2, (j + 1) * (n + 1) + i + 1, (j + 1) * (n + 1) + i + 2
+            for tri in ((a, c, b), (b, c, d)):
+                lines.append("f %d %d %d" % tri)
+                lines.append("f %d %d %d" % tri)   # the duplicate
+    (tmp_path / "dup_grid.obj").write_text("\n".join(lines) + "\n")
+    scene = tmp_path / "dup.rtxscene"
+    scene.write_text("camera 0 3 -7 45\nmaterial lambert 1 1 1 1\nmaterial lambert 0.49 0.57 0.57 1\n"
+                     "mesh dup_grid 1 back\nplane 0 0 0 0 1 0 2\nlight point 0 5 -2 50 1 0.61 0.45\n"
+                     "light point -3 4 1 40 1 0.8 0.45\n")
+    hs = HostScene(f"file:{scene}", asset_dir=str(tmp_path))
+    s, cam = hs.view()
+    for mode in (3, 0):
+        _check(cull_ctx, plain_ctx, s, cam, abi.make_params(256, 192, mode, 1), f"dup/m{mode}", True)

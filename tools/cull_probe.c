@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include "rtx.h"
+#include "../gp1_raytracer_2223_amd/csrc/rtx_cull.h"
 
 typedef struct { float x, y, z; } v3;
 static inline v3 mk(float x, float y, float z) { v3 r = {x, y, z}; return r; }
@@ -196,6 +197,7 @@ typedef struct {
     const rtx_mesh* m;
     double* tmn; double* tmx;   /* tight boxes per node (3 each) */
     double* marg;               /* per node margin (camera), or NULL */
+    double* mdt;                /* per node t bound (camera, t~ <= 64), or NULL */
     double* lmarg;              /* per node x grid margins for the current light, or NULL */
     double delta;
     int use_tight;
@@ -237,6 +239,7 @@ static void margin_rec(walk* w, uint32_t ni, const float* cam, const float* L) {
     const rtx_bvh_node* nd = &w->m->nodes[ni];
     if (nd->idx_count > 0) {
         if (cam) w->marg[ni] = 0;
+        if (cam && w->mdt) w->mdt[ni] = 0;
         if (L) for (int j = 0; j < NGRID; ++j) w->lmarg[(size_t)ni * NGRID + j] = 0;
         for (uint32_t i = 0; i < nd->idx_count; i += 3) {
             tri_info T;
@@ -246,6 +249,17 @@ static void margin_rec(walk* w, uint32_t ni, const float* cam, const float* L) {
             if (cam) {
                 const double g = tri_margin_camera(&T, cam);
                 if (!(g <= w->marg[ni])) w->marg[ni] = g;
+                if (w->mdt) {
+                    rtx_cull_tri Tc;
+                    const float* p0 = &w->m->positions[3 * w->m->indices[nd->first_idx + i]];
+                    const float* p1 = &w->m->positions[3 * w->m->indices[nd->first_idx + i + 1]];
+                    const float* p2 = &w->m->positions[3 * w->m->indices[nd->first_idx + i + 2]];
+                    const float e1[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+                    const float e2[3] = {p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2]};
+                    rtx_cull_tri_setup(&Tc, p0, e1, e2);
+                    const double dt = rtx_cull_point_bounds(&Tc, cam, 64.0).dt;
+                    if (!(dt <= w->mdt[ni])) w->mdt[ni] = dt;
+                }
             }
             if (L)
                 for (int j = 0; j < NGRID; ++j) {
@@ -259,6 +273,7 @@ static void margin_rec(walk* w, uint32_t ni, const float* cam, const float* L) {
         margin_rec(w, nd->left_node + 1, cam, L);
         const uint32_t a = nd->left_node, b = nd->left_node + 1;
         if (cam) w->marg[ni] = fmax(w->marg[a], w->marg[b]);
+        if (cam && w->mdt) w->mdt[ni] = (w->mdt[a] >= w->mdt[b] || w->mdt[a] != w->mdt[a]) ? w->mdt[a] : w->mdt[b];
         if (L)
             for (int j = 0; j < NGRID; ++j)
                 w->lmarg[(size_t)ni * NGRID + j] =
@@ -277,6 +292,28 @@ static double node_margin(const walk* w, uint32_t ni, const ray* r, int shadow) 
     return w->lmarg[(size_t)ni * NGRID + j];
 }
 
+/* entry parameter of the line into box [mn - dl, mx + dl] (+inf: misses) */
+static double enter_t(const double* mn, const double* mx, double dl, const ray* r) {
+    const double o[3] = {r->o.x, r->o.y, r->o.z}, d[3] = {r->d.x, r->d.y, r->d.z};
+    double t0 = -INFINITY, t1 = INFINITY;
+    for (int k = 0; k < 3; ++k) {
+        const double lo = mn[k] - dl, hi = mx[k] + dl;
+        if (d[k] == 0.0) {
+            if (o[k] < lo || o[k] > hi) return INFINITY;
+            continue;
+        }
+        double a = (lo - o[k]) / d[k], b = (hi - o[k]) / d[k];
+        if (a > b) { const double x = a; a = b; b = x; }
+        if (a > t0) t0 = a;
+        if (b < t1) t1 = b;
+        if (t0 > t1) return INFINITY;
+    }
+    return t0;
+}
+static int g_ordered = 0;     /* 1: nearest child first + t pruning (closest-hit), 2: also shadow rays ordered */
+static double g_tslack = 1e-3;
+void cull_probe_ordered(int o, double slack) { g_ordered = o; g_tslack = slack; }
+
 static void visit(walk* w, uint32_t ni, const ray* r, int ignore, int* did, float* bt, int* bi) {
     if (ignore && *did) return;
     const rtx_bvh_node* nd = &w->m->nodes[ni];
@@ -285,6 +322,10 @@ static void visit(walk* w, uint32_t ni, const ray* r, int ignore, int* did, floa
     if (w->use_tight) {
         const double g = node_margin(w, ni, r, ignore);
         if (isfinite(g) && !meets(w->tmn + 3 * ni, w->tmx + 3 * ni, g, r)) return;
+        const double slack = (g_tslack < 0 && w->mdt) ? w->mdt[ni] : g_tslack;
+        if (g_ordered && !ignore && isfinite(g) && *bt < 64.f && isfinite(slack) &&
+            enter_t(w->tmn + 3 * ni, w->tmx + 3 * ni, g, r) - slack > *bt)
+            return;   /* every triangle below would give t > best */
     }
     if (nd->idx_count > 0) {
         for (uint32_t i = 0; i < nd->idx_count; i += 3) {
@@ -299,12 +340,19 @@ static void visit(walk* w, uint32_t ni, const ray* r, int ignore, int* did, floa
             if (tri(v0, v1, v2, n, m->cull_mode, r, ignore, &t)) {
                 *did = 1;
                 if (ignore) return;
-                if (t < *bt) { *bt = t; *bi = li; }
+                if (t < *bt || (t == *bt && li < *bi)) { *bt = t; *bi = li; }
             }
         }
     } else {
-        visit(w, nd->left_node, r, ignore, did, bt, bi);
-        visit(w, nd->left_node + 1, r, ignore, did, bt, bi);
+        uint32_t a = nd->left_node, b = nd->left_node + 1;
+        if (w->use_tight && g_ordered && (!ignore || g_ordered == 2)) {
+            const double ga = node_margin(w, a, r, ignore), gb = node_margin(w, b, r, ignore);
+            const double ta = enter_t(w->tmn + 3 * a, w->tmx + 3 * a, isfinite(ga) ? ga : 0, r);
+            const double tb = enter_t(w->tmn + 3 * b, w->tmx + 3 * b, isfinite(gb) ? gb : 0, r);
+            if (tb < ta) { const uint32_t x = a; a = b; b = x; }
+        }
+        visit(w, a, r, ignore, did, bt, bi);
+        visit(w, b, r, ignore, did, bt, bi);
     }
 }
 
@@ -327,6 +375,7 @@ int cull_probe(const rtx_scene* sc, const rtx_camera* cam, uint32_t W, uint32_t 
     double* lm[16] = {0};
     if (delta < 0) {
         b.marg = (double*)malloc(sizeof(double) * m->n_nodes);
+        b.mdt = (double*)malloc(sizeof(double) * m->n_nodes);
         margin_rec(&b, 0, cam->origin, NULL);
         for (uint32_t li = 0; li < sc->n_lights; ++li) {
             lm[li] = (double*)malloc(sizeof(double) * NGRID * m->n_nodes);
@@ -377,7 +426,7 @@ int cull_probe(const rtx_scene* sc, const rtx_camera* cam, uint32_t W, uint32_t 
         }
     }
     out[0] = a.slabs; out[1] = a.tris; out[2] = b.slabs; out[3] = b.tris;
-    free(a.tmn); free(a.tmx); free(b.marg);
+    free(a.tmn); free(a.tmx); free(b.marg); free(b.mdt);
     for (int li = 0; li < 16; ++li) free(lm[li]);
     return 0;
 }

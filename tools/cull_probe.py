@@ -29,6 +29,8 @@ def main() -> None:
     deltas = [float(x) for x in sys.argv[3:]] or [-1.0, 1e-3, 1e-2, 0.1]
     L = lib()
     import os
+    if os.environ.get("ORDERED"):
+        L.cull_probe_ordered(int(os.environ["ORDERED"]), C.c_double(float(os.environ.get("TSLACK", "1e-3"))))
     if os.environ.get("FIXED_GRID"):
         L.cull_probe_fixed_grid(int(os.environ["FIXED_GRID"]))
     hs = HostScene(name)

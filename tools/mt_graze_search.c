@@ -27,6 +27,9 @@ static v3 cross(v3 a, v3 b) { return mk(a.y * b.z - a.z * b.y, -(a.x * b.z - a.z
 
 /* HitTest_Triangle with NoCulling: the |normal . d| >= FLT_EPSILON guard (Utils.h:111-112) on the
    face normal normalize(e1 x e2) as TriangleMesh computes it, then Möller–Trumbore (:139-171) */
+/* the test's intermediates for an accepted ray (mt_x) */
+typedef struct { float a, alpha, beta, t; v3 s; } mt_vals;
+static mt_vals g_last;
 static int mt(v3 v0, v3 v1, v3 v2, v3 o, v3 d, float tmin, float tmax) {
     const v3 e1 = sub(v1, v0), e2 = sub(v2, v0);
     v3 nn = cross(e1, e2);
@@ -45,7 +48,27 @@ static int mt(v3 v0, v3 v1, v3 v2, v3 o, v3 d, float tmin, float tmax) {
     if (v < 0.f || (u + v) > 1.f) return 0;
     const float t = ai * dot(e2, q);
     if (t < tmin || t >= tmax) return 0;
+    g_last.a = a; g_last.alpha = dot(s, h); g_last.beta = dot(d, q); g_last.t = t; g_last.s = s;
     return 1;
+}
+
+/* For the accepted ray of the last mt(): X = v0 + (alpha~/a~) E1 + (beta~/a~) E2, its distance to
+   the line through o' = v0 + s~ along d, and t* (the line parameter of the point nearest X). */
+static void x_check(v3 v0, v3 v1, v3 v2, v3 d, double* dist_x, double* tstar) {
+    const v3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+    const double U = (double)g_last.alpha / g_last.a, V = (double)g_last.beta / g_last.a;
+    const double X[3] = {v0.x + U * e1.x + V * e2.x, v0.y + U * e1.y + V * e2.y, v0.z + U * e1.z + V * e2.z};
+    const double O[3] = {(double)v0.x + g_last.s.x, (double)v0.y + g_last.s.y, (double)v0.z + g_last.s.z};
+    const double D[3] = {d.x, d.y, d.z};
+    const double dd = D[0] * D[0] + D[1] * D[1] + D[2] * D[2];
+    const double ts = ((X[0] - O[0]) * D[0] + (X[1] - O[1]) * D[1] + (X[2] - O[2]) * D[2]) / dd;
+    double r2 = 0;
+    for (int k = 0; k < 3; ++k) {
+        const double w = X[k] - (O[k] + ts * D[k]);
+        r2 += w * w;
+    }
+    *dist_x = sqrt(r2);
+    *tstar = ts;
 }
 
 typedef struct { double x, y, z; } d3;
@@ -129,7 +152,7 @@ int main(int argc, char** argv) {
     srand(12345);
     long acc_far[4] = {0, 0, 0, 0}, acc[4] = {0, 0, 0, 0}, viol = 0, lacc = 0, lviol = 0;
     const double Xs[4] = {0.01, 0.1, 0.5, 2.0};
-    double worst[4] = {0, 0, 0, 0}, worst_ratio = 0, worst_lratio = 0;
+    double worst[4] = {0, 0, 0, 0}, worst_ratio = 0, worst_lratio = 0, worst_dt = 0;
     for (long it = 0; it < trials; ++it) {
         /* sliver: grid triangle with a steep height step */
         const float x0 = (float)(-3.0 + 6.0 * urand()), z0 = (float)(-1.0 + 4.0 * urand());
@@ -167,6 +190,20 @@ int main(int argc, char** argv) {
                 viol++;
                 printf("VIOLATION camera: dist %.6g > margin %.6g\n", dist, mg);
             }
+            {   /* the derivation's own quantities: |X - P| <= W and |t~ - t*| <= dt */
+                const v3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+                rtx_cull_tri T;
+                rtx_cull_tri_setup(&T, &v0.x, &e1.x, &e2.x);
+                const rtx_cull_bound bd = rtx_cull_point_bounds(&T, &o.x, g_last.t);
+                double dx, ts;
+                x_check(v0, v1, v2, d, &dx, &ts);
+                if (dx > bd.margin || fabs((double)g_last.t - ts) > bd.dt) {
+                    viol++;
+                    printf("VIOLATION camera X: |X-P| %.6g (W %.6g), |t-t*| %.6g (dt %.6g)\n", dx, bd.margin,
+                           fabs((double)g_last.t - ts), bd.dt);
+                }
+                if (bd.dt > 0 && fabs((double)g_last.t - ts) / bd.dt > worst_dt) worst_dt = fabs((double)g_last.t - ts) / bd.dt;
+            }
             if (mg > 0 && dist / mg > worst_ratio) worst_ratio = dist / mg;
             if (dist > worst[k]) {
                 worst[k] = dist;
@@ -193,6 +230,20 @@ int main(int argc, char** argv) {
                 lviol++;
                 printf("VIOLATION light: dist %.6g > margin %.6g\n", dist, mg);
             }
+            {
+                const v3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+                rtx_cull_tri T;
+                rtx_cull_tri_setup(&T, &v0.x, &e1.x, &e2.x);
+                const rtx_cull_bound bd = rtx_cull_light_bounds(&T, &L.x, mag);
+                double dx, ts;
+                x_check(v0, v1, v2, l, &dx, &ts);
+                if (dx > bd.margin || fabs((double)g_last.t - ts) > bd.dt) {
+                    lviol++;
+                    printf("VIOLATION light X: |X-P| %.6g (W %.6g), |t-t*| %.6g (dt %.6g)\n", dx, bd.margin,
+                           fabs((double)g_last.t - ts), bd.dt);
+                }
+                if (bd.dt > 0 && fabs((double)g_last.t - ts) / bd.dt > worst_dt) worst_dt = fabs((double)g_last.t - ts) / bd.dt;
+            }
             if (mg > 0 && dist / mg > worst_lratio) worst_lratio = dist / mg;
         }
     }
@@ -201,5 +252,6 @@ int main(int argc, char** argv) {
                Xs[k], acc[k], acc_far[k], worst[k]);
     printf("camera: violations %ld, largest distance / margin %.4g\n", viol, worst_ratio);
     printf("shadow: accepted %ld, violations %ld, largest distance / margin %.4g\n", lacc, lviol, worst_lratio);
+    printf("t bound: largest |t~ - t*| / dt %.4g\n", worst_dt);
     return (viol || lviol) ? 1 : 0;
 }
