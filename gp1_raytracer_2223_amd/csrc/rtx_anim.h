@@ -24,21 +24,16 @@
 #include <stdint.h>
 
 #include "rtx.h"
+#include "rtx_variants.h"
 
 namespace rtxa {
 
-#ifndef RTX_ANIM_THREADS
-#define RTX_ANIM_THREADS 512
-#endif
 constexpr int kAnimThreads = RTX_ANIM_THREADS;   // threads of every build workgroup
 constexpr int kAnimWaves = kAnimThreads / 64;
 constexpr int kMaxAnimMeshes = 32;               // animated meshes per launch (their matrices travel in the kernel arguments)
 constexpr int kMaxAnimParts = 128;               // frontier entries per mesh (kPartsPerMesh)
 constexpr int kMaxTop = 256;                     // temp ids of task-split nodes and their children per mesh
 constexpr int kMaxSub = kMaxTop;                 // subtrees per mesh (each root is one of those ids)
-#ifndef RTX_ANIM_WORKERS
-#define RTX_ANIM_WORKERS 64
-#endif
 constexpr int kWorkers = RTX_ANIM_WORKERS;       // task workgroups per mesh besides (mesh, 0)
 constexpr int kOutGroups = 16;                   // workgroups per mesh of the output launch
 // The task queue of a mesh (MeshDev::q): counters, then entries {what, reserved ids, epoch, -}

@@ -85,9 +85,6 @@ __device__ __forceinline__ unsigned long long min_key_init() { return min_key(FL
 // then the rows combined: DPP row broadcasts (lane 15 of rows 0 / 2 into rows 1 / 3, lane 31
 // into rows 2 and 3) and lane 63 read back, or (RTX_ANIM_DPP_BCAST=0) the four row results read
 // back (values only, see the header).
-#ifndef RTX_ANIM_DPP_BCAST
-#define RTX_ANIM_DPP_BCAST 1
-#endif
 template <int CTRL, int ROWS = 0xf>
 __device__ __forceinline__ uint32_t dpp_ctl(uint32_t v, uint32_t identity) {
     return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(identity), static_cast<int>(v), CTRL,
@@ -209,18 +206,6 @@ __device__ __forceinline__ void wred_min64(unsigned long long (&v)[N]) {
 // reductions of 15 steps each.  Lane l ends with the wave's fold of value
 // q = 2 (l & 1) + ((l >> 1) & 1), c = 4 ((l >> 2) & 1) + 2 ((l >> 3) & 1) + ((l >> 4) & 1)
 // (lanes l and l + 32 alike).  Order-free, like the other wave reductions.
-#ifndef RTX_ANIM_PRIV_MULTI
-#define RTX_ANIM_PRIV_MULTI 128   // (64ths of an element per lane: 128 = two elements per lane)
-#endif
-#ifndef RTX_ANIM_KEEP_CHILD
-#define RTX_ANIM_KEEP_CHILD 1   // a split task goes on with its larger child instead of queueing it
-#endif
-#ifndef RTX_ANIM_BIN_PASSES
-#define RTX_ANIM_BIN_PASSES 1   // register bins: all eight in one pass (1, 512-thread workgroups) or two halves (2)
-#endif
-#ifndef RTX_ANIM_BINS_TRANSPOSE
-#define RTX_ANIM_BINS_TRANSPOSE 1
-#endif
 __device__ __forceinline__ float fold_c(uint32_t c, float a, float b) {
     return c == 0u ? a + b : (c < 4u ? fminf(a, b) : fmaxf(a, b));
 }
@@ -298,18 +283,6 @@ constexpr uint32_t kLdsBytesTop = 46;    // per element: 9 record floats, 2 + 3 
 constexpr uint32_t kLdsBytesSub = 50;    // + the element's triangle id
 constexpr uint32_t kSubLdsMax = 2816;    // subtrees up to this size build from LDS
 
-#ifndef RTX_ANIM_TEAM_ELEMS
-#define RTX_ANIM_TEAM_ELEMS 64u   // a team gets another wave only for this many elements per wave (96: +13 us of timeline, profiles/r03/anim_exp_team*)
-#endif
-#ifndef RTX_ANIM_SMALL
-#define RTX_ANIM_SMALL 1   // one-wave nodes of up to 128 elements by node_small (0: node_process for all)
-#endif
-#ifndef RTX_ANIM_BINS_ATOMIC
-#define RTX_ANIM_BINS_ATOMIC 0   // experiment: LDS atomics into per-wave bin copies for every node
-#endif
-#ifndef RTX_ANIM_STEP_STAMPS
-#define RTX_ANIM_STEP_STAMPS 0   // diagnostics: the root node's step times in status[64..72]
-#endif
 constexpr int kBins = 8, kPlanes = kBins - 1;
 
 // Per-team LDS scratch (one node at a time per team).
@@ -1539,9 +1512,6 @@ __device__ __forceinline__ void run_task(const Launch& L, const MeshDev& M, uint
 // A waiting worker gives up after Launch::wait_ticks (kWaitTicks = 200 ms of s_memrealtime by
 // default, rtx_anim.h): a stuck build reports, never hangs.  (A worker that gives up leaves the entry it claimed unbuilt, so the tree is
 // incomplete: kErrTimeout, and the output launch disables the mesh, see rtx_anim_out)
-#ifndef RTX_ANIM_POLL_SLEEP
-#define RTX_ANIM_POLL_SLEEP 8   // s_sleep units (64 clocks) between a waiting worker's polls
-#endif
 __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
     const MeshDev& M = L.meshes[blockIdx.x];
     extern __shared__ float s_dyn[];

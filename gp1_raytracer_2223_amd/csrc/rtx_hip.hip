@@ -32,20 +32,10 @@
 #include "rtx_cull.h"
 #include "rtx_fastdiv.h"
 #include "rtx_kernels.h"
+#include "rtx_variants.h"
 
 using namespace rtxd;
 
-// Diagnostic build (never a product build): per-wave {start, end, hw id, node-pair steps,
-// triangle steps, lane-work} stamps, read back by rtx_debug_stamps / tools/stamps.py.
-#ifndef RTX_STAMPS
-#define RTX_STAMPS 0
-#endif
-// RTX_STAMPS_LEAN: stamps with the product walk (timeline only; the step counters stay 0)
-#if RTX_STAMPS && !defined(RTX_STAMPS_LEAN)
-#define RTX_STAMPS_WALK 1
-#else
-#define RTX_STAMPS_WALK 0
-#endif
 [[maybe_unused]] constexpr int kStampWords = 6;
 #if RTX_STAMPS
 #define RTX_SPLIT_STAMP()                                                                          \
@@ -162,7 +152,7 @@ __device__ __forceinline__ float sphere_t(const float4 s, const SphereProj& q) {
 
 // HitTest_Plane (Utils.h:84-97): t = num / den.  With tmin > 0 (every ray here), a hit
 // needs t > 0, i.e. num and den non-zero with the same sign: RN(num/den) carries the exact
-// sign of the quotient, 0/x, x/0 and NaN operands all fail t >= tmin.  `plane_same_sign`
+// sign of the quotient, 0/x, x/0 and NaN operands all fail t >= tmin.  `plane_cand`
 // lets a wave skip the division when no lane can hit.
 __device__ __forceinline__ float plane_num(const float4 p0, const float4 p1, const Ray& r) {
     return (p0.x - r.ox) * p1.x + (p0.y - r.oy) * p1.y + (p0.z - r.oz) * p1.z;
@@ -206,21 +196,14 @@ __device__ __forceinline__ void for_room_planes(Fn&& f) {
 __device__ __forceinline__ bool finite3(float x, float y, float z) {
     return __builtin_isfinite(x) & __builtin_isfinite(y) & __builtin_isfinite(z);
 }
-// Over-inclusive is harmless (it only decides whether the division runs): equal sign bits
-// admit zeros and NaNs too, which then fail the range test on t.
-__device__ __forceinline__ unsigned long long plane_same_sign(float num, float den) {
-    return ballot((__float_as_int(num) ^ __float_as_int(den)) >= 0);
-}
-#ifndef RTX_PLANE_BEYOND
-#define RTX_PLANE_BEYOND 1
-#endif
-// Shadow rays (finite tmax): a lane whose exact |num| / |den| exceeds tmax cannot hit either —
+// Shadow rays (finite tmax): only lanes whose num and den have equal sign bits can hit
+// (over-inclusive is harmless: it only decides whether the division runs; zeros and NaNs then
+// fail the range test on t), and a lane whose exact |num| / |den| exceeds tmax cannot hit either —
 // RN(num/den) >= tmax by monotonicity — and one fma tells it exactly: the sign of
 // RN(|den| * tmax - |num|) is the sign of the exact value (an underflow to -0 reads as "not
 // beyond", and a NaN or inf operand as well; the division then decides).  Walls behind the
 // light are the common case, so most waves skip the division.
 __device__ __forceinline__ unsigned long long plane_cand(float num, float den, float tmax) {
-    if (!RTX_PLANE_BEYOND) return plane_same_sign(num, den);
     const int same = (__float_as_int(num) ^ __float_as_int(den)) >= 0;
     const int beyond = fmaf(fabsf(den), tmax, -fabsf(num)) < 0.f;
     return ballot(same & !beyond);
@@ -241,9 +224,6 @@ __device__ __forceinline__ unsigned long long plane_cand(float num, float den, f
 // `cs` is the mesh's cull sign: -1 FrontFaceCulling (reject cullDot < 0), +1
 // BackFaceCulling (reject cullDot > 0), 0 NoCulling (the term 0*cullDot never exceeds 0);
 // shadow rays pass -cs, which is the reference's front/back swap.
-#ifndef RTX_TRI_NOFIX
-#define RTX_TRI_NOFIX 1
-#endif
 template <bool FAST>
 __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const float4 C, float cs, const Ray& r,
                                        float& t) {
@@ -259,7 +239,7 @@ __device__ __forceinline__ float tri_t(const float4 A, const float4 B, const flo
     // is finite with |d| < 2 and the scene's |e1||e2| <= 2^56 (DevScene::tri_fast), so
     // |a| <= |e1||d||e2| < 2^60 and rcp_rn is exact without the check.
     float ai = rcp_rn(a);
-    if (!(FAST && RTX_TRI_NOFIX) && __builtin_expect(fabsf(a) > 0x1p60f, 0)) ai = 1.f / a;
+    if (!FAST && __builtin_expect(fabsf(a) > 0x1p60f, 0)) ai = 1.f / a;
     const float sx = r.ox - A.x, sy = r.oy - A.y, sz = r.oz - A.z;
     const float u = ai * (sx * hx + sy * hy + sz * hz);
     rej = fmaxf(rej, fmaxf(-u, u - 1.f));
@@ -293,7 +273,7 @@ __device__ __forceinline__ bool tri_t_wave(const float4 A, const float4 B, const
     const float a = B.x * hx + B.y * hy + B.z * hz;
     rej = fmaxf(rej, FLT_EPSILON - fabsf(a));
     float ai = rcp_rn(a);
-    if (!(FAST && RTX_TRI_NOFIX) && __builtin_expect(fabsf(a) > 0x1p60f, 0)) ai = 1.f / a;
+    if (!FAST && __builtin_expect(fabsf(a) > 0x1p60f, 0)) ai = 1.f / a;
     const float sx = r.ox - A.x, sy = r.oy - A.y, sz = r.oz - A.z;
     const float u = ai * (sx * hx + sy * hy + sz * hz);
     rej = fmaxf(rej, fmaxf(-u, u - 1.f));
@@ -314,12 +294,6 @@ __device__ __forceinline__ bool tri_t_wave(const float4 A, const float4 B, const
 // direction is finite (decided once per ray batch with a ballot).
 // Returned as a wave lane mask: one v_cmp per condition straight into SGPRs (a ballot
 // of the && would materialise the bool in a VGPR and compare it again).
-#ifndef RTX_OPAQUE_MR
-#define RTX_OPAQUE_MR 1
-#endif
-#ifndef RTX_SLAB_FOLD
-#define RTX_SLAB_FOLD 1
-#endif
 // Node record (32 B): a = {min.x, max.x, min.y, max.y}, b = {min.z, max.z, link, ntri};
 // link and triangle count are adjacent (one 64-bit SGPR pair).  (Packed f32 for the
 // (min, max) pairs was measured 15-35 % slower: profiles/r01/ablate_history.md.)
@@ -353,7 +327,7 @@ __device__ __forceinline__ unsigned long long slab_mask(const float4 a, const fl
         tMax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
         // no NaN here: tMax > 0 && tMax >= tMin  <=>  tMax >= max(tMin, smallest denormal)
         // (f32 denormals are kept, .amdhsa_float_denorm_mode_32 = 3): one compare, no s_and
-        if (RTX_SLAB_FOLD) return ballot(tMax >= fmaxf(tMin, 0x1p-149f));
+        return ballot(tMax >= fmaxf(tMin, 0x1p-149f));
     } else {
         tMin = smin(tx1, tx2);
         tMax = smax(tx1, tx2);
@@ -510,15 +484,11 @@ __device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t lin
             if (COUNT && in) cnt.c[kSlab]++;               // left child's test
             if (COUNT && !ANY && in) cnt.c[kSlab]++;       // right child's (closest: always reached)
             if (ml) {
-#if RTX_OPAQUE_MR
                 // an opaque copy keeps this test local to the block: a `mr != 0` shared with
                 // the test below is hoisted and carried across blocks as a VGPR boolean
                 // (s_cselect + v_cndmask + v_cmp per node pair)
                 unsigned long long mrl = mr;
                 asm("" : "+s"(mrl));
-#else
-                const unsigned long long mrl = mr;
-#endif
                 if (mrl || (COUNT && ANY)) {               // any-hit COUNT: right is counted at pop
                     stk[sp] = make_uint4(__float_as_uint(P.r1.z), __float_as_uint(P.r1.w),
                                          static_cast<uint32_t>(mrl), static_cast<uint32_t>(mrl >> 32));
@@ -558,52 +528,7 @@ __device__ void bvh_walk(const DevScene& S, float cs, const Ray& r, uint32_t lin
     }
 }
 
-#ifndef RTX_LEAN_WALK
-#define RTX_LEAN_WALK 1
-#endif
-#ifndef RTX_ASM_SELECT
-#define RTX_ASM_SELECT 1
-#endif
-#ifndef RTX_OCTANT
-#define RTX_OCTANT 1
-#endif
-// primary-ray plane loop: skip the division when no lane can hit (1) or always divide (0:
-// camera rays nearly always have candidates, and the skip test costs a ballot, an s_and
-// and a branch per plane)
-#ifndef RTX_TRI_EARLY
-#define RTX_TRI_EARLY 1
-#endif
-// shadow sphere loop: leave once no lane is live (1), or run to the end with a single loop
-// exit (0: a second exit is merged into the loop test as SGPR lane-mask logic)
-#ifndef RTX_SPHERE_BREAK
-#define RTX_SPHERE_BREAK 0
-#endif
-#ifndef RTX_PNUM_CACHE
-#define RTX_PNUM_CACHE 1
-#endif
 constexpr int kPlaneCache = 8;   // planes whose shadow-ray numerators are kept in LDS
-#ifndef RTX_PPLANE_SKIP
-#define RTX_PPLANE_SKIP 0
-#endif
-#ifndef RTX_PREFETCH
-#define RTX_PREFETCH 0
-#endif
-// Prefetch touch (experiment): one wave-uniform vector load of the first dword of each child's
-// record (node pair or first triangle) as soon as the pair arrives, so that the line is in
-// the L2 by the time the walk's scalar load asks for it.  Issued in asm (the compiler does
-// not track it), so every touch is drained with touch_wait (s_waitcnt vmcnt(0), the walk has
-// no other vector loads) before its destination register can be reused.
-#if RTX_PREFETCH
-__device__ __forceinline__ uint32_t touch_ld(const void* base, uint32_t off) {
-    const char* p = static_cast<const char*>(base) + off;
-    uint32_t v;
-    asm volatile("global_load_dword %0, %1, %2" : "=&v"(v) : "v"(0u), "s"(p) : "memory");
-    return v;
-}
-__device__ __forceinline__ void touch_wait(uint32_t a, uint32_t b) {
-    asm volatile("s_waitcnt vmcnt(0)" ::"v"(a), "v"(b) : "memory");
-}
-#endif
 // bvh_walk without counters, shaped for the scalar unit: one inner loop descends through
 // inner nodes with scalar selects (no i1 value crosses a block, so nothing is carried as a
 // VGPR boolean or a lane-mask flow variable), a dead end leaves it as an empty "leaf", and
@@ -623,19 +548,10 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
     constexpr bool FAST = SLAB != kSlabExact;
     constexpr bool ORD = CULL && !ANY;
     uint32_t sp = 0;
-    [[maybe_unused]] uint32_t pf0 = 0, pf1 = 0;
     for (;;) {
         while (ntri == 0) {
             NodePair P;
             ldcb64(nb, link, P.l0, P.l1, P.r0, P.r1);
-#if RTX_PREFETCH
-            touch_wait(pf0, pf1);
-            {
-                const uint32_t nl = __float_as_uint(P.l1.w), nr = __float_as_uint(P.r1.w);
-                pf0 = touch_ld(nl ? static_cast<const void*>(S.tris) : nb, __float_as_uint(P.l1.z));
-                pf1 = touch_ld(nr ? static_cast<const void*>(S.tris) : nb, __float_as_uint(P.r1.z));
-            }
-#endif
             unsigned long long ml = slab_mask<SLAB>(P.l0, P.l1, r) & m;
             unsigned long long mr = slab_mask<SLAB>(P.r0, P.r1, r) & m;
             [[maybe_unused]] bool rfirst = false;
@@ -662,7 +578,6 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                 P.l1 = P.r1;
                 P.r1 = t1;
             }
-#if RTX_ASM_SELECT
             // next (link, ntri): left, else right, else a dead end taken as an empty leaf
             // (ntri = 1 with m = 0); `both` = mr if the left child is taken too (the right
             // one then waits on the stack).  Written as 64-bit s_cselects on one SCC each:
@@ -683,25 +598,10 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                                      static_cast<uint32_t>(mr >> 32));
                 ++sp;
             }
-#else
-            if (ml != 0 && mr != 0) {   // both: descend left, the right child waits on the stack
-                stk[sp] = make_uint4(__float_as_uint(P.r1.z), __float_as_uint(P.r1.w), static_cast<uint32_t>(mr),
-                                     static_cast<uint32_t>(mr >> 32));
-                ++sp;
-            }
-            // next (link, ntri): left, else right, else a dead end taken as an empty leaf
-            // (ntri = 1 with m = 0) — two 64-bit scalar selects
-            unsigned long long nx = mr ? link_ntri(P.r1) : (1ull << 32);
-            nx = ml ? link_ntri(P.l1) : nx;
-            m = ml ? ml : mr;
-#endif
             link = static_cast<uint32_t>(nx);
             // opaque: a 32-bit s_cmp for the loop test (else it becomes a 64-bit v_cmp on nx)
-            ntri = RTX_ASM_SELECT ? opaque(static_cast<uint32_t>(nx >> 32)) : static_cast<uint32_t>(nx >> 32);
+            ntri = opaque(static_cast<uint32_t>(nx >> 32));
         }
-#if RTX_PREFETCH
-        touch_wait(pf0, pf1);
-#endif
         if (m) {
             const bool in = (m >> lane) & 1ull;
             for (uint32_t k = 0; k < ntri; ++k) {
@@ -709,12 +609,8 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                 Tri T;
                 ldcb64(S.tris, ti, T.a, T.b, T.c, T.d);
                 float t;
-#if RTX_TRI_EARLY
                 float rej;
                 if (!tri_t_wave<FAST, CB, ANY>(T.a, T.b, T.c, cs, r, ANY ? (m & live) : m, rej, t)) continue;
-#else
-                const float rej = tri_t<FAST>(T.a, T.b, T.c, cs, r, t);
-#endif
                 if (ANY) {
                     live &= ~(ballot(!(rej > 0.f)) & ballot(!(t >= r.tmax)) & m);
                 } else {
@@ -770,7 +666,7 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
         if (__float_as_uint(c1.w)) m &= cull_pass<ANY>(c0, c1, r, cq, sc_t, n);
     }
     if (m == 0) return;
-    if (RTX_LEAN_WALK && !COUNT && !RTX_STAMPS_WALK)
+    if (!COUNT && !RTX_STAMPS_WALK)
         bvh_walk_lean<ANY, OCT ? kSlabOct : (FAST ? kSlabFast : kSlabExact), CB, CULL>(
             S, nb, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask, lane, stk, sc_t,
             sc_tri, live, nullptr, 0u, cq);
@@ -827,7 +723,7 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int
         ntri = __float_as_uint(c1.w);
     }
     if (m == 0) return;
-    if (RTX_LEAN_WALK && !RTX_STAMPS_WALK)
+    if (!RTX_STAMPS_WALK)
         bvh_walk_lean<ANY, SLAB, CB, CULL>(S, nb, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, sc_t,
                                            sc_tri, live, occ_word, occ_bit, cq);
     else
@@ -920,35 +816,6 @@ __device__ __forceinline__ uint32_t q8(float c) {
 //                                          occlusion + the bits, shading, output
 // Every phase recomputes the primary ray and the sphere/plane hits with the same code, so
 // all of them see bit-identical values.
-// Timing-only ablation switches (results are wrong when set; never in a product build).
-#ifndef RTX_ABL_PPLANE
-#define RTX_ABL_PPLANE 0
-#endif
-#ifndef RTX_ABL_PMESH
-#define RTX_ABL_PMESH 0
-#endif
-#ifndef RTX_ABL_SPLANE
-#define RTX_ABL_SPLANE 0
-#endif
-#ifndef RTX_ABL_SMESH
-#define RTX_ABL_SMESH 0
-#endif
-#ifndef RTX_ABL_LIGHTS
-#define RTX_ABL_LIGHTS 0
-#endif
-#ifndef RTX_MIN_WAVES_PER_EU
-#define RTX_MIN_WAVES_PER_EU 1
-#endif
-// XCD bands (experiment build, tools/xcd_bands_ab.sh; RTX_XCD_BANDS=1 in the environment then
-// turns them on): band x of the image on XCD x.  Off in the product build: the band-aware tile
-// fetch alone costs 3-4 % (profiles/r03/ab_xcd_bands.txt) and the bands gain no time.
-#ifndef RTX_XCD_BANDS
-#define RTX_XCD_BANDS 0
-#endif
-// XCD-aware dispatch: runs of this many consecutive dispatch-order entries per XCD (0/1: off)
-#ifndef RTX_XCD_RUN
-#define RTX_XCD_RUN 0
-#endif
 // DEEP: the variant for scenes whose BVH is kStackDepth or more levels deep (a DFS stack of
 // kStackDepthDeep entries per wave in LDS; fewer waves fit a CU, so it is used only then).
 // HSTK (with DEEP): the stacks in HBM instead (DevScene::hstk, any depth: the reference's
@@ -962,12 +829,6 @@ __device__ __forceinline__ uint32_t q8(float c) {
 // lanes, outside the loops), so the SGPR file no longer caps it at 7 waves like the generic
 // kernel's 106 SGPRs (Bunny 61.1 -> 60.6 us, Bunny + 8 lights 427 -> 418 us; 10 waves: no gain);
 // W4_Optional's variant 231 -> 223 us.  The variant with spheres and meshes stays at 7 (8: +4 %).
-#ifndef RTX_SPEC_WAVES
-#define RTX_SPEC_WAVES 8
-#endif
-#ifndef RTX_SPEC_WAVES_PARTIAL
-#define RTX_SPEC_WAVES_PARTIAL 7
-#endif
 // CULLK: the variant with the exact cull (DevScene::cull; launched only for scenes that have the
 // records — the code of the cull paths costs the kernel without them registers and 8 %).
 template <bool COUNT, int PHASE, bool DEEP = false, int SPEC = 0, bool HSTK = false, bool CULLK = false>
@@ -992,7 +853,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
     __shared__ uint4 stkE[kBlockThreads / 64][kDepth];
     __shared__ unsigned long long stkT[(COUNT && !HSTK) ? kBlockThreads / 64 : 1][(COUNT && !HSTK) ? kDepth : 1];
     // per-lane shadow-ray plane numerators, shared by every light (see the light loop)
-    __shared__ float pnumS[RTX_PNUM_CACHE ? kBlockThreads / 64 : 1][RTX_PNUM_CACHE ? kPlaneCache : 1][64];
+    __shared__ float pnumS[kBlockThreads / 64][kPlaneCache][64];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
 #if RTX_STAMPS
     // diagnostic build only: per-wave {start, end, hw_id} in the counters buffer
@@ -1010,41 +871,10 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
     // -3 %, Synthetic100k -9 %).  Which wave renders a tile never changes a pixel's value.
     const uint32_t b = blockIdx.x;
     uint32_t widx = b * kWavesPerBlock + wave;   // wave index in the launch
-    if (PHASE == 0 && RTX_XCD_RUN > 1) {
-        // Workgroups go round robin to the 8 XCDs (blockIdx % 8), each with its own L2: give
-        // XCD x runs of RTX_XCD_RUN consecutive dispatch-order entries (neighbouring tiles of
-        // one cost class walk the same BVH nodes) instead of every 8th entry.  A bijection on
-        // the grid, which the host pads to a multiple of 8 * RTX_XCD_RUN.
-        constexpr uint32_t kRun = RTX_XCD_RUN > 1 ? RTX_XCD_RUN : 1;
-        const uint32_t x = b % 8u, k = b / 8u;
-        const uint32_t pos = ((k / kRun) * 8u + x) * kRun + (k % kRun);
-        widx = pos * kWavesPerBlock + wave;
-    }
-#if RTX_XCD_BANDS
-    if (PHASE == 0 && F.band_tiles) {
-        // XCD bands: workgroups go round robin to the 8 XCDs (blockIdx % 8), each with its own
-        // 4 MB L2.  XCD x takes dispatch slots [x, x + 1) * band_tiles, which the schedule fills
-        // with band x of the image (consecutive tiles, heaviest first: rtx_sched_scan), so one
-        // XCD's rays walk the part of the scene its band sees.  A bijection onto [0, n_tiles)
-        // (the host sizes the grid 8 x band_tiles / kWavesPerBlock; the rest return).
-        const uint32_t bpb = F.band_tiles / kWavesPerBlock, k = b >> 3;
-        widx = k < bpb ? ((b & 7u) * bpb + k) * kWavesPerBlock + wave : 8u * F.band_tiles;
-        widx = __builtin_amdgcn_readfirstlane(widx);   // wave-uniform: keep the scalar tile loads
-    }
-#endif
     uint32_t tile, part = 0, light = 0;
     if (PHASE == 0) {
-#if RTX_XCD_BANDS
-        // (XCD bands: slots up to 8 x band_tiles, free ones holding the no-tile marker ~0u)
-        const uint32_t lim = F.band_tiles ? 8u * F.band_tiles : F.n_tiles;
-        const uint32_t w = widx < lim ? widx : 0u;
-        tile = F.order ? ldc(F.order, w) : w;
-        tile = __builtin_amdgcn_readfirstlane(widx < lim ? tile : ~0u);   // wave-uniform
-        if (tile >= F.n_tiles) return;
-#else
         if (widx >= F.n_tiles) return;
         tile = F.order ? ldc(F.order, widx) : widx;
-#endif
         if (F.heavy_flag && ldc(F.heavy_flag, tile)) return;   // rendered by the split launches
     } else {
         // grid (heavy tiles / waves per block, parts, lights), tile fastest: every heavy tile's part 0 is
@@ -1101,7 +931,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
     // FAST: every active lane's inverse direction finite and non-zero (make_ray's domain)
     const bool fast = (active & vslow) == 0 && S.tri_fast;
     // octant of the wave's primary rays (-1: mixed signs, or no octant copies)
-    const int poct = (RTX_OCTANT && fast && S.oct_bytes && PHASE == 0) ? batch_octant(vr, active) : -1;
+    const int poct = (fast && S.oct_bytes && PHASE == 0) ? batch_octant(vr, active) : -1;
     // exact cull of the view's camera anchor (FAST waves; a direction normalised from a magnitude
     // of at least 2^-30 has |d| = 1 +- 3u, which the bound assumes)
     constexpr bool kCull = CULLK && !COUNT && !RTX_STAMPS_WALK;
@@ -1163,9 +993,6 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         ldcb32(S.planes, opaque(i), p0, p1);
         if (COUNT && valid) cnt.c[kPlane]++;
         const float num = plane_num(p0, p1, vr), den = plane_den(p1, vr);
-#if RTX_PPLANE_SKIP
-        if (!(plane_same_sign(num, den) & active)) continue;   // no lane can have t >= tmin > 0
-#endif
         const float t = num / den;
         const bool h = valid & (t >= vr.tmin) & (t < vr.tmax);
         sc_t = h ? t : sc_t;
@@ -1202,7 +1029,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         const float sc0 = sc_t;
         uint32_t sc_tri = 0;
         unsigned long long unused = 0;
-        const int oct = (RTX_OCTANT && fast && S.oct_bytes) ? batch_octant(vr, active) : -1;
+        const int oct = (fast && S.oct_bytes) ? batch_octant(vr, active) : -1;
         if (oct >= 0 && pcull)
             part_traverse<false, kSlabOct, kCullBack, kCull>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri, unused,
                                                              cnt, nullptr, 0u, pq);
@@ -1281,7 +1108,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                 unsigned long long live = hitmask;
                 const bool sfast = (hitmask & sslow) == 0 && S.tri_fast;
                 const int soct =
-                    (RTX_OCTANT && sfast && S.oct_bytes && PHASE == 0 && n_mesh) ? batch_octant(sr, hitmask) : -1;
+                    (sfast && S.oct_bytes && PHASE == 0 && n_mesh) ? batch_octant(sr, hitmask) : -1;
                 // exact cull of the light's anchor: lanes with mag <= cull_T[li] (and a direction
                 // normalised from at least 2^-30)
                 const bool scull = kCull && S.cull_stride && sfast && (PHASE == 0 || PHASE == 2) && n_mesh;
@@ -1293,9 +1120,6 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                 // (single-condition loops with a separate exit test: a `&& live` loop
                 // condition is carried as a VGPR boolean by the compiler)
                 for (uint32_t i = 0; i < (PHASE == 2 ? 0u : n_sph * 16u); i += 16u) {
-#if RTX_SPHERE_BREAK
-                    if (!live) break;
-#endif
                     const float4 s = ldcb16(S.spheres, opaque(i));
                     if (COUNT && ((live >> lane) & 1ull)) cnt.c[kSphere]++;
                     const SphereProj q = sphere_perp(s, sr);
@@ -1309,7 +1133,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                 // in LDS, the others read it back (same value, bit for bit).  One loop version
                 // per case, so no per-plane select.
                 const uint32_t np = (RTX_ABL_SPLANE || PHASE == 2 || room_s) ? 0u : n_pl * 32u;
-                const bool cache_ok = RTX_PNUM_CACHE && !COUNT && np <= static_cast<uint32_t>(kPlaneCache) * 32u;
+                const bool cache_ok = !COUNT && np <= static_cast<uint32_t>(kPlaneCache) * 32u;
                 if (room_s) {   // a / d (room_a): cheaper than the cached numerator
                     for_room_planes([&](auto kc) {
                         constexpr int k = decltype(kc)::value;
@@ -1326,7 +1150,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                     for (uint32_t i = 0; i < np; i += 32u) {
                         float4 p0, p1;
                         ldcb32(S.planes, opaque(i), p0, p1);
-                        const float num = pnumS[RTX_PNUM_CACHE ? wave : 0][RTX_PNUM_CACHE ? (i >> 5) : 0][lane];
+                        const float num = pnumS[wave][i >> 5][lane];
                         const float den = plane_den(p1, sr);
                         const unsigned long long cand = plane_cand(num, den, sr.tmax) & live;
                         if (!cand) continue;
@@ -1339,7 +1163,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                         ldcb32(S.planes, opaque(i), p0, p1);
                         if (COUNT && ((live >> lane) & 1ull)) cnt.c[kPlane]++;
                         const float num = plane_num(p0, p1, sr), den = plane_den(p1, sr);
-                        if (cache_ok) pnumS[RTX_PNUM_CACHE ? wave : 0][RTX_PNUM_CACHE ? (i >> 5) : 0][lane] = num;
+                        if (cache_ok) pnumS[wave][i >> 5][lane] = num;
                         const unsigned long long cand = plane_cand(num, den, sr.tmax) & live;
                         if (!cand) continue;   // also taken once no lane is live
                         const float t = num / den;
@@ -1371,7 +1195,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                     const int4 E = ldc(S.parts, part);
                     float st = 0.f;
                     uint32_t stri = 0;
-                    const int poct2 = (RTX_OCTANT && sfast && S.oct_bytes) ? batch_octant(sr, hitmask) : -1;
+                    const int poct2 = (sfast && S.oct_bytes) ? batch_octant(sr, hitmask) : -1;
                     if (poct2 >= 0 && scull)
                         part_traverse<true, kSlabOct, kCullBack, kCull>(S, E, sr, poct2, live, lane, stk, st, stri, live,
                                                                         cnt, &F.occ_bits[slot], 1u << li, sq);
@@ -1755,71 +1579,19 @@ __global__ void __launch_bounds__(kReorderThreads) rtx_sched_count(uint32_t* __r
 
 // Exclusive prefix of hist[class][chunk] in class-major order (in place), the total cost and
 // the heavy threshold; zeroes the heavy counter the scatter appends to.
-// XCD bands (band_tiles != 0, nchunks <= kScanThreads): the chunks (kSchedChunk consecutive
-// tiles: a few image rows) are dealt to the 8 XCDs in snake order of their measured cost
-// (heaviest chunk to XCD 0, the next to XCD 1, ..., the 9th to XCD 7, the 10th to XCD 6, ...),
-// so every XCD gets the same number of chunks and about the same cost.  The prefix then runs
-// band-major (band, class, chunk) and band x's slots start at x * band_tiles; the slots a band
-// leaves free get the no-tile marker ~0u in `order`.
 __global__ void __launch_bounds__(kScanThreads) rtx_sched_scan(uint32_t* __restrict__ hist, uint32_t nchunks,
-                                                               uint32_t band_tiles, uint32_t* __restrict__ order,
                                                                const unsigned long long* __restrict__ csum, uint32_t n,
                                                                uint32_t split_slots, uint32_t split_permille,
                                                                unsigned long long* __restrict__ thr_out,
                                                                uint32_t* __restrict__ heavy_n) {
     __shared__ uint32_t part[kScanThreads];
     __shared__ unsigned long long cpart[kScanThreads];
-    __shared__ uint32_t s_chunk[kScanThreads];   // XCD bands: chunks in (band, round) order
-    __shared__ uint32_t s_nb[8], s_cnt[8], s_fc[8], s_fb[8], s_off[8];
     const uint32_t tid = threadIdx.x;
-    const bool bands = band_tiles != 0u;
-    uint32_t my_band = 0, my_round = 0;
-    if (bands) {
-        if (tid < 8u) { s_nb[tid] = 0u; s_cnt[tid] = 0u; }
-        __syncthreads();
-        if (tid < nchunks) {
-            const unsigned long long my = csum[tid];
-            uint32_t rank = 0;
-            for (uint32_t j = 0; j < nchunks; ++j) {
-                const unsigned long long o = csum[j];
-                rank += (o > my || (o == my && j < tid)) ? 1u : 0u;
-            }
-            my_round = rank >> 3;
-            my_band = (my_round & 1u) ? 7u - (rank & 7u) : (rank & 7u);
-            atomicAdd(&s_nb[my_band], 1u);
-            atomicAdd(&s_cnt[my_band], min(static_cast<uint32_t>(kSchedChunk), n - tid * kSchedChunk));
-        }
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t fc = 0, tiles = 0;
-            for (uint32_t x = 0; x < 8u; ++x) {
-                s_fc[x] = fc;
-                s_fb[x] = fc * kCostBuckets;
-                s_off[x] = x * band_tiles - tiles;
-                fc += s_nb[x];
-                tiles += s_cnt[x];
-            }
-        }
-        __syncthreads();
-        if (tid < nchunks) s_chunk[s_fc[my_band] + my_round] = tid;
-        __syncthreads();
-    }
-    // entry i of the scan order -> its hist index and slot offset
-    auto hidx = [&](uint32_t i, uint32_t& off) -> uint32_t {
-        off = 0;
-        if (!bands) return i;
-        uint32_t x = 0;
-#pragma unroll
-        for (uint32_t y = 1; y < 8u; ++y) x += i >= s_fb[y] ? 1u : 0u;
-        const uint32_t r = i - s_fb[x], nb = s_nb[x], cls = r / nb;
-        off = s_off[x];
-        return cls * nchunks + s_chunk[s_fc[x] + (r - cls * nb)];
-    };
     const uint32_t len = kCostBuckets * nchunks;
     const uint32_t per = (len + kScanThreads - 1) / kScanThreads;
     const uint32_t lo = tid * per, hi = (lo + per < len) ? lo + per : len;
-    uint32_t s = 0, off = 0;
-    for (uint32_t i = lo; i < hi; ++i) s += hist[hidx(i, off)];
+    uint32_t s = 0;
+    for (uint32_t i = lo; i < hi; ++i) s += hist[i];
     unsigned long long cs = 0;
     for (uint32_t i = tid; i < nchunks; i += kScanThreads) cs += csum[i];
     part[tid] = s;
@@ -1835,13 +1607,10 @@ __global__ void __launch_bounds__(kScanThreads) rtx_sched_scan(uint32_t* __restr
     }
     uint32_t acc = part[tid] - s;   // exclusive
     for (uint32_t i = lo; i < hi; ++i) {
-        const uint32_t h = hidx(i, off), v = hist[h];
-        hist[h] = acc + off;
+        const uint32_t v = hist[i];
+        hist[i] = acc;
         acc += v;
     }
-    if (bands)
-        for (uint32_t x = 0; x < 8u; ++x)
-            for (uint32_t k = s_cnt[x] + tid; k < band_tiles; k += kScanThreads) order[x * band_tiles + k] = ~0u;
     if (tid == 0) {
         const unsigned long long total = cpart[kScanThreads - 1];
         const bool force = split_slots == 0xffffffffu;
@@ -1956,11 +1725,9 @@ struct rtx_ctx {
     unsigned long long* d_csum = nullptr;   // per chunk cost sums
     unsigned long long* d_thr = nullptr;    // heavy threshold of the measured frame
     uint32_t sched_cap = 0;
-    uint32_t order_cap = 0;          // slots of d_order (XCD bands pad them to 8 x band_tiles)
     std::string sched_key;
     bool sched_ready = false;
     bool sched_enabled = true;
-    bool xcd_bands = false;          // RTX_XCD_BANDS=1: band x of the image on XCD x (see the kernel)
     uint64_t sched_frame = 0;
     uint64_t scene_gen = 0;
     // split rendering of heavy tiles: double-buffered flag/list sets (the reorder kernel
@@ -2132,7 +1899,6 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     // RTX_TILE_ORDER=0 disables cost-ordered tile dispatch (identity order every frame)
     if (const char* e = std::getenv("RTX_TILE_ORDER")) c->sched_enabled = std::strcmp(e, "0") != 0;
     // RTX_SPLIT=0 renders heavy tiles in one piece; RTX_SPLIT=force splits every tile
-    if (const char* e = std::getenv("RTX_XCD_BANDS")) c->xcd_bands = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_NO_SPEC")) c->no_spec = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_NO_CULL")) c->no_cull = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_CULL_RATIO")) {
@@ -2667,7 +2433,7 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
     d.n_spheres = s->n_spheres; d.n_planes = s->n_planes; d.n_meshes = s->n_meshes;
     d.n_lights = s->n_lights; d.n_materials = nm;
     d.tri_fast = max_ee <= 0x1p56 ? 1u : 0u;
-    d.oct_bytes = (RTX_OCTANT && oct_ok && !std::getenv("RTX_NO_OCTANT")) ? static_cast<uint32_t>(node_bytes) : 0u;
+    d.oct_bytes = (oct_ok && !std::getenv("RTX_NO_OCTANT")) ? static_cast<uint32_t>(node_bytes) : 0u;
     d.n_tris = static_cast<uint32_t>(tri.size() / 4); d.n_nodes = static_cast<uint32_t>(nodes.size() / 2);
     if (cull_on) {
         d.cull = B.cull;
@@ -2828,20 +2594,10 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     F.counters = c->d_counters;
     const uint32_t ntiles = F.tiles_x * gy * static_cast<uint32_t>(n_views);
     F.n_tiles = ntiles;
-    uint32_t nblocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (RTX_XCD_RUN > 1) nblocks = (nblocks + 8 * RTX_XCD_RUN - 1) / (8 * RTX_XCD_RUN) * (8 * RTX_XCD_RUN);
-    F.band_tiles = 0;
-    const uint32_t nch_all = (ntiles + kSchedChunk - 1) / kSchedChunk;
-    if (RTX_XCD_BANDS && c->xcd_bands && RTX_XCD_RUN <= 1 && nch_all <= static_cast<uint32_t>(kScanThreads)) {
-        // XCD bands (the kernel, rtx_sched_scan): the same number of whole scheduling chunks
-        // per XCD, band x's slots from x * band_tiles
-        F.band_tiles = (nch_all + 7u) / 8u * kSchedChunk;
-        nblocks = 8u * (F.band_tiles / kWavesPerBlock);
-    }
-    const uint32_t order_slots = F.band_tiles ? 8u * F.band_tiles : ntiles;
+    const uint32_t nblocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
     grid = dim3(nblocks, 1, 1);
     // Cost-ordered dispatch (see the kernel): keep one order/cost pair per launch shape.
-    if (ntiles > c->sched_cap || order_slots > c->order_cap) {
+    if (ntiles > c->sched_cap) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         (void)hipFree(c->d_order);
         (void)hipFree(c->d_cost);
@@ -2855,9 +2611,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         c->d_order = nullptr;
         c->d_cost = nullptr;
         c->sched_cap = 0;
-        c->order_cap = 0;
-        HIP_TRY(c, hipMalloc(&c->d_order, static_cast<size_t>(std::max(ntiles, order_slots)) * 4));
-        c->order_cap = std::max(ntiles, order_slots);
+        HIP_TRY(c, hipMalloc(&c->d_order, ntiles * 4));
         HIP_TRY(c, hipMalloc(&c->d_cost, ntiles * 4));
         for (int k = 0; k < 2; ++k) HIP_TRY(c, hipMalloc(&c->d_heavy_flag[k], ntiles * 4));
         HIP_TRY(c, hipMalloc(&c->d_saved_cost, ntiles * 4));
@@ -3018,7 +2772,7 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
                            F.heavy_flag, c->d_saved_cost, c->d_hist, c->d_csum, nch);
         HIP_TRY(c, hipGetLastError());
         hipLaunchKernelGGL(rtx_sched_scan, dim3(1), dim3(kScanThreads), 0, c->stream, c->d_hist, nch,
-                           F.band_tiles, c->d_order, c->d_csum,
+                           c->d_csum,
                            F.n_tiles, slots, c->split_permille, c->d_thr, c->d_heavy_n);
         HIP_TRY(c, hipGetLastError());
         hipLaunchKernelGGL(rtx_sched_scatter, dim3(nch), dim3(kReorderThreads), 0, c->stream, F.cost, c->d_order,

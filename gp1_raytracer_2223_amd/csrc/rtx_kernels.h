@@ -164,7 +164,6 @@ struct FrameArgs {
     uint32_t stripe_first, stripe_step;
     uint32_t tiles_x, tiles_y;    // 8x8 wave tiles per view row / per view column (owned)
     uint32_t n_tiles;             // wave tiles in the launch (all views)
-    uint32_t band_tiles;          // XCD bands: XCD x renders dispatch slots [x, x + 1) * band_tiles (0 = off)
     const uint32_t* __restrict__ order;   // dispatch permutation of the tiles (null = identity)
     uint32_t* __restrict__ cost;          // per-tile cost of this frame (null = not measured)
     uint32_t* __restrict__ out_px;   // view v at out_px + v * width * height

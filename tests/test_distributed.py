@@ -79,10 +79,11 @@ def test_stripe_partition_gloo(world):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["views", "frame"])
-def test_bench_multi_rank_hip_gloo(mode, tmp_path):
+def test_bench_two_ranks_hip_shmctl(mode, tmp_path):
     """The real multi-rank path on the HIP renderer: bench.py under torch.distributed.run
-    with 2 gloo ranks pinned to device 0 (RTX_BENCH_DEVICE; the driver's N-GPU runs map
-    rank r to device r).  `views` (the default, weak scaling): 2 views per step, each
+    with 2 ranks pinned to device 0 (RTX_BENCH_DEVICE; the driver's N-GPU runs map rank r
+    to device r), coordinated by bench.py's shared-memory control block (ShmCtl: barriers and
+    the max-over-ranks step time; no process group).  `views` (the default, weak scaling): 2 views per step, each
     striped over both ranks; `frame` (strong): one Bunny 1080p frame per step.  Each rank
     gathers its stripes into the shared page-locked host frames; rank 0 checks view 0 (the
     reference camera) against the reference's SHA-256 (bench.py `parity`)."""

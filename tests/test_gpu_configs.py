@@ -104,28 +104,3 @@ def test_headline_config_many_frames(fresh_ctx):
         fresh_ctx.render_async(cam, p)
     px, rgb = fresh_ctx.render(cam, p)
     check_frame(g, px, rgb, True, "W4_Bunny 1080p frame 131")
-
-
-@pytest.mark.parametrize("name,W,H,exact", [CONFIGS[3], CONFIGS[4], CONFIGS[1]],
-                         ids=["Synthetic100k_1920x1080", "Bunny8Lights_3840x2160", "W3_1280x720"])
-def test_xcd_bands_full_resolution(monkeypatch, name, W, H, exact):
-    """RTX_XCD_BANDS=1 (band x of the image on XCD x, the chunks dealt by measured cost,
-    rtx_sched_scan): the padded grid and the no-tile slots change which wave renders a tile,
-    never a pixel — every frame is still the reference's.  The bands are compiled only into
-    the experiment build (-DRTX_XCD_BANDS=1, tools/xcd_bands_ab.sh sets RTX_TEST_XCD_BANDS)."""
-    if os.environ.get("RTX_TEST_XCD_BANDS") != "1":
-        pytest.skip("XCD bands are an experiment build (tools/xcd_bands_ab.sh)")
-    from gp1_raytracer_2223_amd.renderer import DeviceContext
-    monkeypatch.setenv("RTX_XCD_BANDS", "1")
-    ctx = DeviceContext(int(os.environ.get("RTX_TEST_DEVICE", "0")))
-    try:
-        g = np.load(G / f"config_{name}_{W}x{H}.npz")
-        hs = HostScene(name)
-        s, cam = hs.view()
-        ctx.upload(s)
-        p = abi.make_params(W, H)
-        for f in range(FRAMES):
-            px, rgb = ctx.render(cam, p)
-            check_frame(g, px, rgb, exact, f"{name} {W}x{H} XCD bands frame {f + 1}")
-    finally:
-        ctx.close()

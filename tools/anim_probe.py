@@ -52,8 +52,6 @@ for i in range(50):
     host.update(0.01 * i)
 print(f"{name}: host Update {(time.perf_counter() - t0) / 50 * 1e3:.3f} ms each")
 
-# phase stamps of the last device build (100 MHz)
-st = (C.c_uint32 * 64)() if False else None
 # scene image of the device Update vs the registration (host-built) image of the same state
 import ctypes as C  # noqa: E402
 lib = abi.load_hip()
@@ -84,28 +82,43 @@ if len(diff):
 st = (C.c_uint32 * 128)()
 abi.check(lib.rtx_anim_stamps(an1.h, 0, st), "rtx_anim_stamps")
 w = [int(x) for x in st]
-us = lambda x: ((x - w[8]) & 0xffffffff) / 100.0  # noqa: E731  (s_memrealtime, 100 MHz)
+
+
+def us(x, ref=None):
+    """A stamp (low 32 bits of s_memrealtime, 100 MHz) in us from `ref` (default: the build's start,
+    w[8]), as a SIGNED 32-bit difference, so a stamp taken before the start (a worker workgroup
+    that entered early) reads negative instead of wrapping to ~42.9 s; an unwritten stamp is None."""
+    if x == 0:
+        return None
+    d = (x - (w[8] if ref is None else ref)) & 0xffffffff
+    return (d - (1 << 32) if d >= 1 << 31 else d) / 100.0
+
+
+def r1(x):
+    return None if x is None else round(x, 1)
+
+
 print(f"status: err {w[0]} deepest {w[1]} nodesUsed {w[2]} parts {w[3]} subtrees {w[4]} task-split ids {w[5]} "
       f"nodes split as tasks {w[6]}")
-print(f"build phases (us from start): set-up {us(w[9]):.1f}, root split {us(w[10]):.1f}, "
-      f"subtrees {us(w[11]):.1f} .. {us(w[12]):.1f}, output start {us(w[13]):.1f}, ranks {us(w[14]):.1f}, "
-      f"frontier {us(w[15]):.1f}")
-print(f"subtree 0: staged {us(w[29]):.1f}, levels end {[round(us(x), 1) for x in w[32:40] if x]}, levels done {us(w[30]):.1f}, "
-      f"ranks {us(w[31]):.1f}")
-print(f"output wg0: records written {us(w[57]):.1f}")
+print(f"build phases (us from start): set-up {r1(us(w[9]))}, root split {r1(us(w[10]))}, "
+      f"subtrees {r1(us(w[11]))} .. {r1(us(w[12]))}, output start {r1(us(w[13]))}, ranks {r1(us(w[14]))}, "
+      f"frontier {r1(us(w[15]))}")
+print(f"subtree 0: staged {r1(us(w[29]))}, levels end {[r1(us(x)) for x in w[32:40] if x]}, levels done {r1(us(w[30]))}, "
+      f"ranks {r1(us(w[31]))}")
+print(f"output wg0: records written {r1(us(w[57]))}")
 if w[61] != w[60] and w[31] != w[29]:
     print(f"shader clock during subtree 0: {((w[61] - w[60]) & 0xffffffff) / (((w[31] - w[29]) & 0xffffffff) / 100.0):.0f} MHz")
-print("first splits (size, start, end us):", [(w[16 + k], round(us(w[20 + 2 * k]), 1), round(us(w[21 + 2 * k]), 1))
+print("first splits (size, start, end us):", [(w[16 + k], r1(us(w[20 + 2 * k])), r1(us(w[21 + 2 * k])))
                                                for k in range(min(4, w[6]))])
 if w[63]:
-    print("top root steps (us from its start):", [round(((w[64 + i] - w[63]) & 0xffffffff) / 100.0, 1) for i in range(9)])
+    print("top root steps (us from its start):", [r1(us(w[64 + i], w[63])) for i in range(9)])
 if w[40]:
-    print("subtree-0 root steps (us from its start):", [round(((w[41 + i] - w[40]) & 0xffffffff) / 100.0, 1) for i in range(9)],
-          "bins/axis:", [round(((w[50 + a] - w[40]) & 0xffffffff) / 100.0, 1) for a in range(3)],
-          "sweep lanes done, key reduced:", [round(((w[55 + a] - w[40]) & 0xffffffff) / 100.0, 1) for a in range(2)],
-          "child bounds loop done, reduced:", [round(((w[53 + a] - w[40]) & 0xffffffff) / 100.0, 1) for a in range(2)])
-print("subtrees (start, end us):", [(round(us(w[80 + 2 * f]), 1), round(us(w[81 + 2 * f]), 1)) for f in range(min(8, w[4]))])
-print("worker workgroup entry (us):", [round(us(w[112 + f]), 1) for f in range(16)])
+    print("subtree-0 root steps (us from its start):", [r1(us(w[41 + i], w[40])) for i in range(9)],
+          "bins/axis:", [r1(us(w[50 + a], w[40])) for a in range(3)],
+          "sweep lanes done, key reduced:", [r1(us(w[55 + a], w[40])) for a in range(2)],
+          "child bounds loop done, reduced:", [r1(us(w[53 + a], w[40])) for a in range(2)])
+print("subtrees (start, end us):", [(r1(us(w[80 + 2 * f])), r1(us(w[81 + 2 * f]))) for f in range(min(8, w[4]))])
+print("worker workgroup entry (us):", [r1(us(w[112 + f])) for f in range(16)])
 print("subtree sizes:", [w[96 + f] for f in range(min(16, w[4]))])
 if w[63]:
-    print("top root bins per axis done (us from its start):", [round(((w[73 + a] - w[63]) & 0xffffffff) / 100.0, 1) for a in range(3)])
+    print("top root bins per axis done (us from its start):", [r1(us(w[73 + a], w[63])) for a in range(3)])
