@@ -534,9 +534,10 @@ constexpr int kPlaneCache = 8;   // planes whose shadow-ray numerators are kept 
 // VGPR boolean or a lane-mask flow variable), a dead end leaves it as an empty "leaf", and
 // the pop loop is the only other path.  Same visits, tests and order as bvh_walk.
 // `nb` is the node copy the slab form reads (the octant's (near, far) copy for kSlabOct).
-// CULL: a child is entered only by the lanes cull_pass keeps, and a closest-hit walk is ORDERED:
-// the child most lanes enter first is walked first, and the scratch hit is replaced by t < sc_t or,
-// on a tie, by the lower triangle index — the reference's first-found winner whatever the visiting
+// CULL: a child is entered only by the lanes cull_pass keeps, and the walk is ORDERED: the child
+// most lanes enter first is walked first.  Shadow rays (RTX_CULL_ORDER_ANY): nearer occluders end
+// their lanes sooner, and any-hit is a yes/no that no order changes.  Closest hit: the scratch hit
+// is replaced by t < sc_t or, on a tie, by the lower triangle index — the reference's first-found winner whatever the visiting
 // order, because left-then-right DFS order is increasing triangle index (the scene has the cull
 // only when that holds, upload_scene; the split launches' key minimum rests on the same fact) — so
 // nearer subtrees lower sc_t before farther ones are tested and cull_pass prunes those.
@@ -546,7 +547,7 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                               float& sc_t, uint32_t& sc_tri, unsigned long long& live, const uint32_t* occ_word,
                               uint32_t occ_bit, const CullRay& cq = CullRay{}) {
     constexpr bool FAST = SLAB != kSlabExact;
-    constexpr bool ORD = CULL && !ANY;
+    constexpr bool ORD = CULL && (!ANY || RTX_CULL_ORDER_ANY);
     uint32_t sp = 0;
     for (;;) {
         while (ntri == 0) {
@@ -614,7 +615,7 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                 if (ANY) {
                     live &= ~(ballot(!(rej > 0.f)) & ballot(!(t >= r.tmax)) & m);
                 } else {
-                    const bool better = ORD ? ((t < sc_t) | ((t == sc_t) & (ti < sc_tri))) : (t < sc_t);
+                    const bool better = CULL ? ((t < sc_t) | ((t == sc_t) & (ti < sc_tri))) : (t < sc_t);
                     const bool u = in & !(rej > 0.f) & !(t >= r.tmax) & better;
                     sc_t = u ? t : sc_t;
                     sc_tri = u ? ti : sc_tri;

@@ -31,6 +31,12 @@
 #define RTX_SPEC_WAVES_PARTIAL 7
 #endif
 
+// ---- formulation choices (product values; the other value is the measured alternative) ----
+// shadow-ray walks with cull records visit the child most lanes enter first (1) or left first (0)
+#ifndef RTX_CULL_ORDER_ANY
+#define RTX_CULL_ORDER_ANY 1
+#endif
+
 // ---- diagnostics (never a product build) -------------------------------------------------
 // RTX_STAMPS=1: per-wave {start, end, hw id, node-pair steps, triangle steps, lane-work}
 // stamps, read back by rtx_debug_stamps / tools/stamps.py.  RTX_STAMPS_LEAN: the stamps

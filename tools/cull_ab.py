@@ -1,6 +1,7 @@
 """A/B of the exact cull on one GPU: every BASELINE config (and the other mesh
 scenes) rendered by contexts created under different cull settings (environment variables read
-by rtx_create: RTX_NO_CULL, RTX_CULL_RATIO, RTX_CULL_LEAVES).  Checks every setting's frame is
+by rtx_create: RTX_NO_CULL, RTX_CULL_*, and the split / tile-order knobs RTX_SPLIT*, RTX_TILE_ORDER).
+CULL_AB_SCENES=a,b restricts the configs.  Checks every setting's frame is
 bit-identical to the unculled one (uint32 and float planes) and prints kernel ms/frame of each
 (rtx_time_frames: HIP events, mean over `iters` serialized launches, best of 3).
 
@@ -24,7 +25,8 @@ from gp1_raytracer_2223_amd.scene import HostScene  # noqa: E402
 
 CONFIGS = [("W4_Bunny", 1920, 1080), ("W4_Optional", 1920, 1080), ("Synthetic100k", 1920, 1080),
            ("Bunny8Lights", 3840, 2160), ("W4_Reference", 1920, 1080), ("W3", 1280, 720), ("W1", 640, 480)]
-KNOBS = ("RTX_NO_CULL", "RTX_CULL_RATIO", "RTX_CULL_LEAVES")
+KNOBS = ("RTX_NO_CULL", "RTX_CULL_RATIO", "RTX_CULL_LEAVES", "RTX_CULL_MIN_SA", "RTX_SPLIT", "RTX_SPLIT_FACTOR",
+         "RTX_SPLIT_PARTS", "RTX_TILE_ORDER")
 
 
 def ctx_with(env: dict) -> DeviceContext:
@@ -51,7 +53,10 @@ def main() -> None:
     settings = [parse(a) for a in sys.argv[3:]] or [("cull", {})]
     settings = [("no_cull", {"RTX_NO_CULL": "1"})] + settings
     rows = []
+    only = os.environ.get("CULL_AB_SCENES")
     for name, W, H in CONFIGS:
+        if only and name not in only.split(","):
+            continue
         hs = HostScene(name)
         s, cam = hs.view()
         p = abi.make_params(W, H)

@@ -234,6 +234,10 @@ static void tight_rec(walk* w, uint32_t ni) {
     }
 }
 
+/* UNSOUND measurement knob (cull_probe_cap): triangle margins above `g_cap` are clipped to it,
+   to price the heavy tail of the margin distribution (mismatches may then appear) */
+static double g_cap = INFINITY;
+void cull_probe_cap(double cap) { g_cap = cap; }
 /* per node margin = max over its triangles (camera: one value; light: NGRID values) */
 static void margin_rec(walk* w, uint32_t ni, const float* cam, const float* L) {
     const rtx_bvh_node* nd = &w->m->nodes[ni];
@@ -247,7 +251,7 @@ static void margin_rec(walk* w, uint32_t ni, const float* cam, const float* L) {
                       &w->m->positions[3 * w->m->indices[nd->first_idx + i + 1]],
                       &w->m->positions[3 * w->m->indices[nd->first_idx + i + 2]]);
             if (cam) {
-                const double g = tri_margin_camera(&T, cam);
+                const double g = fmin(tri_margin_camera(&T, cam), g_cap);
                 if (!(g <= w->marg[ni])) w->marg[ni] = g;
                 if (w->mdt) {
                     rtx_cull_tri Tc;
@@ -263,7 +267,7 @@ static void margin_rec(walk* w, uint32_t ni, const float* cam, const float* L) {
             }
             if (L)
                 for (int j = 0; j < NGRID; ++j) {
-                    const double g = tri_margin_light(&T, L, grid_t(j));
+                    const double g = fmin(tri_margin_light(&T, L, grid_t(j)), g_cap);
                     double* x = &w->lmarg[(size_t)ni * NGRID + j];
                     if (!(g <= *x)) *x = g;
                 }
