@@ -36,6 +36,11 @@
 #ifndef RTX_CULL_ORDER_ANY
 #define RTX_CULL_ORDER_ANY 1
 #endif
+// split closest hit with cull records: a part starts from the smallest key the tile's other parts
+// published (1), and re-reads it after every leaf (2), so the t-pruning sees the best t so far
+#ifndef RTX_SPLIT_SHARE_T
+#define RTX_SPLIT_SHARE_T 2
+#endif
 
 // ---- diagnostics (never a product build) -------------------------------------------------
 // RTX_STAMPS=1: per-wave {start, end, hw id, node-pair steps, triangle steps, lane-work}

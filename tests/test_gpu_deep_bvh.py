@@ -108,3 +108,24 @@ def test_hbm_stack_variant_serves_frames_of_any_size(gpu_ctx):
         rpx, _ = oracle_bind.render(s, cam, p)
         assert np.array_equal(gpx, rpx), f"{w}x{h}"
     del keep
+
+
+def test_hbm_stack_limit_is_frame_size_times_depth(gpu_ctx):
+    """The HBM stacks take (depth + 1) x 24 B for every wave of the launch:
+    a 25,000-level chain needs 0.6 GB at 64 x 32 but 77.8 GB at 3840 x 2160, past the 64 GiB cap,
+    so the 4K frame is refused with RTX_E_UNSUPPORTED before anything is allocated, and the
+    context still renders the small frame bit-exact afterwards."""
+    s, cam, keep = deep_scene(25000)
+    gpu_ctx.upload(s)
+    small = abi.make_params(64, 32)
+    rpx, _ = oracle_bind.render(s, cam, small)
+    gpx, _ = gpu_ctx.render(cam, small)
+    assert np.array_equal(gpx, rpx)
+    px = np.zeros(3840 * 2160, np.uint32)
+    rc = gpu_ctx.lib.rtx_render(gpu_ctx.h, C.byref(cam), C.byref(abi.make_params(3840, 2160)),
+                                px.ctypes.data_as(C.POINTER(C.c_uint32)), None)
+    assert rc == abi.RTX_E_UNSUPPORTED
+    assert b"exceed 64 GB" in gpu_ctx.lib.rtx_last_error(gpu_ctx.h)
+    gpx, _ = gpu_ctx.render(cam, small)
+    assert np.array_equal(gpx, rpx)
+    del keep
