@@ -200,6 +200,7 @@ typedef struct {
     double* mdt;                /* per node t bound (camera, t~ <= 64), or NULL */
     double* lmarg;              /* per node x grid margins for the current light, or NULL */
     double delta;
+    double* cone;               /* per node {axis xyz, K}: every triangle below faces away when a.d > K */
     int use_tight;
     uint64_t slabs, tris;
 } walk;
@@ -314,6 +315,53 @@ static double enter_t(const double* mn, const double* mx, double dl, const ray* 
     }
     return t0;
 }
+/* Normal-cone skip (probe of a DESIGN §9 idea): a back-face-culled mesh rejects a triangle with
+   fl(n.d) > 0 (front-face: < 0; shadow rays swap), so a node whose every normal is within theta of
+   axis a can be skipped by a ray with a.d > sin(theta + delta) + 1e-6 (delta = 1e-5 covers the
+   float dot's error).  g_cone = 1 enables it. */
+static int g_cone = 0;
+void cull_probe_cone(int on) { g_cone = on; }
+static void cone_rec(walk* w, uint32_t ni, uint32_t* first, uint32_t* cnt) {
+    const rtx_bvh_node* nd = &w->m->nodes[ni];
+    double* c = w->cone + 4 * ni;
+    uint32_t f, n;
+    if (nd->idx_count > 0) {
+        f = nd->first_idx / 3; n = nd->idx_count / 3;
+    } else {
+        uint32_t f1, n1, f2, n2;
+        cone_rec(w, nd->left_node, &f1, &n1);
+        cone_rec(w, nd->left_node + 1, &f2, &n2);
+        f = f1 < f2 ? f1 : f2; n = (f1 < f2 ? f2 + n2 : f1 + n1) - f;
+    }
+    *first = f; *cnt = n;
+    double a[3] = {0, 0, 0};
+    for (uint32_t t = f; t < f + n; ++t)
+        for (int k = 0; k < 3; ++k) a[k] += w->m->normals[3 * t + k];
+    const double l = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+    c[3] = INFINITY;
+    if (!(l > 1e-9)) return;
+    for (int k = 0; k < 3; ++k) c[k] = a[k] / l;
+    double th = 0;
+    for (uint32_t t = f; t < f + n; ++t) {
+        const float* nn = &w->m->normals[3 * t];
+        const double ln = sqrt((double)nn[0] * nn[0] + (double)nn[1] * nn[1] + (double)nn[2] * nn[2]);
+        double cs = (c[0] * nn[0] + c[1] * nn[1] + c[2] * nn[2]) / ln;
+        if (!(cs == cs)) return;
+        if (cs > 1) cs = 1;
+        const double x = acos(cs);
+        if (x > th) th = x;
+    }
+    if (th + 1e-5 < 1.5707963) c[3] = sin(th + 1e-5) + 1e-6;
+}
+static int cone_skip(const walk* w, uint32_t ni, const ray* r, int shadow) {
+    if (!g_cone || !w->cone) return 0;
+    int cull = w->m->cull_mode;
+    if (cull == RTX_CULL_NONE) return 0;
+    if (shadow) cull = cull == RTX_CULL_BACK ? RTX_CULL_FRONT : RTX_CULL_BACK;
+    const double* c = w->cone + 4 * ni;
+    const double ad = c[0] * r->d.x + c[1] * r->d.y + c[2] * r->d.z;
+    return cull == RTX_CULL_BACK ? ad > c[3] : -ad > c[3];
+}
 static int g_ordered = 0;     /* 1: nearest child first + t pruning (closest-hit), 2: also shadow rays ordered */
 static double g_tslack = 1e-3;
 void cull_probe_ordered(int o, double slack) { g_ordered = o; g_tslack = slack; }
@@ -323,6 +371,7 @@ static void visit(walk* w, uint32_t ni, const ray* r, int ignore, int* did, floa
     const rtx_bvh_node* nd = &w->m->nodes[ni];
     w->slabs++;
     if (!slab(nd->min, nd->max, r)) return;
+    if (cone_skip(w, ni, r, ignore)) return;
     if (w->use_tight) {
         const double g = node_margin(w, ni, r, ignore);
         if (isfinite(g) && !meets(w->tmn + 3 * ni, w->tmx + 3 * ni, g, r)) return;
@@ -375,7 +424,12 @@ int cull_probe(const rtx_scene* sc, const rtx_camera* cam, uint32_t W, uint32_t 
     a.tmn = (double*)malloc(sizeof(double) * 3 * m->n_nodes);
     a.tmx = (double*)malloc(sizeof(double) * 3 * m->n_nodes);
     tight_rec(&a, 0);
-    b = a; b.use_tight = 1; b.delta = delta;
+    b = a; b.use_tight = delta != 0.0; b.delta = delta;
+    if (g_cone) {
+        uint32_t f0, n0;
+        b.cone = (double*)malloc(sizeof(double) * 4 * m->n_nodes);
+        cone_rec(&b, 0, &f0, &n0);
+    }
     double* lm[16] = {0};
     if (delta < 0) {
         b.marg = (double*)malloc(sizeof(double) * m->n_nodes);
@@ -430,7 +484,7 @@ int cull_probe(const rtx_scene* sc, const rtx_camera* cam, uint32_t W, uint32_t 
         }
     }
     out[0] = a.slabs; out[1] = a.tris; out[2] = b.slabs; out[3] = b.tris;
-    free(a.tmn); free(a.tmx); free(b.marg); free(b.mdt);
+    free(a.tmn); free(a.tmx); free(b.marg); free(b.mdt); free(b.cone);
     for (int li = 0; li < 16; ++li) free(lm[li]);
     return 0;
 }
@@ -445,5 +499,81 @@ int cull_margins(const rtx_scene* sc, const rtx_camera* cam, double tm, double* 
         out_cam[i / 3] = tri_margin_camera(&T, cam->origin);
         out_light[i / 3] = tri_margin_light(&T, sc->lights[0].origin, tm);
     }
+    return 0;
+}
+
+/* Per-pixel cost map of the culled, ordered walk (the product's traversal rules), planes included:
+ * for every step-th pixel, the slab + triangle tests of its primary ray (closest of planes and the
+ * mesh) and of the shadow rays toward every light from that hit (mesh only; planes are O(1)).
+ * out_p / out_s: primary / shadow tests per sampled pixel, row-major (W/step x H/step).
+ * A wave's cost is roughly the union of its 64 lanes' visits, between the max and the sum of
+ * these per-pixel counts. */
+int cull_probe_cost_map(const rtx_scene* sc, const rtx_camera* cam, uint32_t W, uint32_t H, uint32_t step,
+                        uint32_t* out_p, uint32_t* out_s) {
+    if (sc->n_meshes != 1 || sc->n_lights > 16) return -1;
+    const rtx_mesh* m = &sc->meshes[0];
+    walk b;
+    memset(&b, 0, sizeof b);
+    b.m = m;
+    b.tmn = (double*)malloc(sizeof(double) * 3 * m->n_nodes);
+    b.tmx = (double*)malloc(sizeof(double) * 3 * m->n_nodes);
+    tight_rec(&b, 0);
+    b.use_tight = 1;
+    b.delta = -1;
+    b.marg = (double*)malloc(sizeof(double) * m->n_nodes);
+    b.mdt = (double*)malloc(sizeof(double) * m->n_nodes);
+    margin_rec(&b, 0, cam->origin, NULL);
+    double* lm[16] = {0};
+    for (uint32_t li = 0; li < sc->n_lights; ++li) {
+        lm[li] = (double*)malloc(sizeof(double) * NGRID * m->n_nodes);
+        b.lmarg = lm[li];
+        margin_rec(&b, 0, NULL, sc->lights[li].origin);
+    }
+    const float aspect = (int)W / (float)(int)H;
+    uint32_t k = 0;
+    for (uint32_t py = 0; py < H; py += step) {
+        for (uint32_t px = 0; px < W; px += step, ++k) {
+            const float cx = (2.f * (((int)px + 0.5f) / W) - 1) * aspect * cam->fov;
+            const float cy = (1.f - (2.f * ((int)py + 0.5f) / H)) * cam->fov;
+            v3 vd = mk(cam->right[0] * cx + cam->up[0] * cy + cam->forward[0] * 1.f,
+                       cam->right[1] * cx + cam->up[1] * cy + cam->forward[1] * 1.f,
+                       cam->right[2] * cx + cam->up[2] * cy + cam->forward[2] * 1.f);
+            const float mg = sqrtf(vd.x * vd.x + vd.y * vd.y + vd.z * vd.z);
+            vd.x /= mg; vd.y /= mg; vd.z /= mg;
+            const ray vr = mkray(ld3(cam->origin), vd, 0.0001f, FLT_MAX);
+            /* planes first: the scratch t the mesh walk starts from */
+            float bt = FLT_MAX;
+            v3 nrm = mk(0, 1, 0);
+            for (uint32_t i = 0; i < sc->n_planes; ++i) {
+                const v3 p0 = ld3(sc->planes[i].origin), pn = ld3(sc->planes[i].normal);
+                const float t = dot(sub(p0, vr.o), pn) / dot(vr.d, pn);
+                if (t >= vr.tmin && t < vr.tmax && t < bt) { bt = t; nrm = pn; }
+            }
+            int did = 0, bi = -1;
+            const float bt0 = bt;
+            b.slabs = b.tris = 0;
+            visit(&b, 0, &vr, 0, &did, &bt, &bi);
+            out_p[k] = (uint32_t)(b.slabs + b.tris);
+            if (bi >= 0 && bt < bt0) nrm = ld3(&m->normals[3 * (bi / 3)]);
+            out_s[k] = 0;
+            if (bt >= FLT_MAX) continue;
+            const v3 P = add(vr.o, scale(vr.d, bt));
+            const v3 oo = add(P, scale(nrm, 0.0001f));
+            b.slabs = b.tris = 0;
+            for (uint32_t li = 0; li < sc->n_lights; ++li) {
+                v3 ld = sub(ld3(sc->lights[li].origin), oo);
+                const float mag = sqrtf(ld.x * ld.x + ld.y * ld.y + ld.z * ld.z);
+                ld.x /= mag; ld.y /= mag; ld.z /= mag;
+                const ray sr = mkray(oo, ld, 0.0001f, mag);
+                int sd = 0, xi = -1;
+                float ft = FLT_MAX;
+                b.lmarg = lm[li];
+                visit(&b, 0, &sr, 1, &sd, &ft, &xi);
+            }
+            out_s[k] = (uint32_t)(b.slabs + b.tris);
+        }
+    }
+    free(b.tmn); free(b.tmx); free(b.marg); free(b.mdt);
+    for (int li = 0; li < 16; ++li) free(lm[li]);
     return 0;
 }

@@ -33,6 +33,8 @@ def main() -> None:
         L.cull_probe_ordered(int(os.environ["ORDERED"]), C.c_double(float(os.environ.get("TSLACK", "1e-3"))))
     if os.environ.get("CAP"):   # UNSOUND: clip triangle margins (prices the margin distribution's tail)
         L.cull_probe_cap(C.c_double(float(os.environ["CAP"])))
+    if os.environ.get("CONE"):
+        L.cull_probe_cone(int(os.environ["CONE"]))
     if os.environ.get("FIXED_GRID"):
         L.cull_probe_fixed_grid(int(os.environ["FIXED_GRID"]))
     hs = HostScene(name)

@@ -10,3 +10,7 @@ export RTX_HIP_LIB=gp1_raytracer_2223_amd/lib/exp/librtx_hip_stampslean.so
 timeout -k 10 90 python -u tools/stamps.py Synthetic100k 1920 1080 > gpurun_out/r04_st/syn_split.txt 2>&1
 RTX_SPLIT=0 timeout -k 10 90 python -u tools/stamps.py Synthetic100k 1920 1080 > gpurun_out/r04_st/syn_nosplit.txt 2>&1
 cat gpurun_out/r04_st/syn_split.txt gpurun_out/r04_st/syn_nosplit.txt
+STAMPS_STRIPE=16,0,8 timeout -k 10 90 python -u tools/stamps.py Synthetic100k 1920 1080 > gpurun_out/r04_st/syn_s8.txt 2>&1
+timeout -k 10 90 python -u tools/stamps.py Bunny8Lights 3840 2160 > gpurun_out/r04_st/b8_full.txt 2>&1
+STAMPS_STRIPE=16,0,8 timeout -k 10 90 python -u tools/stamps.py Bunny8Lights 3840 2160 > gpurun_out/r04_st/b8_s8.txt 2>&1
+head -12 gpurun_out/r04_st/syn_s8.txt gpurun_out/r04_st/b8_full.txt gpurun_out/r04_st/b8_s8.txt

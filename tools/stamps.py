@@ -1,6 +1,7 @@
 """Per-wave start/end stamps (diagnostic build, RTX_STAMPS=1): occupancy over time, tail,
 per-XCD balance.  Usage: RTX_HIP_LIB=.../librtx_hip_stamps.so python tools/stamps.py [scene W H]"""
 import ctypes as C
+import os
 import sys
 from pathlib import Path
 
@@ -23,7 +24,9 @@ ctx = DeviceContext(0)
 hs = HostScene(name)
 s, cam = hs.view()
 ctx.upload(s)
-p = abi.make_params(W, H)
+# STAMPS_STRIPE=rows,first,step: one rank's share of a striped frame (bench.py's strong scaling)
+stripe = [int(x) for x in os.environ.get("STAMPS_STRIPE", "0,0,1").split(",")]
+p = abi.make_params(W, H, stripe_rows=stripe[0], stripe_first=stripe[1], stripe_step=stripe[2])
 for _ in range(5):
     ctx.time_frames(cam, p, 20)
 heavy, nparts = ctx.split_info()
