@@ -577,3 +577,102 @@ int cull_probe_cost_map(const rtx_scene* sc, const rtx_camera* cam, uint32_t W, 
     for (int li = 0; li < 16; ++li) free(lm[li]);
     return 0;
 }
+
+/* Wave-packet coherence (DESIGN §3, 128-ray packets): the reference traversal (no cull) of every
+ * pixel's primary ray and its shadow rays, with the visited nodes of each tile of tw x th pixels
+ * collected in a bitset: out[0] = sum over tiles of |union of primary visits| (node tests a packet
+ * walking the union would make), out[1] = the same for the shadow rays (per light), out[2] =
+ * per-ray primary visits summed, out[3] = per-ray shadow visits summed, out[4] = tiles. */
+static uint8_t* g_mark = NULL;
+static void visit_mark(const rtx_mesh* m, uint32_t ni, const ray* r, int ignore, int* did, float* bt, uint64_t* cnt) {
+    if (ignore && *did) return;
+    const rtx_bvh_node* nd = &m->nodes[ni];
+    ++*cnt;
+    g_mark[ni] = 1;
+    if (!slab(nd->min, nd->max, r)) return;
+    if (nd->idx_count > 0) {
+        for (uint32_t i = 0; i < nd->idx_count; i += 3) {
+            const int li = (int)(nd->first_idx + i);
+            const v3 v0 = ld3(&m->positions[3 * m->indices[li]]);
+            const v3 v1 = ld3(&m->positions[3 * m->indices[li + 1]]);
+            const v3 v2 = ld3(&m->positions[3 * m->indices[li + 2]]);
+            const v3 n = ld3(&m->normals[3 * (li / 3)]);
+            float t;
+            if (tri(v0, v1, v2, n, m->cull_mode, r, ignore, &t)) {
+                *did = 1;
+                if (ignore) return;
+                if (t < *bt) *bt = t;
+            }
+        }
+    } else {
+        visit_mark(m, nd->left_node, r, ignore, did, bt, cnt);
+        visit_mark(m, nd->left_node + 1, r, ignore, did, bt, cnt);
+    }
+}
+int cull_probe_packet_union(const rtx_scene* sc, const rtx_camera* cam, uint32_t W, uint32_t H, uint32_t tw,
+                            uint32_t th, uint64_t* out) {
+    if (sc->n_meshes != 1 || sc->n_lights > 16) return -1;
+    const rtx_mesh* m = &sc->meshes[0];
+    memset(out, 0, 5 * sizeof(uint64_t));
+    uint8_t* um = (uint8_t*)malloc(m->n_nodes);
+    g_mark = (uint8_t*)malloc(m->n_nodes);
+    const float aspect = (int)W / (float)(int)H;
+    for (uint32_t ty = 0; ty + th <= H; ty += th)
+        for (uint32_t tx = 0; tx + tw <= W; tx += tw) {
+            for (int pass = 0; pass < 1 + (int)sc->n_lights; ++pass) {
+                memset(um, 0, m->n_nodes);
+                for (uint32_t py = ty; py < ty + th; ++py)
+                    for (uint32_t px = tx; px < tx + tw; ++px) {
+                        const float cx = (2.f * (((int)px + 0.5f) / W) - 1) * aspect * cam->fov;
+                        const float cy = (1.f - (2.f * ((int)py + 0.5f) / H)) * cam->fov;
+                        v3 vd = mk(cam->right[0] * cx + cam->up[0] * cy + cam->forward[0] * 1.f,
+                                   cam->right[1] * cx + cam->up[1] * cy + cam->forward[1] * 1.f,
+                                   cam->right[2] * cx + cam->up[2] * cy + cam->forward[2] * 1.f);
+                        const float mg = sqrtf(vd.x * vd.x + vd.y * vd.y + vd.z * vd.z);
+                        vd.x /= mg; vd.y /= mg; vd.z /= mg;
+                        const ray vr = mkray(ld3(cam->origin), vd, 0.0001f, FLT_MAX);
+                        float bt = FLT_MAX;
+                        v3 nrm = mk(0, 1, 0);
+                        for (uint32_t i = 0; i < sc->n_planes; ++i) {
+                            const v3 p0 = ld3(sc->planes[i].origin), pn = ld3(sc->planes[i].normal);
+                            const float t = dot(sub(p0, vr.o), pn) / dot(vr.d, pn);
+                            if (t >= vr.tmin && t < vr.tmax && t < bt) { bt = t; nrm = pn; }
+                        }
+                        int did = 0;
+                        uint64_t c = 0;
+                        memset(g_mark, 0, m->n_nodes);
+                        const float bt0 = bt;
+                        visit_mark(m, 0, &vr, 0, &did, &bt, &c);
+                        if (pass == 0) {
+                            out[2] += c;
+                            for (uint32_t i = 0; i < m->n_nodes; ++i) um[i] |= g_mark[i];
+                            continue;
+                        }
+                        if (bt >= FLT_MAX) continue;
+                        (void)bt0;
+                        const v3 P = add(vr.o, scale(vr.d, bt));
+                        const v3 oo = add(P, scale(nrm, 0.0001f));
+                        const uint32_t li = (uint32_t)pass - 1;
+                        v3 ld = sub(ld3(sc->lights[li].origin), oo);
+                        const float mag = sqrtf(ld.x * ld.x + ld.y * ld.y + ld.z * ld.z);
+                        ld.x /= mag; ld.y /= mag; ld.z /= mag;
+                        const ray sr = mkray(oo, ld, 0.0001f, mag);
+                        int sd = 0;
+                        float ft = FLT_MAX;
+                        c = 0;
+                        memset(g_mark, 0, m->n_nodes);
+                        visit_mark(m, 0, &sr, 1, &sd, &ft, &c);
+                        out[3] += c;
+                        for (uint32_t i = 0; i < m->n_nodes; ++i) um[i] |= g_mark[i];
+                    }
+                uint64_t u = 0;
+                for (uint32_t i = 0; i < m->n_nodes; ++i) u += um[i];
+                out[pass == 0 ? 0 : 1] += u;
+            }
+            out[4]++;
+        }
+    free(um);
+    free(g_mark);
+    g_mark = NULL;
+    return 0;
+}
