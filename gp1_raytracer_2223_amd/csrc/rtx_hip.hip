@@ -1356,378 +1356,6 @@ RTX_CULL_VARIANTS(2)
 RTX_CULL_VARIANTS(3)
 #undef RTX_CULL_VARIANTS
 
-// ====================================================================== 128-ray wave packets
-// The pair kernel (RTX_PAIR, kSpecVariants[0] frames without cull records): one wave renders a
-// 16 x 8 tile, every lane two pixels — A at (x, y) and B at (x + 8, y) — and the BVH walks of the
-// two 8 x 8 halves are FUSED: one scalar DFS over the union of the two packets' visits, with a
-// 64-bit lane mask per half (the node-pair step tests both rays; a child is entered when either
-// half's mask is non-empty).  Each ray visits exactly the nodes and triangles, in exactly the
-// order, of its own single-packet walk (left before right, a ray's mask bit set iff every ancestor
-// passed for that ray), so every closest hit and occlusion is the one-ray kernel's.  What it saves
-// is the scalar control per ray: the two halves' unions overlap almost entirely (W4_Bunny: 0.523
-// node tests per ray pair-packet against 1 for two packets, tools/cull_probe.c
-// cull_probe_packet_union).
-template <bool ANY, int SLAB, bool CB>
-__device__ void bvh_walk_pair(const DevScene& S, const float4* nb, float cs, const Ray& ra, const Ray& rb,
-                              uint32_t link, uint32_t ntri, unsigned long long ma, unsigned long long mb,
-                              unsigned long long maska, unsigned long long maskb, uint32_t lane, uint4* stk,
-                              float& sta, uint32_t& stria, float& stb, uint32_t& strib, unsigned long long& livea,
-                              unsigned long long& liveb) {
-    constexpr bool FAST = SLAB != kSlabExact;
-    uint32_t sp = 0;
-    for (;;) {
-        while (ntri == 0) {
-            NodePair P;
-            ldcb64(nb, link, P.l0, P.l1, P.r0, P.r1);
-            const unsigned long long mla = slab_mask<SLAB>(P.l0, P.l1, ra) & ma;
-            const unsigned long long mra = slab_mask<SLAB>(P.r0, P.r1, ra) & ma;
-            const unsigned long long mlb = slab_mask<SLAB>(P.l0, P.l1, rb) & mb;
-            const unsigned long long mrb = slab_mask<SLAB>(P.r0, P.r1, rb) & mb;
-            const bool goL = (mla | mlb) != 0ull, goR = (mra | mrb) != 0ull;
-            if (goL && goR) {   // the right child waits on the stack (two slots: both halves' masks)
-                stk[2 * sp] = make_uint4(__float_as_uint(P.r1.z), __float_as_uint(P.r1.w), static_cast<uint32_t>(mra),
-                                         static_cast<uint32_t>(mra >> 32));
-                stk[2 * sp + 1] = make_uint4(static_cast<uint32_t>(mrb), static_cast<uint32_t>(mrb >> 32), 0u, 0u);
-                ++sp;
-            }
-            // next: left, else right, else a dead end taken as an empty leaf (ntri = 1, no lanes)
-            const unsigned long long nx = goL ? link_ntri(P.l1) : (goR ? link_ntri(P.r1) : (1ull << 32));
-            ma = goL ? mla : mra;
-            mb = goL ? mlb : mrb;
-            link = static_cast<uint32_t>(nx);
-            ntri = opaque(static_cast<uint32_t>(nx >> 32));
-        }
-        if (ma | mb) {
-            const bool ina = (ma >> lane) & 1ull, inb = (mb >> lane) & 1ull;
-            for (uint32_t k = 0; k < ntri; ++k) {
-                const uint32_t ti = link + k * 64u;
-                Tri T;
-                ldcb64(S.tris, ti, T.a, T.b, T.c, T.d);
-                float t, rej;
-                if (ma && tri_t_wave<FAST, CB, ANY>(T.a, T.b, T.c, cs, ra, ANY ? (ma & livea) : ma, rej, t)) {
-                    if (ANY) {
-                        livea &= ~(ballot(!(rej > 0.f)) & ballot(!(t >= ra.tmax)) & ma);
-                    } else {
-                        const bool u = ina & !(rej > 0.f) & !(t >= ra.tmax) & (t < sta);
-                        sta = u ? t : sta;
-                        stria = u ? ti : stria;
-                    }
-                }
-                if (mb && tri_t_wave<FAST, CB, ANY>(T.a, T.b, T.c, cs, rb, ANY ? (mb & liveb) : mb, rej, t)) {
-                    if (ANY) {
-                        liveb &= ~(ballot(!(rej > 0.f)) & ballot(!(t >= rb.tmax)) & mb);
-                    } else {
-                        const bool u = inb & !(rej > 0.f) & !(t >= rb.tmax) & (t < stb);
-                        stb = u ? t : stb;
-                        strib = u ? ti : strib;
-                    }
-                }
-                if (ANY) {   // a half whose lanes are all occluded stops testing
-                    ma &= livea;
-                    mb &= liveb;
-                }
-            }
-            if (ANY && (livea & maska) == 0 && (liveb & maskb) == 0) return;
-        }
-        for (;;) {   // pop the next pending right child
-            if (sp == 0) return;
-            --sp;
-            const uint4 e = stk[2 * sp], f = stk[2 * sp + 1];
-            link = uni(e.x);
-            ntri = uni(e.y);
-            ma = (static_cast<unsigned long long>(uni(e.w)) << 32) | uni(e.z);
-            mb = (static_cast<unsigned long long>(uni(f.y)) << 32) | uni(f.x);
-            if (ANY) {
-                ma &= livea;
-                mb &= liveb;
-            }
-            if (ma | mb) break;
-        }
-    }
-}
-
-// One mesh for both halves: the fused walk when both batches are FAST and share a node copy
-// (the octant copy both halves' octants select, else copy 0 with the FAST slab form), else each
-// half alone through mesh_traverse (the one-packet path).
-template <bool ANY, bool CB>
-__device__ __forceinline__ void mesh_traverse_pair(const DevScene& S, const int4 M, const Ray& ra, const Ray& rb, bool fa,
-                                                   bool fb, int octa, int octb, unsigned long long maska,
-                                                   unsigned long long maskb, uint32_t lane, uint4* stk, float& sta,
-                                                   uint32_t& stria, float& stb, uint32_t& strib,
-                                                   unsigned long long& livea, unsigned long long& liveb) {
-    if (M.y == 0) return;
-    Counts cnt;
-    if (!(fa && fb)) {   // a half outside the FAST domain: one packet at a time, the exact form where needed
-        unsigned long long* sT = nullptr;
-        if (maska) {
-            if (octa >= 0) mesh_traverse<ANY, kSlabOct, false, CB>(S, M, ra, octa, maska, lane, stk, sT, sta, stria, livea, cnt);
-            else if (fa) mesh_traverse<ANY, kSlabFast, false, CB>(S, M, ra, 0, maska, lane, stk, sT, sta, stria, livea, cnt);
-            else mesh_traverse<ANY, kSlabExact, false, CB>(S, M, ra, 0, maska, lane, stk, sT, sta, stria, livea, cnt);
-        }
-        if (maskb) {
-            if (octb >= 0) mesh_traverse<ANY, kSlabOct, false, CB>(S, M, rb, octb, maskb, lane, stk, sT, stb, strib, liveb, cnt);
-            else if (fb) mesh_traverse<ANY, kSlabFast, false, CB>(S, M, rb, 0, maskb, lane, stk, sT, stb, strib, liveb, cnt);
-            else mesh_traverse<ANY, kSlabExact, false, CB>(S, M, rb, 0, maskb, lane, stk, sT, stb, strib, liveb, cnt);
-        }
-        return;
-    }
-    const int oct = (octa >= 0 && (octa == octb || maskb == 0)) ? octa : ((octb >= 0 && maska == 0) ? octb : -1);
-    const float cs = cull_sign(M.z, ANY);
-    if (oct >= 0) {
-        const float4* nb = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.nodes) +
-                                                           static_cast<uint32_t>(oct) * S.oct_bytes);
-        float4 b0, b1;
-        ldcb32(nb, static_cast<uint32_t>(M.x), b0, b1);
-        const unsigned long long ma = slab_mask<kSlabOct>(b0, b1, ra) & maska;
-        const unsigned long long mb = slab_mask<kSlabOct>(b0, b1, rb) & maskb;
-        if ((ma | mb) == 0) return;
-        bvh_walk_pair<ANY, kSlabOct, CB>(S, nb, cs, ra, rb, __float_as_uint(b1.z), __float_as_uint(b1.w), ma, mb, maska,
-                                         maskb, lane, stk, sta, stria, stb, strib, livea, liveb);
-    } else {
-        float4 b0, b1;
-        ldcb32(S.nodes, static_cast<uint32_t>(M.x), b0, b1);
-        const unsigned long long ma = slab_mask<kSlabFast>(b0, b1, ra) & maska;
-        const unsigned long long mb = slab_mask<kSlabFast>(b0, b1, rb) & maskb;
-        if ((ma | mb) == 0) return;
-        bvh_walk_pair<ANY, kSlabFast, CB>(S, S.nodes, cs, ra, rb, __float_as_uint(b1.z), __float_as_uint(b1.w), ma, mb,
-                                          maska, maskb, lane, stk, sta, stria, stb, strib, livea, liveb);
-    }
-}
-
-// Per-pixel state of one half of the pair tile.
-struct PairPix {
-    int px, py;
-    bool valid;
-    float dx, dy, dz;
-    Ray vr;
-    bool fast;
-    int oct;
-    unsigned long long active;
-    float best_t, sc_t;
-    uint32_t best_kind, best_idx, sc_tri;
-};
-
-// SPEC: kSpecVariants[0] (Lambert only, point lights, one back-face-culled mesh, no spheres, the
-// room's five planes, Combined lighting with shadows); PHASE 0 only, no split, no cull records.
-template <int SPEC>
-__global__ void __launch_bounds__(kBlockThreads, RTX_PAIR_WAVES) rtx_render_pair_kernel(const DevScene S, const FrameArgs F) {
-    static_assert(SPEC == kSpecVariants[0], "the pair kernel is compiled for the Lambert one-mesh variant");
-    constexpr int kKinds = SPEC & kSpecKindAll;
-    constexpr bool kCullBack = (SPEC & kSpecCullBack) != 0;
-    __shared__ uint4 stkE[kBlockThreads / 64][2 * kStackDepth];
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint4* stk = stkE[wave];
-    const uint32_t widx = blockIdx.x * kWavesPerBlock + wave;
-    if (widx >= F.n_tiles) return;
-    const uint32_t tile = F.order ? ldc(F.order, widx) : widx;
-    const uint32_t per_view = F.tiles_x * F.tiles_y;
-    const uint32_t view = tile / per_view;
-    const uint32_t rem = tile - view * per_view;
-    const uint32_t bx = rem % F.tiles_x;
-    const ViewCam& V = F.cam[view];
-    uint32_t gy = rem / F.tiles_x;
-    unsigned long long t_block0 = 0;
-    if (F.cost) t_block0 = __builtin_amdgcn_s_memtime();
-    if (F.groups_per_stripe) {
-        const uint32_t first = (F.stripe_first + F.stripe_step - view % F.stripe_step) % F.stripe_step;
-        const uint32_t k = gy / F.groups_per_stripe, sub = gy % F.groups_per_stripe;
-        gy = (first + k * F.stripe_step) * F.groups_per_stripe + sub;
-    }
-    const int W = static_cast<int>(F.width), H = static_cast<int>(F.height);
-    const float fW = static_cast<float>(W), fH = static_cast<float>(H);
-    PairPix P[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {   // ---- primary rays (Renderer.cpp:104-114), as the one-packet kernel
-        PairPix& Q = P[h];
-        Q.px = static_cast<int>(bx * 2u * kWaveTile + h * kWaveTile + (lane & 7u));
-        Q.py = static_cast<int>(gy * kWaveTile + (lane >> 3));
-        Q.valid = Q.px < W && Q.py < H;
-        const float cx = (2.f * div_rn(Q.px + 0.5f, fW, F.inv_width) - 1) * F.aspect * V.fov;
-        const float cy = (1.f - div_rn(2.f * (Q.py + 0.5f), fH, F.inv_height)) * V.fov;
-        float dx = V.right[0] * cx + V.up[0] * cy + V.forward[0] * 1.f;
-        float dy = V.right[1] * cx + V.up[1] * cy + V.forward[1] * 1.f;
-        float dz = V.right[2] * cx + V.up[2] * cy + V.forward[2] * 1.f;
-        const float dm = sqrtf(dx * dx + dy * dy + dz * dz);
-        div3_exact(dx, dy, dz, dm);
-        Q.dx = dx; Q.dy = dy; Q.dz = dz;
-        unsigned long long vslow;
-        Q.vr = make_ray(V.origin[0], V.origin[1], V.origin[2], dx, dy, dz, 0.0001f, FLT_MAX, vslow);
-        Q.active = ballot(Q.valid);
-        Q.fast = (Q.active & vslow) == 0 && S.tri_fast;
-        Q.oct = (Q.fast && S.oct_bytes && Q.active) ? batch_octant(Q.vr, Q.active) : -1;
-        // ---- Scene::GetClosestHit (Scene.cpp:29-66): the room's planes, then the mesh
-        Q.best_t = FLT_MAX; Q.sc_t = FLT_MAX; Q.best_kind = 0; Q.best_idx = 0; Q.sc_tri = 0;
-        const bool room_p = (Q.active & ~ballot(finite3(Q.vr.ox, Q.vr.oy, Q.vr.oz))) == 0;
-        if (room_p) {
-            const ViewCam& VU = F.cam[uni(view)];
-            const bool mk = Q.fast && VU.room_fast;
-            for_room_planes([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                constexpr int A = kRoomAxes[k];
-                float t;
-                if (mk) {
-                    t = div_rn(VU.room_a[k], room_d<A>(Q.vr), room_inv<A>(Q.vr));
-                } else {
-                    float4 p0, p1;
-                    ldcb32(S.planes, k * 32u, p0, p1);
-                    t = room_a<A>(p0, Q.vr) / room_d<A>(Q.vr);
-                }
-                const bool hh = Q.valid & (t >= Q.vr.tmin) & (t < Q.vr.tmax);
-                Q.sc_t = hh ? t : Q.sc_t;
-                const bool bb = hh & (t < Q.best_t);
-                Q.best_t = bb ? t : Q.best_t;
-                Q.best_kind = bb ? 2u : Q.best_kind;
-                Q.best_idx = bb ? static_cast<uint32_t>(k * 32) : Q.best_idx;
-            });
-        } else {
-            for (uint32_t i = 0; i < 5u * 32u; i += 32u) {
-                float4 p0, p1;
-                ldcb32(S.planes, opaque(i), p0, p1);
-                const float num = plane_num(p0, p1, Q.vr), den = plane_den(p1, Q.vr);
-                const float t = num / den;
-                const bool hh = Q.valid & (t >= Q.vr.tmin) & (t < Q.vr.tmax);
-                Q.sc_t = hh ? t : Q.sc_t;
-                const bool bb = hh & (t < Q.best_t);
-                Q.best_t = bb ? t : Q.best_t;
-                Q.best_kind = bb ? 2u : Q.best_kind;
-                Q.best_idx = bb ? i : Q.best_idx;
-            }
-        }
-    }
-    {   // the mesh, both halves in one walk
-        const int4 M = ldcb16i(S.meshes, 0u);
-        unsigned long long ua = 0, ub = 0;
-        mesh_traverse_pair<false, kCullBack>(S, M, P[0].vr, P[1].vr, P[0].fast, P[1].fast, P[0].oct, P[1].oct,
-                                             P[0].active, P[1].active, lane, stk, P[0].sc_t, P[0].sc_tri, P[1].sc_t,
-                                             P[1].sc_tri, ua, ub);
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-            if (P[h].sc_t < P[h].best_t) { P[h].best_t = P[h].sc_t; P[h].best_kind = 3; P[h].best_idx = P[h].sc_tri; }
-    }
-    // ---- hit records (Utils.h:62-64), shadow-ray set-up
-    float hx[2], hy[2], hz[2], nx[2], ny[2], nz[2], oox[2], ooy[2], ooz[2];
-    uint32_t mat[2];
-    bool did[2];
-    unsigned long long hitmask[2];
-    bool room_s[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const PairPix& Q = P[h];
-        did[h] = Q.best_kind != 0;
-        hx[h] = hy[h] = hz[h] = nx[h] = ny[h] = nz[h] = 0.f;
-        mat[h] = 0;
-        if (did[h]) {
-            hx[h] = Q.vr.ox + Q.vr.dx * Q.best_t; hy[h] = Q.vr.oy + Q.vr.dy * Q.best_t; hz[h] = Q.vr.oz + Q.vr.dz * Q.best_t;
-            if (Q.best_kind == 2) {
-                float4 p0, p1;
-                ldcb32(S.planes, Q.best_idx, p0, p1);
-                nx[h] = p1.x; ny[h] = p1.y; nz[h] = p1.z;
-                mat[h] = __float_as_uint(p0.w);
-            } else {
-                Tri T;
-                ldcb64(S.tris, Q.best_idx, T.a, T.b, T.c, T.d);
-                nx[h] = T.a.w; ny[h] = T.b.w; nz[h] = T.c.w;
-                mat[h] = __float_as_uint(T.d.x);
-            }
-        }
-        hitmask[h] = ballot(did[h]);
-        oox[h] = hx[h] + nx[h] * 0.0001f; ooy[h] = hy[h] + ny[h] * 0.0001f; ooz[h] = hz[h] + nz[h] * 0.0001f;
-        room_s[h] = (hitmask[h] & ~ballot(finite3(oox[h], ooy[h], ooz[h]))) == 0;
-    }
-    float shadowFactor[2] = {1.f, 1.f};
-    float fr[2] = {0.f, 0.f}, fg[2] = {0.f, 0.f}, fb[2] = {0.f, 0.f};
-    if (hitmask[0] | hitmask[1]) {
-        for (uint32_t li = 0; li < S.n_lights; ++li) {
-            float4 L0, L1;
-            ldcb32(S.lights, opaque(li * 32u), L0, L1);
-            float lx[2], ly[2], lz[2];
-            Ray sr[2];
-            bool sfast[2];
-            int soct[2];
-            unsigned long long live[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {   // Scene::DoesHit (Scene.cpp:68-96) on Ray{originOffset, l, 1e-4, |l|}
-                lx[h] = L0.x - oox[h]; ly[h] = L0.y - ooy[h]; lz[h] = L0.z - ooz[h];
-                const float mag = sqrtf(lx[h] * lx[h] + ly[h] * ly[h] + lz[h] * lz[h]);
-                div3_exact(lx[h], ly[h], lz[h], mag);
-                unsigned long long sslow;
-                sr[h] = make_ray(oox[h], ooy[h], ooz[h], lx[h], ly[h], lz[h], 0.0001f, mag, sslow);
-                live[h] = hitmask[h];
-                sfast[h] = (hitmask[h] & sslow) == 0 && S.tri_fast;
-                soct[h] = (sfast[h] && S.oct_bytes && hitmask[h]) ? batch_octant(sr[h], hitmask[h]) : -1;
-                if (room_s[h]) {
-                    for_room_planes([&](auto kc) {
-                        constexpr int k = decltype(kc)::value;
-                        constexpr int A = kRoomAxes[k];
-                        float4 p0, p1;
-                        ldcb32(S.planes, k * 32u, p0, p1);
-                        const float num = room_a<A>(p0, sr[h]), den = room_d<A>(sr[h]);
-                        const unsigned long long cand = plane_cand(num, den, sr[h].tmax) & live[h];
-                        if (!cand) return;
-                        const float t = num / den;
-                        live[h] &= ~(ballot(t >= sr[h].tmin) & ballot(t < sr[h].tmax) & cand);
-                    });
-                } else {
-                    for (uint32_t i = 0; i < 5u * 32u; i += 32u) {
-                        float4 p0, p1;
-                        ldcb32(S.planes, opaque(i), p0, p1);
-                        const float num = plane_num(p0, p1, sr[h]), den = plane_den(p1, sr[h]);
-                        const unsigned long long cand = plane_cand(num, den, sr[h].tmax) & live[h];
-                        if (!cand) continue;
-                        const float t = num / den;
-                        live[h] &= ~(ballot(t >= sr[h].tmin) & ballot(t < sr[h].tmax) & cand);
-                    }
-                }
-            }
-            if (live[0] | live[1]) {
-                const int4 M = ldcb16i(S.meshes, 0u);
-                float sa = 0.f, sb = 0.f;
-                uint32_t ta = 0, tb = 0;
-                const unsigned long long la = live[0], lb = live[1];
-                mesh_traverse_pair<true, kCullBack>(S, M, sr[0], sr[1], sfast[0], sfast[1], soct[0], soct[1], la, lb, lane,
-                                                    stk, sa, ta, sb, tb, live[0], live[1]);
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (!did[h]) continue;
-                if (!((live[h] >> lane) & 1ull)) {
-                    shadowFactor[h] *= 0.95f;
-                    continue;
-                }
-                // LightUtils::GetRadiance (Utils.h:355-369), point light, at hit.origin; Lambert
-                const float ex = L0.x - hx[h], ey = L0.y - hy[h], ez = L0.z - hz[h];
-                const float s = L1.w / (ex * ex + ey * ey + ez * ez);
-                const float rr = L1.x * s, rg = L1.y * s, rb = L1.z * s;
-                const float oa = smax(nx[h] * lx[h] + ny[h] * ly[h] + nz[h] * lz[h], 0.f);
-                Counts cnt;
-                const RGB br = shade<kKinds>(S, mat[h], nx[h], ny[h], nz[h], lx[h], ly[h], lz[h], -P[h].dx, -P[h].dy,
-                                             -P[h].dz, cnt, false);
-                fr[h] += (rr * oa) * br.r; fg[h] += (rg * oa) * br.g; fb[h] += (rb * oa) * br.b;
-            }
-        }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        float r = fr[h], g = fg[h], b = fb[h];
-        if (did[h]) { r *= shadowFactor[h]; g *= shadowFactor[h]; b *= shadowFactor[h]; }
-        const float mv = smax(r, smax(g, b));   // ColorRGB::MaxToOne (ColorRGB.h:12-17)
-        if (mv > 1.f) { r /= mv; g /= mv; b /= mv; }
-        if (P[h].valid) {
-            const size_t o = static_cast<size_t>(view) * F.width * F.height + static_cast<size_t>(P[h].py) * F.width +
-                             static_cast<size_t>(P[h].px);
-            F.out_px[o] = (q8(r) << F.rshift) | (q8(g) << F.gshift) | (q8(b) << F.bshift) | F.amask;
-            if (F.out_rgb) {
-                F.out_rgb[3 * o] = r; F.out_rgb[3 * o + 1] = g; F.out_rgb[3 * o + 2] = b;
-            }
-        }
-    }
-    if (F.cost && lane == 0) {
-        const unsigned long long dt = (__builtin_amdgcn_s_memtime() - t_block0) >> 4;
-        atomicMax(&F.cost[tile], static_cast<uint32_t>(dt < 0xffffffffull ? dt : 0xffffffffull));
-    }
-}
-template __global__ void rtx_render_pair_kernel<kSpecVariants[0]>(const DevScene, const FrameArgs);
-
 // Octant copies 1..7 of an uploaded node array from copy 0 (blockIdx.y + 1 = octant k):
 // copy k stores (hi, lo) on the axes set in k, the same swap the host applies for small
 // arrays (upload_scene).  Zero padding maps to zero padding.  `n2` node records of 32 B per
@@ -2147,9 +1775,6 @@ struct rtx_ctx {
     int scene_spec = 0;              // kSpec* facts of the uploaded scene (kernel specialisation)
     float room_p0[5] = {};           // kSpecRoomPlanes: plane k's origin on axis kRoomAxes[k]
     bool no_spec = false;            // RTX_NO_SPEC=1: always the generic kernel (tests)
-    bool pair_mode = false;          // RTX_PAIR=1: the 128-ray pair kernel where it applies (rtx_render_pair_kernel)
-    bool frame_pair = false;         // the prepared frame runs the pair kernel (16 x 8 tiles)
-    uint32_t sched_ntiles = 0;       // tiles of the prepared launch shape (rtx_schedule_state)
     unsigned long long* d_hit_key = nullptr;
     uint32_t* d_occ = nullptr;
     // exact cull (DevScene::cull): on for host uploads (RTX_NO_CULL=1: off); the
@@ -2294,7 +1919,6 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     if (const char* e = std::getenv("RTX_TILE_ORDER")) c->sched_enabled = std::strcmp(e, "0") != 0;
     // RTX_SPLIT=0 renders heavy tiles in one piece; RTX_SPLIT=force splits every tile
     if (const char* e = std::getenv("RTX_NO_SPEC")) c->no_spec = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("RTX_PAIR")) c->pair_mode = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_NO_CULL")) c->no_cull = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_CULL_RATIO")) {
         const double v = std::atof(e);
@@ -2903,11 +2527,8 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
 
 namespace {
 
-int spec_variant(int facts);
-
-// allow_pair: the frame may run the pair kernel (not the instrumented or stamped launches)
 int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_params* p, bool want_rgb, FrameArgs& F,
-            dim3& grid, bool allow_pair = true) {
+            dim3& grid) {
     if (!c || !cams || !p) return RTX_E_INVALID;
     if (n_views < 1 || n_views > kMaxViews) return fail(c, RTX_E_INVALID, "n_views must be 1..8");
     if (!c->has_scene) return fail(c, RTX_E_STATE, "no scene uploaded");
@@ -2985,21 +2606,13 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         F.groups_per_stripe = gps; F.stripe_first = p->stripe_first; F.stripe_step = p->stripe_step;
         gy = owned * gps;
     }
-    // The pair kernel (16 x 8 tiles, two pixels per lane) for frames of the Lambert one-mesh variant
-    // without cull records, unless the split is forced (RTX_SPLIT=force: tests of the split path)
-    const int facts = c->scene_spec | ((p->lighting_mode == RTX_MODE_COMBINED && p->shadows_enabled) ? kSpecCombShadows : 0);
-    const bool pair = allow_pair && c->pair_mode && !c->no_spec && !c->deep_stack && !c->hbm_stack &&
-                      !c->dev.cull_stride && c->split_mode != 2 && spec_variant(facts) == 0;
-    c->frame_pair = pair;
-    const uint32_t tile_w = (pair ? 2u : 1u) * kWaveTile;
-    F.tiles_x = (p->width + tile_w - 1) / tile_w;
+    F.tiles_x = (p->width + kWaveTile - 1) / kWaveTile;
     F.tiles_y = gy;
     F.out_px = c->d_px;
     F.out_rgb = want_rgb ? c->d_rgb : nullptr;
     F.counters = c->d_counters;
     const uint32_t ntiles = F.tiles_x * gy * static_cast<uint32_t>(n_views);
     F.n_tiles = ntiles;
-    c->sched_ntiles = ntiles;
     const uint32_t nblocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
     grid = dim3(nblocks, 1, 1);
     // Cost-ordered dispatch (see the kernel): keep one order/cost pair per launch shape.
@@ -3030,7 +2643,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     std::string key = std::to_string(p->width) + "x" + std::to_string(p->height) + "v" + std::to_string(n_views) +
                       "s" + std::to_string(p->stripe_rows) + "/" + std::to_string(p->stripe_first) + "/" +
                       std::to_string(p->stripe_step) + "g" + c->scene_sig + "m" +
-                      std::to_string(p->lighting_mode) + std::to_string(p->shadows_enabled) + (pair ? "P" : "");
+                      std::to_string(p->lighting_mode) + std::to_string(p->shadows_enabled);
     if (key != c->sched_key) {   // new shape or scene: identity order, fresh costs, no split
         if (c->heavy_pending) HIP_TRY(c, hipEventSynchronize(c->ev_heavy));
         c->heavy_pending = false;
@@ -3046,7 +2659,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         c->heavy_n = std::min<uint32_t>(*c->h_heavy_n, kMaxHeavyTiles);
         c->heavy_cur ^= 1;
     }
-    const bool split = c->split_mode != 0 && c->split_ok && c->sched_enabled && c->heavy_n > 0 && !pair;
+    const bool split = c->split_mode != 0 && c->split_ok && c->sched_enabled && c->heavy_n > 0;
     F.heavy_flag = split ? c->d_heavy_flag[c->heavy_cur] : nullptr;
     F.heavy_list = c->d_heavy_list[c->heavy_cur];
     F.heavy_n = split ? c->heavy_n : 0u;
@@ -3165,8 +2778,6 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, true, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
     else if (c->deep_stack)
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
-    else if (c->frame_pair)
-        hipLaunchKernelGGL((rtx_render_pair_kernel<kSpecVariants[0]>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
     else
         launch_phase<0>(v, grid, c->stream, c->dev, F);
     HIP_TRY(c, hipGetLastError());
@@ -3366,7 +2977,7 @@ extern "C" int rtx_count_work_ex(rtx_ctx* c, const rtx_camera* cam, const rtx_re
     if (n_counts > kNumCounters) n_counts = kNumCounters;
     FrameArgs F;
     dim3 grid;
-    int rc = prepare(c, cam, 1, p, false, F, grid, false);
+    int rc = prepare(c, cam, 1, p, false, F, grid);
     if (rc != RTX_OK) return rc;
     HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long) * kNumCounters, c->stream));
     rc = launch(c, F, grid, true);
@@ -3382,9 +2993,9 @@ extern "C" int rtx_count_work_ex(rtx_ctx* c, const rtx_camera* cam, const rtx_re
 
 extern "C" int rtx_schedule_state(rtx_ctx* c, uint32_t* order, uint32_t* cost, uint32_t n, uint32_t* n_tiles) {
     if (!c) return RTX_E_INVALID;
-    if (n_tiles) *n_tiles = c->sched_ready ? c->sched_ntiles : 0u;
+    if (n_tiles) *n_tiles = c->sched_ready ? c->sched_cap : 0u;
     if (!c->sched_ready || !order || !cost) return RTX_OK;
-    if (n > c->sched_ntiles) return fail(c, RTX_E_INVALID, "n exceeds the schedule size");
+    if (n > c->sched_cap) return fail(c, RTX_E_INVALID, "n exceeds the schedule size");
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipMemcpy(order, c->d_order, n * 4, hipMemcpyDeviceToHost));
@@ -3418,7 +3029,7 @@ extern "C" int rtx_debug_stamps(rtx_ctx* c, const rtx_camera* cam, const rtx_ren
                                 uint64_t capacity, uint64_t* n_waves) {
     FrameArgs F;
     dim3 grid;
-    int rc = prepare(c, cam, 1, p, false, F, grid, false);
+    int rc = prepare(c, cam, 1, p, false, F, grid);
     if (rc != RTX_OK) return rc;
     const uint64_t nw = F.n_tiles;   // one record per wave tile
     *n_waves = nw;

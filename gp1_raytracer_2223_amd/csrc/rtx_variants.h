@@ -30,11 +30,6 @@
 #ifndef RTX_SPEC_WAVES_PARTIAL
 #define RTX_SPEC_WAVES_PARTIAL 7
 #endif
-// the pair kernel (128-ray packets): 7 waves per SIMD = 69 VGPRs, no scratch (8: 64 VGPRs + 44 B
-// of scratch spills)
-#ifndef RTX_PAIR_WAVES
-#define RTX_PAIR_WAVES 7
-#endif
 
 // ---- formulation choices (product values; the other value is the measured alternative) ----
 // shadow-ray walks with cull records visit the child most lanes enter first (1) or left first (0)

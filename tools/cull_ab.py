@@ -26,7 +26,7 @@ from gp1_raytracer_2223_amd.scene import HostScene  # noqa: E402
 CONFIGS = [("W4_Bunny", 1920, 1080), ("W4_Optional", 1920, 1080), ("Synthetic100k", 1920, 1080),
            ("Bunny8Lights", 3840, 2160), ("W4_Reference", 1920, 1080), ("W3", 1280, 720), ("W1", 640, 480)]
 KNOBS = ("RTX_NO_CULL", "RTX_CULL_RATIO", "RTX_CULL_LEAVES", "RTX_CULL_MIN_SA", "RTX_SPLIT", "RTX_SPLIT_FACTOR",
-         "RTX_SPLIT_PARTS", "RTX_TILE_ORDER", "RTX_PAIR")
+         "RTX_SPLIT_PARTS", "RTX_TILE_ORDER")
 
 
 def ctx_with(env: dict) -> DeviceContext:
