@@ -13,7 +13,8 @@
 // Experiments that lost their A/B were deleted from the kernel rather than kept behind a
 // switch; their records stay under profiles/ (profiles/r01/ablate_history.md, profiles/r03/
 // ab_*.txt): the plane-skip of primary rays, the touch prefetch of child records, XCD bands
-// and XCD runs, the early sphere-loop exit, the unfused triangle test, the non-asm child select.
+// and XCD runs, the early sphere-loop exit, the unfused triangle test, the non-asm child select;
+// round 4: the 128-ray pair kernel and the culled walks' prefetch touches (profiles/r04/).
 #ifndef RTX_VARIANTS_H
 #define RTX_VARIANTS_H
 

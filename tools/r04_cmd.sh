@@ -1,17 +1,8 @@
-# round-4 GPU session script: parity suite, pair-kernel A/B, timelines (tools/, not product)
-mkdir -p gpurun_out/r04_pair
-RTX_PAIR=1 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > gpurun_out/r04_pair/tests.log 2>&1; rc=$?
-tail -3 gpurun_out/r04_pair/tests.log
-[ $rc -ne 0 ] && { grep -n "FAILED\|Error\|assert" gpurun_out/r04_pair/tests.log | head -20; exit 1; }
-export CULL_AB_SCENES=W4_Bunny,Bunny8Lights,Synthetic100k,W4_Optional
-timeout -k 10 200 python -u tools/cull_ab.py 100 - cull= pair=RTX_PAIR:1 > gpurun_out/r04_pair/ab.log 2>&1
-cut -c1-330 gpurun_out/r04_pair/ab.log
-RTX_HIP_LIB=gp1_raytracer_2223_amd/lib/exp/librtx_hip_pw8.so CULL_AB_SCENES=W4_Bunny,Bunny8Lights timeout -k 10 100 python -u tools/cull_ab.py 100 - pair=RTX_PAIR:1 > gpurun_out/r04_pair/ab_pw8.log 2>&1
-cut -c1-200 gpurun_out/r04_pair/ab_pw8.log
-export RTX_HIP_LIB=gp1_raytracer_2223_amd/lib/exp/librtx_hip_stampslean.so
-unset CULL_AB_SCENES
-timeout -k 10 60 python -u tools/stamps.py Synthetic100k 1920 1080 > gpurun_out/r04_pair/st_syn.txt 2>&1
-STAMPS_STRIPE=16,0,8 timeout -k 10 60 python -u tools/stamps.py Synthetic100k 1920 1080 > gpurun_out/r04_pair/st_syn_s8.txt 2>&1
-timeout -k 10 60 python -u tools/stamps.py Bunny8Lights 3840 2160 > gpurun_out/r04_pair/st_b8.txt 2>&1
-STAMPS_STRIPE=16,0,8 timeout -k 10 60 python -u tools/stamps.py Bunny8Lights 3840 2160 > gpurun_out/r04_pair/st_b8_s8.txt 2>&1
-head -8 gpurun_out/r04_pair/st_*.txt
+# round-4 GPU session script: split-phase key sharing and part count A/B (tools/, not product)
+mkdir -p gpurun_out/r04_sh
+for L in share0 product; do
+  if [ $L = product ]; then unset RTX_HIP_LIB; else export RTX_HIP_LIB=gp1_raytracer_2223_amd/lib/exp/librtx_hip_$L.so; fi
+  timeout -k 10 150 python -u tools/share_probe.py Synthetic100k 1920 1080 p64=RTX_SPLIT_PARTS:64 p256=RTX_SPLIT_PARTS:256 > gpurun_out/r04_sh/share_$L.log 2>&1
+  CULL_AB_SCENES=W4_Optional,Synthetic100k timeout -k 10 120 python -u tools/cull_ab.py 50 - cull= p64=RTX_SPLIT_PARTS:64 p256=RTX_SPLIT_PARTS:256 > gpurun_out/r04_sh/ab_$L.log 2>&1
+  echo "== $L"; cut -c1-400 gpurun_out/r04_sh/share_$L.log; cut -c1-330 gpurun_out/r04_sh/ab_$L.log
+done
