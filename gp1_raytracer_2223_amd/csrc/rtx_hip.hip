@@ -545,8 +545,7 @@ template <bool ANY, int SLAB, bool CB = false, bool CULL = false>
 __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, const Ray& r, uint32_t link,
                               uint32_t ntri, unsigned long long m, unsigned long long mask, uint32_t lane, uint4* stk,
                               float& sc_t, uint32_t& sc_tri, unsigned long long& live, const uint32_t* occ_word,
-                              uint32_t occ_bit, const CullRay& cq = CullRay{},
-                              const unsigned long long* key_word = nullptr) {
+                              uint32_t occ_bit, const CullRay& cq = CullRay{}) {
     constexpr bool FAST = SLAB != kSlabExact;
     constexpr bool ORD = CULL && (!ANY || RTX_CULL_ORDER_ANY);
     uint32_t sp = 0;
@@ -627,14 +626,6 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                 live &= ~ballot((o & occ_bit) != 0u);
             }
             if (ANY && (live & mask) == 0) return;
-            if (!ANY && CULL && RTX_SPLIT_SHARE_T >= 2 && key_word) {
-                // split closest hit: adopt a smaller key another part has published (a real
-                // candidate of the same pixel), so cull_pass prunes against the best t so far
-                const unsigned long long k = __hip_atomic_load(key_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const bool take = k < ((static_cast<unsigned long long>(__float_as_uint(sc_t)) << 32) | sc_tri);
-                sc_t = take ? __uint_as_float(static_cast<uint32_t>(k >> 32)) : sc_t;
-                sc_tri = take ? static_cast<uint32_t>(k) : sc_tri;
-            }
         }
         for (;;) {
             if (sp == 0) return;
@@ -698,7 +689,7 @@ template <bool ANY, int SLAB, bool CB = false, bool CULL = false>
 __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int oct, unsigned long long mask,
                               uint32_t lane, uint4* stk, float& sc_t, uint32_t& sc_tri, unsigned long long& live,
                               Counts& cnt, const uint32_t* occ_word = nullptr, uint32_t occ_bit = 0,
-                              const CullRay& cq = CullRay{}, const unsigned long long* key_word = nullptr) {
+                              const CullRay& cq = CullRay{}) {
     static_assert(!CULL || SLAB != kSlabExact, "the cull runs in FAST batches only");
     constexpr bool FAST = SLAB != kSlabExact;
     if (E.x < 0) return;   // unused entry of a device-animated mesh's reserved frontier
@@ -735,7 +726,7 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int
     if (m == 0) return;
     if (!RTX_STAMPS_WALK)
         bvh_walk_lean<ANY, SLAB, CB, CULL>(S, nb, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, sc_t,
-                                           sc_tri, live, occ_word, occ_bit, cq, key_word);
+                                           sc_tri, live, occ_word, occ_bit, cq);
     else
         bvh_walk<ANY, FAST, false>(S, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, nullptr, sc_t, sc_tri,
                                    live, cnt, occ_word, occ_bit);
@@ -1040,23 +1031,14 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         uint32_t sc_tri = 0;
         unsigned long long unused = 0;
         const int oct = (fast && S.oct_bytes) ? batch_octant(vr, active) : -1;
-        const unsigned long long* kw = nullptr;
-        if (RTX_SPLIT_SHARE_T && pcull) {
-            // start from the smallest key the tile's other parts have published so far
-            kw = &F.hit_key[slot];
-            const unsigned long long k = __hip_atomic_load(kw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const bool take = valid && __uint_as_float(static_cast<uint32_t>(k >> 32)) < sc_t;   // NaN (unset): no
-            sc_t = take ? __uint_as_float(static_cast<uint32_t>(k >> 32)) : sc_t;
-            sc_tri = take ? static_cast<uint32_t>(k) : sc_tri;
-        }
         if (oct >= 0 && pcull)
             part_traverse<false, kSlabOct, kCullBack, kCull>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri, unused,
-                                                             cnt, nullptr, 0u, pq, kw);
+                                                             cnt, nullptr, 0u, pq);
         else if (oct >= 0)
             part_traverse<false, kSlabOct, kCullBack>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri, unused, cnt);
         else if (fast && pcull)
             part_traverse<false, kSlabFast, kCullBack, kCull>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused,
-                                                              cnt, nullptr, 0u, pq, kw);
+                                                              cnt, nullptr, 0u, pq);
         else if (fast)
             part_traverse<false, kSlabFast, kCullBack>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused, cnt);
         else

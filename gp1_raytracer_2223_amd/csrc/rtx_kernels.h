@@ -27,7 +27,8 @@ constexpr int kSchedPeriod = 64;      // frames between tile-cost measurements
 // Split rendering of heavy tiles: a wave tile whose measured cost exceeds
 // kSplitPermille/1000 x (frame cost / concurrent wave slots) is rendered by three extra
 // launches in which its BVH traversals are cut into subtree parts run by separate workgroups.
-constexpr int kPartsPerMesh = 128;     // target frontier size per mesh BVH (Synthetic100k: 128 beat 64 by 6 %)
+constexpr int kPartsPerMesh = 64;      // target frontier size per mesh BVH (with the exact cull, Synthetic100k
+                                       // 1080p: 64 parts 1.00 ms, 128 1.12, 256 1.46; before it 128 beat 64 by 6 %)
 constexpr int kMaxParts = 1024;        // all meshes together
 constexpr int kMaxHeavyTiles = 8192;   // heavy wave tiles per frame (hit-key buffer: 64 px each)
 // 1.5 (v14 sweep, tools/split_sweep.sh): Synthetic100k 4.38 -> 3.51 ms, W4_Optional within

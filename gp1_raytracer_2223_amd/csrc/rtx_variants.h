@@ -14,7 +14,8 @@
 // switch; their records stay under profiles/ (profiles/r01/ablate_history.md, profiles/r03/
 // ab_*.txt): the plane-skip of primary rays, the touch prefetch of child records, XCD bands
 // and XCD runs, the early sphere-loop exit, the unfused triangle test, the non-asm child select;
-// round 4: the 128-ray pair kernel and the culled walks' prefetch touches (profiles/r04/).
+// round 4: the 128-ray pair kernel, the culled walks' prefetch touches and the split parts' shared
+// best key (profiles/r04/).
 #ifndef RTX_VARIANTS_H
 #define RTX_VARIANTS_H
 
@@ -36,11 +37,6 @@
 // shadow-ray walks with cull records visit the child most lanes enter first (1) or left first (0)
 #ifndef RTX_CULL_ORDER_ANY
 #define RTX_CULL_ORDER_ANY 1
-#endif
-// split closest hit with cull records: a part starts from the smallest key the tile's other parts
-// published (1), and re-reads it after every leaf (2), so the t-pruning sees the best t so far
-#ifndef RTX_SPLIT_SHARE_T
-#define RTX_SPLIT_SHARE_T 2
 #endif
 
 // ---- diagnostics (never a product build) -------------------------------------------------
