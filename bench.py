@@ -664,6 +664,12 @@ def main() -> int:
                     for k in per_rank[:, 0]]
                 entry["hbm_note"] = ("rank 0's PMC bytes per launch over each rank's own launch time (ranks render "
                                      "equal shares of 16-row stripes)")
+            if ctxs[0].cull_info()[0]:
+                # the FLOP model counts the reference's own traversal (rtx_count_work); the exact cull
+                #  proves most of those slab and triangle tests unnecessary and skips them
+                entry["roofline_rank0"]["flop_basis"] = (
+                    "reference-equivalent: the model's FLOP of the reference's traversal over the measured time; "
+                    "the exact cull skips most of those tests, so this is an effective rate, not executed FLOP")
             if d.rank == 0:
                 entry["parity"] = parity_report(r["px0"], r["rgb0"], scene, mw, mh, with_fnv=False)
             if N == 1:
