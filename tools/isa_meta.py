@@ -31,7 +31,7 @@ def main() -> None:
                                  capture_output=True, text=True).stdout
             notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", str(co)], check=True,
                                    capture_output=True, text=True).stdout
-        names = sorted(set(re.findall(r"<(_Z\d+rtx_render_(?:pair_)?kernel[^>]*)>:", dis)))
+        names = sorted(set(re.findall(r"<(_Z\d+rtx_(?:render|split)_kernel[^>]*)>:", dis)))
         for name in names:
             start = dis.index(f"<{name}>:")
             body = dis[start:dis.index("s_endpgm", start)]
@@ -47,7 +47,7 @@ def main() -> None:
                         mm = re.search(rf"\.{key}:\s+(\d+)", block)
                         if mm:
                             meta[key] = int(mm.group(1))
-            k = re.sub(r"^_Z\d+rtx_render_(?:pair_)?kernelI(.*)EvN4rtxd.*$", r"\1", name)
+            k = re.sub(r"^_Z\d+rtx_((?:render|split)_kernel)I(.*)EvN4rtxd.*$", r"\1<\2>", name)
             print(f"{Path(lib).name:28s} {k:22s} vgpr {meta.get('vgpr_count')} sgpr {meta.get('sgpr_count')} "
                   f"scratch {meta.get('private_segment_fixed_size')}  static v_* {ops['valu']} s_* {ops['salu']}")
 
