@@ -39,7 +39,15 @@ def _ctx_env(**env):
 def cull_ctx():
     """A context that culls every scene (the product enables the cull only where the SAH estimate
     says it pays, RTX_CULL_MIN_SA) and tests every record (RTX_CULL_RATIO=0)."""
-    ctx = _ctx_env(RTX_CULL_MIN_SA="0", RTX_CULL_RATIO="0")
+    ctx = _ctx_env(RTX_CULL_MIN_SA="0", RTX_CULL_RATIO="0", RTX_CULL_ANIMATED="1")
+    yield ctx
+    ctx.close()
+
+
+@pytest.fixture(scope="module")
+def product_ctx():
+    """The product's cull decision, independent of the upload history (RTX_CULL_ANIMATED=1)."""
+    ctx = _ctx_env(RTX_CULL_ANIMATED="1")
     yield ctx
     ctx.close()
 
@@ -167,13 +175,39 @@ def test_cull_camera_moves_between_frames(cull_ctx):
 
 @pytest.mark.parametrize("name,on", [("Synthetic100k", True), ("W4_Optional", True), ("W4_Bunny", False),
                                      ("Bunny8Lights", False), ("W3", False)])
-def test_cull_enabled_where_it_pays(gpu_ctx, name, on):
+def test_cull_enabled_where_it_pays(product_ctx, name, on):
     """The product enables the cull where the reference's boxes are inflated enough (the SAH
     estimate of upload_scene: W4_Bunny 1.19, W4_Optional 2.40, Synthetic100k 9.26)."""
     hs = HostScene(name)   # (the scene's arrays live as long as hs)
     s, cam = hs.view()
-    gpu_ctx.upload(s)
-    assert gpu_ctx.cull_info()[0] == on
+    product_ctx.upload(s)
+    assert product_ctx.cull_info()[0] == on
+
+
+def test_cull_skipped_for_animated_uploads(plain_ctx):
+    """An animated loop re-uploads every frame and renders it once: after two such uploads the
+    records are not built (they would cost more than the one frame gains), and an upload rendered
+    twice or more turns the cull back on.  Every frame equals the unculled walk's and the reference's."""
+    ctx = _ctx_env()
+    try:
+        hs = HostScene("W4_Optional")
+        p = abi.make_params(96, 64)
+        seen = []
+        for k, renders in enumerate([1, 1, 1, 1, 3, 1, 1]):
+            hs.update(0.05 * k)
+            s, cam = hs.view()
+            ctx.upload(s)
+            seen.append(ctx.cull_info()[0])
+            for _ in range(renders):
+                px, rgb = ctx.render(cam, p)
+            plain_ctx.upload(s)
+            _same((px, rgb), plain_ctx.render(cam, p), f"upload {k + 1}")   # bit for bit, both planes
+            assert np.array_equal(px, oracle_bind.render(s, cam, p)[0]), k   # (Cook-Torrance: powf in rgb)
+        # uploads 1-2 follow at most one short upload, 3-5 two or more; 6 follows an upload rendered
+        # three times, 7 one short upload
+        assert seen == [True, True, False, False, False, True, True], seen
+    finally:
+        ctx.close()
 
 
 def test_cull_records_follow_the_camera(cull_ctx):
