@@ -151,3 +151,44 @@ def test_bench_control_plane_shm(world):
             assert sm == [world * (world + 1) // 2, world * k]
         assert g == [[float(i), 2.0 * i] for i in range(world)]
     assert not [f for f in os.listdir("/dev/shm") if f.startswith(f"rtx_ctl_{port}_")]
+
+
+@pytest.mark.gpu
+def test_bench_one_gpu_contract(tmp_path):
+    """The driver's N = 1 command (`bench.py --gpus 1 --steps 20 --warmup 5`, here with a 1-frame CPU
+    sample): one JSON line with the contract's fields; `value` = pixels / ms_per_step; the roofline
+    object; the CPU baseline and `speedup_vs_cpu` against its best configuration; every extra
+    workload with its parity and the one-GPU strong-scaling predictor (efficiency = t_full / (s x the
+    slowest share)); the culled Synthetic100k line marks its FLOP basis as reference-equivalent."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    cmd = [sys.executable, str(root / "bench.py"), "--gpus", "1", "--steps", "20", "--warmup", "5", "--cpu-frames", "1"]
+    out = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=400)
+    assert out.returncode == 0, out.stderr[-4000:]
+    r = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in r, k
+    assert r["n_gpus"] == 1 and r["steps"] == 20 and r["warmup"] == 5 and r["higher_is_better"] is True
+    assert abs(r["value"] - 1920 * 1080 / (r["ms_per_step"] * 1e-3) / 1e6) <= 1e-3 * r["value"]
+    rf = r["roofline"]
+    assert rf["bound"] in ("valu", "hbm", "mfma") and 0 < rf["frac"] < 1 and rf["peak"] > 0
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    cpu = r["cpu_baseline"]
+    assert cpu["kind"] in ("reference", "port") and cpu["value"] > 0 and cpu["cores"] >= 1
+    assert cpu["value"] >= cpu["all_threads_mpix_s"] - 1e-6   # the best configuration measured
+    assert abs(r["speedup_vs_cpu"] - r["value"] / cpu["value"]) <= 0.1 + 1e-3 * r["speedup_vs_cpu"]
+    assert r["parity"]["bit_exact"] is True and r["parity_configs_all_ok"] is True
+    scenes = {e["scene"]: e for e in r["multi_gpu_configs"]}
+    for name, e in scenes.items():
+        assert e["parity"]["ok"] is True, name
+        sp = e["strong_scaling_predictor"]
+        for s in (2, 4, 8):
+            x = sp[f"s{s}"]
+            assert len(x["share_ms"]) == s
+            assert abs(x["efficiency"] - sp["t_full_ms"] / (s * max(x["share_ms"]))) < 1e-3
+    assert "flop_basis" in scenes["Synthetic100k"]["roofline_rank0"]
+    assert "flop_basis" not in scenes["Bunny8Lights"]["roofline_rank0"]

@@ -2,7 +2,7 @@
 ranks, timed alone (rtx_time_views), with the heavy-tile count the schedule splits, under context
 settings given as environment variables read by rtx_create (e.g. RTX_SPLIT=0, RTX_TILE_ORDER=0).
 
-Usage (GPU box): python tools/share_probe.py <scene> <W> <H> [setting ...]
+Usage (GPU box): [SHARE_ROWS=16] [SHARE_ALL_RANKS=1] python tools/share_probe.py <scene> <W> <H> [setting ...]
   setting = name=VAR:value,VAR:value   (default: the product settings)
 """
 import ctypes as C
@@ -46,16 +46,21 @@ def main():
         ctx = ctx_with(env)
         ctx.upload(s)
         row = {"setting": name}
+        rows = int(os.environ.get("SHARE_ROWS", "16"))   # stripe height
+        ranks = os.environ.get("SHARE_ALL_RANKS") == "1"   # time every rank's share (else rank 0's)
         for st in (1, 2, 4, 8):
-            p = abi.make_params(W, H, stripe_rows=16 if st > 1 else 0, stripe_first=0, stripe_step=st)
-            ms = C.c_float()
-            abi.check(ctx.lib.rtx_time_views(ctx.h, cam, 1, C.byref(p), 5, C.byref(ms)), "t", ctx.h)
-            best = 1e9
-            for _ in range(2):
-                abi.check(ctx.lib.rtx_time_views(ctx.h, cam, 1, C.byref(p), 30, C.byref(ms)), "t", ctx.h)
-                best = min(best, ms.value)
+            times = []
+            for first in (range(st) if ranks else [0]):
+                p = abi.make_params(W, H, stripe_rows=rows if st > 1 else 0, stripe_first=first, stripe_step=st)
+                ms = C.c_float()
+                abi.check(ctx.lib.rtx_time_views(ctx.h, cam, 1, C.byref(p), 5, C.byref(ms)), "t", ctx.h)
+                best = 1e9
+                for _ in range(2):
+                    abi.check(ctx.lib.rtx_time_views(ctx.h, cam, 1, C.byref(p), 30, C.byref(ms)), "t", ctx.h)
+                    best = min(best, ms.value)
+                times.append(best)
             heavy, parts = ctx.split_info()
-            row[f"s{st}"] = {"ms": round(best, 4), "heavy": heavy, "parts": parts}
+            row[f"s{st}"] = {"ms": round(max(times), 4), "rank0_ms": round(times[0], 4), "heavy": heavy, "parts": parts}
         row["eff"] = {k: round(row["s1"]["ms"] / (int(k[1:]) * row[k]["ms"]), 3) for k in ("s2", "s4", "s8")}
         print(json.dumps(row), flush=True)
         ctx.close()
