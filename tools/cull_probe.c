@@ -8,7 +8,7 @@
  * the number of rays whose result differs (closest t / triangle, occlusion), which must be
  * zero for any sound margin.
  *
- * Margins: a fixed delta, or (delta < 0) the per-triangle bound of DESIGN.md §9.2 —
+ * Margins: a fixed delta, or (delta < 0) the per-triangle bound of DESIGN.md §3 ("Exact cull") —
  * for camera rays computed from the camera origin, for shadow rays from the light and the
  * ray's tmax (per node on a geometric tmax grid, the next grid value above the ray's).
  *
@@ -93,7 +93,7 @@ static int tri(v3 v0, v3 v1, v3 v2, v3 n, int cull, const ray* r, int ignore, fl
     return 1;
 }
 
-/* ---------------------------------------------------------------- margins */
+/* ---------------------------------------------------------------- margins ("Exact cull") */
 static const double U = 0x1p-24;
 static double gam(int n) { return n * U / (1.0 - n * U); }
 
@@ -123,7 +123,7 @@ static void tri_setup(tri_info* T, const float* p0, const float* p1, const float
 }
 
 /* Bound W on the distance between the ray's line and a point X of the triangle (inflated by
- * rho) for any ray the float Möller–Trumbore test accepts.  sb[k] >= |s~_k|
+ * rho) for any ray the float Möller–Trumbore test accepts (DESIGN.md §3 ("Exact cull")).  sb[k] >= |s~_k|
  * (s~ = fl(o - v0)).  omega bounds the in-plane part of w' = w x d (w: X's offset from the
  * line) and |w . n|; the in-plane part of w itself is omega / |cos theta|, and
  * |cos theta| >= (Dist - omega) / R from an anchor point on the line (camera origin / light)

@@ -1,5 +1,5 @@
 /*
- * mt_graze_search.c — diagnostic for DESIGN.md §9.2 (never product, never a checker).
+ * mt_graze_search.c — diagnostic for DESIGN.md §3 ("Exact cull") (never product, never a checker).
  *
  * Question: can the reference's float Möller–Trumbore (Utils.h:109-184, binary32, no FMA)
  * accept a ray whose exact line passes FAR from the triangle?  If it can, a BVH cull that
