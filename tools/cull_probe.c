@@ -676,3 +676,99 @@ int cull_probe_packet_union(const rtx_scene* sc, const rtx_camera* cam, uint32_t
     g_mark = NULL;
     return 0;
 }
+
+/* Shadow-hull skip estimate: per (tile of tw x th pixels, light), the shadow rays' union of reference
+ * node visits (as cull_probe_packet_union), and whether the AABB of the tile's shadow origins and
+ * the light misses the mesh's tight box grown by `grow` (then no shadow ray of the tile can hit the
+ * mesh: the wave could skip that light's mesh walk).  out[0] = shadow union visits, out[1] = those in
+ * (tile, light) pairs the hull test skips, out[2] = pairs with a shadow ray, out[3] = pairs skipped. */
+int cull_probe_shadow_hull(const rtx_scene* sc, const rtx_camera* cam, uint32_t W, uint32_t H, uint32_t tw,
+                           uint32_t th, double grow, uint64_t* out) {
+    if (sc->n_meshes != 1 || sc->n_lights > 16) return -1;
+    const rtx_mesh* m = &sc->meshes[0];
+    memset(out, 0, 4 * sizeof(uint64_t));
+    double bmn[3] = {INFINITY, INFINITY, INFINITY}, bmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = 0; i < m->n_indices; ++i)
+        for (int k = 0; k < 3; ++k) {
+            const double v = m->positions[3 * m->indices[i] + k];
+            if (v < bmn[k]) bmn[k] = v;
+            if (v > bmx[k]) bmx[k] = v;
+        }
+    uint8_t* um = (uint8_t*)malloc(m->n_nodes);
+    g_mark = (uint8_t*)malloc(m->n_nodes);
+    const float aspect = (int)W / (float)(int)H;
+    const uint32_t npx = tw * th;
+    v3* oo = (v3*)malloc(sizeof(v3) * npx);
+    int* hit = (int*)malloc(sizeof(int) * npx);
+    for (uint32_t ty = 0; ty + th <= H; ty += th)
+        for (uint32_t tx = 0; tx + tw <= W; tx += tw) {
+            uint32_t q = 0;
+            for (uint32_t py = ty; py < ty + th; ++py)
+                for (uint32_t px = tx; px < tx + tw; ++px, ++q) {
+                    const float cx = (2.f * (((int)px + 0.5f) / W) - 1) * aspect * cam->fov;
+                    const float cy = (1.f - (2.f * ((int)py + 0.5f) / H)) * cam->fov;
+                    v3 vd = mk(cam->right[0] * cx + cam->up[0] * cy + cam->forward[0] * 1.f,
+                               cam->right[1] * cx + cam->up[1] * cy + cam->forward[1] * 1.f,
+                               cam->right[2] * cx + cam->up[2] * cy + cam->forward[2] * 1.f);
+                    const float mg = sqrtf(vd.x * vd.x + vd.y * vd.y + vd.z * vd.z);
+                    vd.x /= mg; vd.y /= mg; vd.z /= mg;
+                    const ray vr = mkray(ld3(cam->origin), vd, 0.0001f, FLT_MAX);
+                    float bt = FLT_MAX;
+                    v3 nrm = mk(0, 1, 0);
+                    for (uint32_t i = 0; i < sc->n_planes; ++i) {
+                        const v3 p0 = ld3(sc->planes[i].origin), pn = ld3(sc->planes[i].normal);
+                        const float t = dot(sub(p0, vr.o), pn) / dot(vr.d, pn);
+                        if (t >= vr.tmin && t < vr.tmax && t < bt) { bt = t; nrm = pn; }
+                    }
+                    int did = 0;
+                    uint64_t c = 0;
+                    const float bt0 = bt;
+                    visit_mark(m, 0, &vr, 0, &did, &bt, &c);
+                    hit[q] = bt < FLT_MAX;
+                    if (bt < bt0) {   /* the mesh hit's normal: find the triangle again (probe only) */
+                        nrm = mk(0, 0, 0);
+                        for (uint32_t i = 0; i < m->n_indices; i += 3) {
+                            float t;
+                            const v3 v0 = ld3(&m->positions[3 * m->indices[i]]);
+                            const v3 v1 = ld3(&m->positions[3 * m->indices[i + 1]]);
+                            const v3 v2 = ld3(&m->positions[3 * m->indices[i + 2]]);
+                            const v3 n = ld3(&m->normals[3 * (i / 3)]);
+                            if (tri(v0, v1, v2, n, m->cull_mode, &vr, 0, &t) && t == bt) { nrm = n; break; }
+                        }
+                    }
+                    oo[q] = add(add(vr.o, scale(vr.d, bt)), scale(nrm, 0.0001f));
+                }
+            for (uint32_t li = 0; li < sc->n_lights; ++li) {
+                const v3 L = ld3(sc->lights[li].origin);
+                double hmn[3] = {L.x, L.y, L.z}, hmx[3] = {L.x, L.y, L.z};
+                int any = 0;
+                memset(um, 0, m->n_nodes);
+                for (uint32_t k = 0; k < npx; ++k) {
+                    if (!hit[k]) continue;
+                    any = 1;
+                    const double o[3] = {oo[k].x, oo[k].y, oo[k].z};
+                    for (int a = 0; a < 3; ++a) { if (o[a] < hmn[a]) hmn[a] = o[a]; if (o[a] > hmx[a]) hmx[a] = o[a]; }
+                    v3 ld = sub(L, oo[k]);
+                    const float mag = sqrtf(ld.x * ld.x + ld.y * ld.y + ld.z * ld.z);
+                    ld.x /= mag; ld.y /= mag; ld.z /= mag;
+                    const ray sr = mkray(oo[k], ld, 0.0001f, mag);
+                    int sd = 0;
+                    float ft = FLT_MAX;
+                    uint64_t c = 0;
+                    memset(g_mark, 0, m->n_nodes);
+                    visit_mark(m, 0, &sr, 1, &sd, &ft, &c);
+                    for (uint32_t i = 0; i < m->n_nodes; ++i) um[i] |= g_mark[i];
+                }
+                if (!any) continue;
+                uint64_t u = 0;
+                for (uint32_t i = 0; i < m->n_nodes; ++i) u += um[i];
+                int miss = 0;
+                for (int a = 0; a < 3; ++a) miss |= hmx[a] < bmn[a] - grow || hmn[a] > bmx[a] + grow;
+                out[0] += u;
+                out[2]++;
+                if (miss) { out[1] += u; out[3]++; }
+            }
+        }
+    free(um); free(g_mark); g_mark = NULL; free(oo); free(hit);
+    return 0;
+}
