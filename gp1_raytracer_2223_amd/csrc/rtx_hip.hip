@@ -605,6 +605,11 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
         }
         if (m) {
             const bool in = (m >> lane) & 1ull;
+            // split any-hit: the other parts' occlusion bits, read before the leaf's tests so the
+            // L2 round trip overlaps them (RTX_OCC_POLL, rtx_variants.h)
+            uint32_t occ_pre = 0u;
+            if (ANY && RTX_OCC_POLL == 2 && occ_word)
+                occ_pre = __hip_atomic_load(occ_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             for (uint32_t k = 0; k < ntri; ++k) {
                 const uint32_t ti = link + k * 64u;
                 Tri T;
@@ -621,8 +626,10 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                     sc_tri = u ? ti : sc_tri;
                 }
             }
-            if (ANY && occ_word) {
-                const uint32_t o = __hip_atomic_load(occ_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (ANY && RTX_OCC_POLL != 0 && occ_word) {
+                const uint32_t o = RTX_OCC_POLL == 2
+                                       ? occ_pre
+                                       : __hip_atomic_load(occ_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 live &= ~ballot((o & occ_bit) != 0u);
             }
             if (ANY && (live & mask) == 0) return;

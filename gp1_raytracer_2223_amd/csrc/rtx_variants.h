@@ -38,6 +38,11 @@
 #ifndef RTX_CULL_ORDER_ANY
 #define RTX_CULL_ORDER_ANY 1
 #endif
+// split any-hit (PHASE 2): another part's occlusion bit is polled after every leaf, read after the
+// leaf's triangle tests (1), before them (2), or never (0; the wave then ends only on its own hits)
+#ifndef RTX_OCC_POLL
+#define RTX_OCC_POLL 1
+#endif
 
 // ---- diagnostics (never a product build) -------------------------------------------------
 // RTX_STAMPS=1: per-wave {start, end, hw id, node-pair steps, triangle steps, lane-work}
