@@ -38,10 +38,12 @@
 #ifndef RTX_CULL_ORDER_ANY
 #define RTX_CULL_ORDER_ANY 1
 #endif
-// split any-hit (PHASE 2): another part's occlusion bit is polled after every leaf, read after the
-// leaf's triangle tests (1), before them (2), or never (0; the wave then ends only on its own hits)
+// split any-hit (PHASE 2): another part's occlusion bit is polled after every leaf, read before the
+// leaf's triangle tests so its L2 round trip overlaps them (2, product), after them (1), or never
+// (0; the wave then ends only on its own hits).  profiles/r04/ab_occ_poll.txt: 2 is 1-4 % faster
+// than 1 on Synthetic100k and its shares, W4_Optional and Bunny + 8 lights at s = 8; 0 is slower.
 #ifndef RTX_OCC_POLL
-#define RTX_OCC_POLL 1
+#define RTX_OCC_POLL 2
 #endif
 
 // ---- diagnostics (never a product build) -------------------------------------------------
