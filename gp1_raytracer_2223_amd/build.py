@@ -97,6 +97,19 @@ def build_oracle(force: bool = False) -> Path:
     return out
 
 
+def build_checkers(force: bool = False) -> Path:
+    """Test infrastructure: the brute-force CPU restatement of the cull records
+    (tools/cull_records_ref.c), the checker of tests/test_gpu_cull.py."""
+    bdir = REPO / "tools" / "bin"
+    bdir.mkdir(exist_ok=True)
+    out = bdir / "libcull_records_ref.so"
+    src = REPO / "tools" / "cull_records_ref.c"
+    if force or _stale(out, [src, CSRC / "rtx_cull.h"]):
+        _run(["gcc", "-std=c11", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared", "-Wall", "-Wextra",
+              src, "-o", out, "-lm"])
+    return out
+
+
 def build_reference(force: bool = False) -> Path | None:
     """Test infrastructure: the reference's own sources compiled in place (oracle/ref)."""
     out = ORACLE / "_ref" / "ref_harness"
@@ -111,6 +124,7 @@ def build_reference(force: bool = False) -> Path | None:
 def build_all(force: bool = False) -> None:
     build_host(force)
     build_oracle(force)
+    build_checkers(force)
     build_hip(force)
     build_reference(force)   # after librtx_hip.so: oracle/_ref/ref_binding links it
     build_cli(force)

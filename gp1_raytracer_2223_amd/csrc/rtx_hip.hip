@@ -1361,13 +1361,24 @@ __global__ void __launch_bounds__(256) rtx_octant_expand(float4* __restrict__ no
 }
 
 // ---------------------------------------------------------------- exact cull records
-// (rtx_cull.h; DevScene::cull).  Three launches derive them from the uploaded
-// triangle records, all on the context stream before the frames that read them:
-//   rtx_cull_tri_box     per triangle: the box of (v0, v0 + E1, v0 + E2), rounded outward
-//   rtx_cull_tri_margin  per (anchor, triangle): rtx_cull.h's margin, rounded up
-//   rtx_cull_nodes_*     per node slot: the box over its subtree's triangle range (contiguous in
-//                        leaf order; a superset range is merely looser) widened by the range's
-//                        largest margin and the kernel test's own padding -> the record
+// (rtx_cull.h; DevScene::cull).  Each node slot's record needs, over the node's
+// triangle range (contiguous in leaf order: children partition their parent's range), the union
+// of the triangles' boxes and, per anchor, the largest margin and dt.  Those range reductions
+// run over SEGMENT TREES of the per-triangle values: a perfect binary tree over n = 2^k leaves
+// (leaf n + i = triangle i, padding leaves hold the identity; node i = comb(2i, 2i + 1)), so a
+// slot's range [x, y) is the combination of at most 2 log2(y - x) tree nodes (cull_tree_query),
+// found by one thread in log2(y - x) + 1 dependent steps.  The tree is built in the launch that
+// computes the leaves: levels 0-6 across the wave, 7-8 in LDS across the 256-thread workgroup,
+// and the levels above by the last workgroup of the tree to arrive (an arrival counter).  Total
+// work O(N) for the trees and O(S log N) for S slots; critical path O(log N) — the round-4 kernels
+// re-reduced each slot's whole range (the root's wave walked every triangle once per anchor:
+// 0.57-1.47 ms for Synthetic100k).  Launches, all on the context stream before the frames:
+//   rtx_cull_tris_box    at upload: per triangle the box of (v0, v0 + E1, v0 + E2), rounded
+//                        outward, and its tree
+//   rtx_cull_tris_marg   per (anchor, triangle): rtx_cull.h's (margin, dt) and the anchor's tree
+//   rtx_cull_nodes<BOX>  per node slot: the box (queried at upload, then kept per context) widened
+//                        by the range's largest margin and the kernel test's own padding -> the
+//                        anchors' records
 // Light anchors at upload; a view's camera anchor when a frame's view origin is not the one its
 // records were made for.  A NaN, infinite or huge (> 2^40) coordinate anywhere gives +inf (the
 // record then always passes: the bound's finite-arithmetic domain, rtx_cull.h).
@@ -1390,39 +1401,143 @@ __device__ __forceinline__ float f_ru(double x) {   // smallest float >= x
 }
 __device__ __forceinline__ bool cull_domain(float x) { return fabsf(x) <= 0x1p40f; }   // false for NaN / inf
 
-__global__ void __launch_bounds__(256) rtx_cull_tri_box(const Tri* __restrict__ tris, uint32_t n, float4* __restrict__ box) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= n) return;
-    const float4 a = tris[i].a, b = tris[i].b, c = tris[i].c;
-    const float v0[3] = {a.x, a.y, a.z}, e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
-    float lo[3], hi[3];
-    bool ok = true;
-    for (int k = 0; k < 3; ++k) {
-        ok = ok && cull_domain(v0[k]) && cull_domain(e1[k]) && cull_domain(e2[k]);
-        const double p = v0[k], q = p + static_cast<double>(e1[k]), r = p + static_cast<double>(e2[k]);
-        const double mn = fmin(p, fmin(q, r)), mx = fmax(p, fmax(q, r));
-        // the double sums are exact unless the exponents differ by > 29: widen by 2^-40 anyway
-        lo[k] = f_rd(mn - fabs(mn) * 0x1p-40);
-        hi[k] = f_ru(mx + fabs(mx) * 0x1p-40);
-    }
-    const float bad = ok ? 0.f : 1.f;   // out of the domain: the node records pass every ray
-    box[2u * i] = make_float4(lo[0], lo[1], lo[2], bad);
-    box[2u * i + 1u] = make_float4(hi[0], hi[1], hi[2], 0.f);
+// The two kinds of tree values.  Margins and dt are >= 0 or +inf (never NaN: the margin kernel
+// maps NaN to +inf), so their identity is 0; box bounds never hold a NaN either (an out-of-domain
+// triangle's box is (-inf, +inf)), so min / max are exact folds in any order (only the sign of a
+// zero bound can depend on the order, and no record test observes it).
+struct alignas(8) CullMD {
+    float m, dt;
+};
+struct alignas(16) CullBox {
+    float lo[3], pad0, hi[3], pad1;
+};
+__device__ __forceinline__ CullMD cull_ident(CullMD*) { return {0.f, 0.f}; }
+__device__ __forceinline__ CullBox cull_ident(CullBox*) {
+    return {{INFINITY, INFINITY, INFINITY}, 0.f, {-INFINITY, -INFINITY, -INFINITY}, 0.f};
+}
+__device__ __forceinline__ CullMD cull_comb(const CullMD& a, const CullMD& b) { return {fmaxf(a.m, b.m), fmaxf(a.dt, b.dt)}; }
+__device__ __forceinline__ CullBox cull_comb(const CullBox& a, const CullBox& b) {
+    CullBox r;
+    for (int k = 0; k < 3; ++k) { r.lo[k] = fminf(a.lo[k], b.lo[k]); r.hi[k] = fmaxf(a.hi[k], b.hi[k]); }
+    r.pad0 = r.pad1 = 0.f;
+    return r;
+}
+__device__ __forceinline__ CullMD cull_xor(const CullMD& a, int o) { return {__shfl_xor(a.m, o, 64), __shfl_xor(a.dt, o, 64)}; }
+__device__ __forceinline__ CullBox cull_xor(const CullBox& a, int o) {
+    CullBox r;
+    for (int k = 0; k < 3; ++k) { r.lo[k] = __shfl_xor(a.lo[k], o, 64); r.hi[k] = __shfl_xor(a.hi[k], o, 64); }
+    r.pad0 = r.pad1 = 0.f;
+    return r;
 }
 
-__global__ void __launch_bounds__(256) rtx_cull_tri_margin(const Tri* __restrict__ tris, uint32_t n, const CullAnchors A,
-                                                         float* __restrict__ marg) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x, j = blockIdx.y;
-    if (i >= n || j >= A.n) return;
-    const float4 a = tris[i].a, b = tris[i].b, c = tris[i].c;
-    const float v0[3] = {a.x, a.y, a.z}, e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
-    rtx_cull_tri T;
-    rtx_cull_tri_setup(&T, v0, e1, e2);
-    const float* p = A.p[j];
-    const rtx_cull_bound bd = p[3] > 0.f ? rtx_cull_light_bounds(&T, p, p[3]) : rtx_cull_point_bounds(&T, p, A.bt[j]);
-    // NaN -> inf; (margin, dt) of anchor j for triangle i
-    marg[2 * (static_cast<size_t>(j) * n + i)] = (bd.margin >= 0.0 && bd.margin < 0x1p100) ? f_ru(bd.margin) : INFINITY;
-    marg[2 * (static_cast<size_t>(j) * n + i) + 1] = (bd.dt >= 0.0 && bd.dt < 0x1p100) ? f_ru(bd.dt) : INFINITY;
+// Leaf i = blockIdx.x * kCullTreeWG + threadIdx.x holds v; writes the tree levels of `t` (2n
+// entries, n = gridDim.x * kCullTreeWG).  `arrive`: the tree's arrival counter (0 before the
+// launch, 0 again after it); `top_lds` (<= kCullTopLds): the most workgroup roots the last
+// workgroup combines in LDS (tests lower it to exercise the global-memory path).
+template <class V>
+__device__ void cull_tree_build(V v, V* __restrict__ t, uint32_t* arrive, uint32_t top_lds) {
+    __shared__ V part[kCullTreeWG / 64];
+    __shared__ V top[kCullTopLds / 2];
+    __shared__ uint32_t last;
+    const uint32_t tid = threadIdx.x, nwg = gridDim.x, n = nwg * kCullTreeWG;
+    const uint32_t leaf = n + blockIdx.x * kCullTreeWG + tid;
+    t[leaf] = v;
+    for (int k = 1; k <= 6; ++k) {   // levels 1-6: butterflies over aligned 2^k lanes
+        v = cull_comb(v, cull_xor(v, 1 << (k - 1)));
+        if ((tid & ((1u << k) - 1u)) == 0u) t[leaf >> k] = v;
+    }
+    if ((tid & 63u) == 0u) part[tid >> 6] = v;
+    __syncthreads();
+    if (tid == 0) {   // levels 7 and 8 (kCullTreeWG = 256 = 4 waves)
+        const V a = cull_comb(part[0], part[1]), b = cull_comb(part[2], part[3]), r = cull_comb(a, b);
+        t[leaf >> 7] = a;
+        t[(leaf >> 7) + 1u] = b;
+        t[leaf >> 8] = r;
+        __threadfence();   // release: this workgroup's nodes before its arrival
+        last = atomicAdd(arrive, 1u) == nwg - 1u ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();   // acquire: every other workgroup's root is visible
+    // levels above 8: the workgroup roots are nodes [nwg, 2 nwg); node j of a level = comb(2j, 2j + 1)
+    if (nwg == 1u) {
+        // the workgroup's root is the tree's
+    } else if (nwg <= top_lds) {
+        for (uint32_t w = tid; w < nwg / 2u; w += kCullTreeWG)
+            top[w] = cull_comb(t[nwg + 2u * w], t[nwg + 2u * w + 1u]);
+        for (uint32_t c = nwg / 2u;; c >>= 1) {   // `top` holds level-nodes [c, 2c)
+            __syncthreads();
+            for (uint32_t w = tid; w < c; w += kCullTreeWG) t[c + w] = top[w];
+            if (c == 1u) break;
+            V r[kCullTopLds / 2 / kCullTreeWG];
+            uint32_t q = 0;
+            for (uint32_t w = tid; w < c / 2u; w += kCullTreeWG) r[q++] = cull_comb(top[2u * w], top[2u * w + 1u]);
+            __syncthreads();
+            q = 0;
+            for (uint32_t w = tid; w < c / 2u; w += kCullTreeWG) top[w] = r[q++];
+        }
+    } else {
+        for (uint32_t c = nwg / 2u; c >= 1u; c >>= 1) {
+            for (uint32_t w = tid; w < c; w += kCullTreeWG) t[c + w] = cull_comb(t[2u * (c + w)], t[2u * (c + w) + 1u]);
+            __threadfence();
+            __syncthreads();
+        }
+    }
+    if (tid == 0) *arrive = 0u;   // for the next launch (stream order)
+}
+
+// the combination of the leaves [x, y) (x <= y <= n)
+template <class V>
+__device__ __forceinline__ V cull_tree_query(const V* __restrict__ t, uint32_t n, uint32_t x, uint32_t y) {
+    V acc = cull_ident(static_cast<V*>(nullptr));
+    for (uint32_t l = x + n, r = y + n; l < r; l >>= 1, r >>= 1) {
+        if (l & 1u) acc = cull_comb(acc, t[l++]);
+        if (r & 1u) acc = cull_comb(acc, t[--r]);
+    }
+    return acc;
+}
+
+__global__ void __launch_bounds__(kCullTreeWG) rtx_cull_tris_box(const Tri* __restrict__ tris, uint32_t nt,
+                                                                 CullBox* __restrict__ tree, uint32_t* arrive,
+                                                                 uint32_t top_lds) {
+    const uint32_t i = blockIdx.x * kCullTreeWG + threadIdx.x;
+    CullBox v = cull_ident(static_cast<CullBox*>(nullptr));
+    if (i < nt) {
+        const float4 a = tris[i].a, b = tris[i].b, c = tris[i].c;
+        const float v0[3] = {a.x, a.y, a.z}, e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
+        bool ok = true;
+        for (int k = 0; k < 3; ++k) {
+            ok = ok && cull_domain(v0[k]) && cull_domain(e1[k]) && cull_domain(e2[k]);
+            const double p = v0[k], q = p + static_cast<double>(e1[k]), r = p + static_cast<double>(e2[k]);
+            const double mn = fmin(p, fmin(q, r)), mx = fmax(p, fmax(q, r));
+            // the double sums are exact unless the exponents differ by > 29: widen by 2^-40 anyway
+            v.lo[k] = f_rd(mn - fabs(mn) * 0x1p-40);
+            v.hi[k] = f_ru(mx + fabs(mx) * 0x1p-40);
+        }
+        if (!ok)   // out of the domain: every box holding it passes every ray
+            for (int k = 0; k < 3; ++k) { v.lo[k] = -INFINITY; v.hi[k] = INFINITY; }
+    }
+    cull_tree_build(v, tree, arrive, top_lds);
+}
+
+// grid (n / kCullTreeWG, A.n): tree j at trees + 2n j, counter arrive[j]
+__global__ void __launch_bounds__(kCullTreeWG) rtx_cull_tris_marg(const Tri* __restrict__ tris, uint32_t nt,
+                                                                  const CullAnchors A, CullMD* __restrict__ trees,
+                                                                  uint32_t* arrive, uint32_t top_lds) {
+    const uint32_t i = blockIdx.x * kCullTreeWG + threadIdx.x, j = blockIdx.y;
+    CullMD v{0.f, 0.f};
+    if (i < nt) {
+        const float4 a = tris[i].a, b = tris[i].b, c = tris[i].c;
+        const float v0[3] = {a.x, a.y, a.z}, e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
+        rtx_cull_tri T;
+        rtx_cull_tri_setup(&T, v0, e1, e2);
+        const float* p = A.p[j];
+        const rtx_cull_bound bd = p[3] > 0.f ? rtx_cull_light_bounds(&T, p, p[3]) : rtx_cull_point_bounds(&T, p, A.bt[j]);
+        // NaN -> inf
+        v.m = (bd.margin >= 0.0 && bd.margin < 0x1p100) ? f_ru(bd.margin) : INFINITY;
+        v.dt = (bd.dt >= 0.0 && bd.dt < 0x1p100) ? f_ru(bd.dt) : INFINITY;
+    }
+    cull_tree_build(v, trees + 2ull * gridDim.x * kCullTreeWG * j, arrive + j, top_lds);
 }
 
 // Which records the walk tests (CullParams): a box some axis of which the reference's box (node
@@ -1458,74 +1573,31 @@ __device__ __forceinline__ void cull_write(float4* __restrict__ cull, uint32_t s
     r[1] = make_float4(Ef[1], Ef[2], (bad || !(dt < 0x1p100f)) ? INFINITY : dt, __uint_as_float(worth ? 1u : 0u));
 }
 
-// node slots whose triangle range holds at most kCullBigTris triangles, one thread each
-__global__ void __launch_bounds__(256) rtx_cull_nodes_small(const uint2* __restrict__ rng, uint32_t nslots,
-                                                           const float4* __restrict__ box, const float* __restrict__ marg,
-                                                           uint32_t ntris, const CullAnchors A, float4* __restrict__ cull,
-                                                           uint32_t stride4, const CullParams P) {
+// One thread per node slot.  BOX (at upload): the slot's box from the box tree, kept in `nbox`
+// for the camera anchors' later launches; else read from `nbox`.  An empty range (padding slot)
+// or a box with an infinite bound (an out-of-domain triangle below) gives the always-pass record.
+template <bool BOX>
+__global__ void __launch_bounds__(256) rtx_cull_nodes(const uint2* __restrict__ rng, uint32_t nslots, uint32_t ntris,
+                                                      uint32_t n, const CullBox* __restrict__ btree,
+                                                      CullBox* __restrict__ nbox, const CullMD* __restrict__ trees,
+                                                      const CullAnchors A, float4* __restrict__ cull, uint32_t stride4,
+                                                      const CullParams P) {
     const uint32_t s = blockIdx.x * 256u + threadIdx.x;
     if (s >= nslots) return;
     const uint2 r = rng[s];
-    if (r.y - r.x > kCullBigTris) return;
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    bool bad = r.y <= r.x || r.y > ntris;   // empty range (padding slot): pass
-    for (uint32_t t = r.x; !bad && t < r.y; ++t) {
-        const float4 l = box[2u * t], h = box[2u * t + 1u];
-        bad = bad || l.w != 0.f;
-        lo[0] = fminf(lo[0], l.x); lo[1] = fminf(lo[1], l.y); lo[2] = fminf(lo[2], l.z);
-        hi[0] = fmaxf(hi[0], h.x); hi[1] = fmaxf(hi[1], h.y); hi[2] = fmaxf(hi[2], h.z);
-    }
-    for (uint32_t j = 0; j < A.n; ++j) {
-        float m = 0.f, dt = 0.f;
-        for (uint32_t t = r.x; !bad && t < r.y; ++t) {
-            const float x = marg[2 * (static_cast<size_t>(j) * ntris + t)], y = marg[2 * (static_cast<size_t>(j) * ntris + t) + 1];
-            m = (x > m || x != x) ? x : m;   // NaN sticks (then +inf)
-            dt = (y > dt || y != y) ? y : dt;
-        }
-        cull_write(cull, stride4, A.idx[j], s, lo, hi, bad, m, dt, P);
-    }
-}
-
-__device__ __forceinline__ float wave_min(float x) {
-    for (int o = 32; o > 0; o >>= 1) x = fminf(x, __shfl_xor(x, o, 64));
-    return x;
-}
-__device__ __forceinline__ float wave_max(float x) {
-    for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
-    return x;
-}
-
-// the listed node slots (ranges above kCullBigTris), one wave each
-__global__ void __launch_bounds__(64) rtx_cull_nodes_big(const uint32_t* __restrict__ big, const uint2* __restrict__ rng,
-                                                        const float4* __restrict__ box, const float* __restrict__ marg,
-                                                        uint32_t ntris, const CullAnchors A, float4* __restrict__ cull,
-                                                        uint32_t stride4, const CullParams P) {
-    const uint32_t s = big[blockIdx.x], lane = threadIdx.x;
-    const uint2 r = rng[s];
     const bool empty = r.y <= r.x || r.y > ntris;
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    uint32_t badl = empty ? 1u : 0u;
-    for (uint32_t t = r.x + lane; !empty && t < r.y; t += 64u) {
-        const float4 l = box[2u * t], h = box[2u * t + 1u];
-        badl |= l.w != 0.f ? 1u : 0u;
-        lo[0] = fminf(lo[0], l.x); lo[1] = fminf(lo[1], l.y); lo[2] = fminf(lo[2], l.z);
-        hi[0] = fmaxf(hi[0], h.x); hi[1] = fmaxf(hi[1], h.y); hi[2] = fmaxf(hi[2], h.z);
+    CullBox b;
+    if (BOX) {
+        b = empty ? cull_ident(static_cast<CullBox*>(nullptr)) : cull_tree_query(btree, n, r.x, r.y);
+        nbox[s] = b;
+    } else {
+        b = nbox[s];
     }
-    const bool bad = __builtin_amdgcn_ballot_w64(badl != 0u) != 0ull;
-    for (int k = 0; k < 3; ++k) { lo[k] = wave_min(lo[k]); hi[k] = wave_max(hi[k]); }
+    bool bad = empty;
+    for (int k = 0; k < 3; ++k) bad = bad || !(fabsf(b.lo[k]) < INFINITY) || !(fabsf(b.hi[k]) < INFINITY);
     for (uint32_t j = 0; j < A.n; ++j) {
-        float m = 0.f, dt = 0.f;
-        uint32_t nanl = 0u;
-        for (uint32_t t = r.x + lane; !empty && t < r.y; t += 64u) {
-            const float x = marg[2 * (static_cast<size_t>(j) * ntris + t)], y = marg[2 * (static_cast<size_t>(j) * ntris + t) + 1];
-            nanl |= (x != x || y != y) ? 1u : 0u;
-            m = fmaxf(m, x);
-            dt = fmaxf(dt, y);
-        }
-        m = wave_max(m);
-        dt = wave_max(dt);
-        if (__builtin_amdgcn_ballot_w64(nanl != 0u)) m = dt = INFINITY;
-        if (lane == 0) cull_write(cull, stride4, A.idx[j], s, lo, hi, bad, m, dt, P);
+        const CullMD md = bad ? CullMD{0.f, 0.f} : cull_tree_query(trees + 2ull * n * j, n, r.x, r.y);
+        cull_write(cull, stride4, A.idx[j], s, b.lo, b.hi, bad, md.m, md.dt, P);
     }
 }
 
@@ -1753,6 +1825,7 @@ struct rtx_ctx {
     uint32_t split_mode = 1;         // 0 off, 1 auto, 2 force (RTX_SPLIT=0 / unset / force)
     uint32_t split_slots = 0;        // concurrent render waves on this device
     uint32_t split_permille = kSplitPermille;   // RTX_SPLIT_FACTOR (tuning)
+    uint32_t sched_period = kSchedPeriod;       // RTX_SCHED_PERIOD (tuning)
     uint32_t split_parts = kPartsPerMesh;            // RTX_SPLIT_PARTS (tuning)
     bool split_ok = false;           // the uploaded scene admits split rendering
     bool deep_stack = false;         // the uploaded scene needs rtx_render_kernel<..., DEEP = true>
@@ -1767,29 +1840,34 @@ struct rtx_ctx {
     unsigned long long* d_hit_key = nullptr;
     uint32_t* d_occ = nullptr;
     // exact cull (DevScene::cull): on for host uploads (RTX_NO_CULL=1: off); the
-    // scratch of its record launches (per-triangle boxes and margins) and the node-slot ranges
-    // and big-node list in the current image
+    // scratch of its record launches (the segment trees of the per-triangle boxes and of each
+    // anchor's margins, the slots' boxes, the trees' arrival counters) and the node-slot ranges
+    // in the current image
     bool no_cull = false;
     float cull_ratio = 1.5f;              // CullParams (RTX_CULL_RATIO, RTX_CULL_LEAVES: tuning)
     double cull_min_sa = 1.5;             // upload_scene's worth test (RTX_CULL_MIN_SA)
     bool cull_leaves = false;
-    // Animated loops re-upload every frame and render it once: the records would be rebuilt per
-    // frame for one frame's gain (W4_Optional serial F6 loop 1,082 -> 935 FPS with them).  After two
-    // consecutive uploads rendered at most once each, uploads skip the cull (RTX_CULL_ANIMATED=1:
-    // build the records anyway, tests); one upload rendered twice or more turns it back on.
-    bool cull_animated = false;
+    // Animated loops re-upload every frame and render it once, so the records are rebuilt per
+    // frame.  Round 4's records cost more than a frame and were skipped after two such uploads;
+    // the segment-tree records (tens of us) are built for every upload.  RTX_CULL_ANIMATED=0
+    // restores the skip (after two consecutive uploads rendered at most once each, until an
+    // upload is rendered twice).
+    bool cull_animated = true;
     uint32_t renders_since_upload = 0;
     uint32_t short_uploads = 0;
-    float4* d_cull_box = nullptr;
-    float* d_cull_marg = nullptr;
-    size_t cull_box_cap = 0, cull_marg_cap = 0;
+    CullBox* d_cull_btree = nullptr;      // 2n entries
+    CullMD* d_cull_mtree = nullptr;       // 2n entries per anchor of one launch
+    CullBox* d_cull_nbox = nullptr;       // per node slot of the current image
+    uint32_t* d_cull_arrive = nullptr;    // per tree (kCullMaxAnchors margin trees, then the box tree)
+    size_t cull_tree_cap = 0, cull_nbox_cap = 0;   // leaves n the trees hold, slots nbox holds
+    uint32_t cull_top_lds = kCullTopLds;  // RTX_CULL_TOP_LDS (tests: the global-memory top levels)
     const uint2* cull_rng = nullptr;
-    const uint32_t* cull_big = nullptr;
-    uint32_t cull_nslots = 0, cull_nbig = 0, cull_ntris = 0;
+    uint32_t cull_nslots = 0, cull_ntris = 0, cull_n = 0;
     float cull_view[kMaxViews][3] = {};   // camera origin each view's records of the current image were made for
     uint32_t cull_view_valid = 0;         // bit v: view v's records are current
     double cull_bmin[3] = {}, cull_bmax[3] = {};   // the meshes' box (a camera anchor's t bound, cull_bt)
     uint64_t cull_updates = 0;            // camera-anchor record launches so far (rtx_cull_info)
+    float cull_anchor[kMaxViews + kMaxCullLights][5] = {};   // per record copy: anchor xyz, w, bt (rtx_cull_dump)
     rtx_render_params last{};
     int last_views = 1;
     bool last_valid = false, last_rgb = false;
@@ -1913,6 +1991,8 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     c->device = device_id;
     // RTX_TILE_ORDER=0 disables cost-ordered tile dispatch (identity order every frame)
     if (const char* e = std::getenv("RTX_TILE_ORDER")) c->sched_enabled = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RTX_SCHED_PERIOD"))
+        c->sched_period = std::max<uint32_t>(1u, static_cast<uint32_t>(std::strtoul(e, nullptr, 10)));
     // RTX_SPLIT=0 renders heavy tiles in one piece; RTX_SPLIT=force splits every tile
     if (const char* e = std::getenv("RTX_NO_SPEC")) c->no_spec = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_NO_CULL")) c->no_cull = std::strcmp(e, "0") != 0;
@@ -1922,6 +2002,8 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     }
     if (const char* e = std::getenv("RTX_CULL_LEAVES")) c->cull_leaves = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_CULL_ANIMATED")) c->cull_animated = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RTX_CULL_TOP_LDS"))
+        c->cull_top_lds = std::min<uint32_t>(kCullTopLds, static_cast<uint32_t>(std::strtoul(e, nullptr, 10)));
     if (const char* e = std::getenv("RTX_CULL_MIN_SA")) {
         const double v = std::atof(e);
         if (v >= 0.0 && v < 1e30) c->cull_min_sa = v;
@@ -2001,8 +2083,10 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     (void)hipFree(c->d_occ);
     (void)hipFree(c->d_hstk);
     (void)hipFree(c->d_hstkT);
-    (void)hipFree(c->d_cull_box);
-    (void)hipFree(c->d_cull_marg);
+    (void)hipFree(c->d_cull_btree);
+    (void)hipFree(c->d_cull_mtree);
+    (void)hipFree(c->d_cull_nbox);
+    (void)hipFree(c->d_cull_arrive);
     if (c->ev_heavy) (void)hipEventDestroy(c->ev_heavy);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -2042,43 +2126,60 @@ struct UploadLayout {
 
 int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay);
 
-// Queue the record launches of the anchors in A (rtx_cull_tri_margin + rtx_cull_nodes_*) on the
-// context stream, the per-triangle boxes first when `boxes`.  Grows the scratch (after a stream
-// sync: queued launches may still read the old buffers).
+// Queue the record launches on the context stream: with `boxes` (at upload) the box tree and
+// every slot's box, then, for the anchors in A, their margin trees and records.  Grows the
+// scratch (after a stream sync: queued launches may still read the old buffers).
 int cull_launch(rtx_ctx* c, const CullAnchors& A, bool boxes) {
     const uint32_t nt = c->cull_ntris;
-    const size_t marg_need = 2 * static_cast<size_t>(kMaxViews > kMaxCullLights ? kMaxViews : kMaxCullLights) * nt;
-    if (2 * static_cast<size_t>(nt) > c->cull_box_cap || marg_need > c->cull_marg_cap) {
+    const uint32_t n = c->cull_n;
+    if (n > c->cull_tree_cap || c->cull_nslots > c->cull_nbox_cap || !c->d_cull_arrive) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));
-        (void)hipFree(c->d_cull_box);
-        (void)hipFree(c->d_cull_marg);
-        c->d_cull_box = nullptr;
-        c->d_cull_marg = nullptr;
-        c->cull_box_cap = c->cull_marg_cap = 0;
-        HIP_TRY(c, hipMalloc(&c->d_cull_box, 2 * static_cast<size_t>(nt) * sizeof(float4)));
-        HIP_TRY(c, hipMalloc(&c->d_cull_marg, marg_need * sizeof(float)));
-        c->cull_box_cap = 2 * static_cast<size_t>(nt);
-        c->cull_marg_cap = marg_need;
+        if (n > c->cull_tree_cap) {
+            (void)hipFree(c->d_cull_btree);
+            (void)hipFree(c->d_cull_mtree);
+            c->d_cull_btree = nullptr;
+            c->d_cull_mtree = nullptr;
+            c->cull_tree_cap = 0;
+            HIP_TRY(c, hipMalloc(&c->d_cull_btree, 2 * static_cast<size_t>(n) * sizeof(CullBox)));
+            HIP_TRY(c, hipMalloc(&c->d_cull_mtree, 2 * static_cast<size_t>(n) * kCullMaxAnchors * sizeof(CullMD)));
+            c->cull_tree_cap = n;
+        }
+        if (c->cull_nslots > c->cull_nbox_cap) {
+            (void)hipFree(c->d_cull_nbox);
+            c->d_cull_nbox = nullptr;
+            c->cull_nbox_cap = 0;
+            HIP_TRY(c, hipMalloc(&c->d_cull_nbox, static_cast<size_t>(c->cull_nslots) * sizeof(CullBox)));
+            c->cull_nbox_cap = c->cull_nslots;
+        }
+        if (!c->d_cull_arrive) {
+            HIP_TRY(c, hipMalloc(&c->d_cull_arrive, (kCullMaxAnchors + 1) * sizeof(uint32_t)));
+            HIP_TRY(c, hipMemset(c->d_cull_arrive, 0, (kCullMaxAnchors + 1) * sizeof(uint32_t)));
+        }
     }
-    const uint32_t tb = (nt + 255u) / 256u;
-    if (boxes) {
-        hipLaunchKernelGGL(rtx_cull_tri_box, dim3(tb), dim3(256), 0, c->stream, c->dev.tris, nt, c->d_cull_box);
-        HIP_TRY(c, hipGetLastError());
+    for (uint32_t j = 0; j < A.n; ++j) {
+        for (int k = 0; k < 4; ++k) c->cull_anchor[A.idx[j]][k] = A.p[j][k];
+        c->cull_anchor[A.idx[j]][4] = A.bt[j];
     }
-    if (A.n == 0) return RTX_OK;
+    const uint32_t nwg = n / kCullTreeWG, sb = (c->cull_nslots + 255u) / 256u;
     float4* rec = const_cast<float4*>(c->dev.cull);
     const uint32_t stride4 = c->dev.cull_stride / 16u;
     const CullParams P{c->dev.nodes, c->cull_ratio, c->cull_leaves ? 1u : 0u};
-    hipLaunchKernelGGL(rtx_cull_tri_margin, dim3(tb, A.n), dim3(256), 0, c->stream, c->dev.tris, nt, A, c->d_cull_marg);
-    HIP_TRY(c, hipGetLastError());
-    hipLaunchKernelGGL(rtx_cull_nodes_small, dim3((c->cull_nslots + 255u) / 256u), dim3(256), 0, c->stream, c->cull_rng,
-                       c->cull_nslots, c->d_cull_box, c->d_cull_marg, nt, A, rec, stride4, P);
-    HIP_TRY(c, hipGetLastError());
-    if (c->cull_nbig) {
-        hipLaunchKernelGGL(rtx_cull_nodes_big, dim3(c->cull_nbig), dim3(64), 0, c->stream, c->cull_big, c->cull_rng,
-                           c->d_cull_box, c->d_cull_marg, nt, A, rec, stride4, P);
+    if (A.n) {
+        hipLaunchKernelGGL(rtx_cull_tris_marg, dim3(nwg, A.n), dim3(kCullTreeWG), 0, c->stream, c->dev.tris, nt, A,
+                           c->d_cull_mtree, c->d_cull_arrive, c->cull_top_lds);
         HIP_TRY(c, hipGetLastError());
     }
+    if (boxes) {
+        hipLaunchKernelGGL(rtx_cull_tris_box, dim3(nwg), dim3(kCullTreeWG), 0, c->stream, c->dev.tris, nt,
+                           c->d_cull_btree, c->d_cull_arrive + kCullMaxAnchors, c->cull_top_lds);
+        HIP_TRY(c, hipGetLastError());
+        hipLaunchKernelGGL(rtx_cull_nodes<true>, dim3(sb), dim3(256), 0, c->stream, c->cull_rng, c->cull_nslots, nt, n,
+                           c->d_cull_btree, c->d_cull_nbox, c->d_cull_mtree, A, rec, stride4, P);
+    } else if (A.n) {
+        hipLaunchKernelGGL(rtx_cull_nodes<false>, dim3(sb), dim3(256), 0, c->stream, c->cull_rng, c->cull_nslots, nt,
+                           n, c->d_cull_btree, c->d_cull_nbox, c->d_cull_mtree, A, rec, stride4, P);
+    }
+    HIP_TRY(c, hipGetLastError());
     return RTX_OK;
 }
 
@@ -2258,11 +2359,10 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
     if (parts.size() > static_cast<size_t>(kMaxParts)) split_ok = false;
     if (!split_ok) parts.clear();
     // Cull records' inputs: per node slot the range of device triangles under it (leaf order is
-    // contiguous within a subtree; children's slots follow their parent's, so one backward sweep),
-    // the slots whose range a wave reduces (rtx_cull_nodes_big), and per light the tmax up to which
-    // its shadow rays are culled: 4x the farthest mesh-box corner + 1 (longer rays pass).
+    // contiguous within a subtree; children's slots follow their parent's, so one backward sweep)
+    // and per light the tmax up to which its shadow rays are culled: 4x the farthest mesh-box
+    // corner + 1 (longer rays pass).
     std::vector<uint2> cull_rng;
-    std::vector<uint32_t> cull_big;
     std::vector<float> cull_T;
     if (cull_on) {
         cull_on = !tri.empty() && !mesh_slots.empty();
@@ -2302,7 +2402,6 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
                         b[2 * a + 1] = std::fmax(nb[6 * link + 2 * a + 1], nb[6 * (link + 1) + 2 * a + 1]);
                     }
                 }
-                if (cull_rng[sl].y - cull_rng[sl].x > kCullBigTris) cull_big.push_back(sl);
                 const float4 r0v = nodes[2 * sl], r1v = nodes[2 * sl + 1];
                 sa_ref += sa(double(r0v.y) - r0v.x, double(r0v.w) - r0v.z, double(r1v.y) - r1v.x);
                 sa_tight += sa(std::fmax(double(b[1]) - b[0], 0.0), std::fmax(double(b[3]) - b[2], 0.0),
@@ -2365,8 +2464,7 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
                   {nullptr, node_sec, 0},
                   {meshes.data(), meshes.size() * 16, 0}, {lights.data(), lights.size() * 16, 0},
                   {mats.data(), mats.size() * 16, 0},     {parts.data(), parts.size() * 16, 0},
-                  {cull_rng.data(), cull_rng.size() * 8, 0}, {cull_big.data(), cull_big.size() * 4, 0},
-                  {cull_T.data(), cull_T.size() * 4, 0}};
+                  {cull_rng.data(), cull_rng.size() * 8, 0}, {cull_T.data(), cull_T.size() * 4, 0}};
     size_t total = 0;
     for (auto& x : secs) { x.off = total; total += align256(x.n ? x.n : 16); }
     HIP_TRY(c, hipSetDevice(c->device));
@@ -2460,14 +2558,14 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
     d.n_tris = static_cast<uint32_t>(tri.size() / 4); d.n_nodes = static_cast<uint32_t>(nodes.size() / 2);
     if (cull_on) {
         d.cull = B.cull;
-        d.cull_T = reinterpret_cast<const float*>(base + secs[11].off);
+        d.cull_T = reinterpret_cast<const float*>(base + secs[10].off);
         d.cull_stride = static_cast<uint32_t>(cull_stride);
         c->cull_rng = reinterpret_cast<const uint2*>(base + secs[9].off);
-        c->cull_big = reinterpret_cast<const uint32_t*>(base + secs[10].off);
         c->cull_nslots = d.n_nodes;
         for (int a = 0; a < 3; ++a) { c->cull_bmin[a] = bmin[a]; c->cull_bmax[a] = bmax[a]; }
-        c->cull_nbig = static_cast<uint32_t>(cull_big.size());
         c->cull_ntris = d.n_tris;
+        c->cull_n = kCullTreeWG;   // the segment trees' leaves: a power of two >= the triangles
+        while (c->cull_n < d.n_tris) c->cull_n *= 2u;
     }
     c->cull_view_valid = 0;
     c->dev = d;
@@ -2671,7 +2769,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     F.occ_bits = c->d_occ;
     // Measure tile costs on the first frame of a shape and then every kSchedPeriod frames;
     // the frames in between reuse the last order and pay nothing for scheduling.
-    const bool measure = c->sched_enabled && (!c->sched_ready || c->sched_frame % kSchedPeriod == 0);
+    const bool measure = c->sched_enabled && (!c->sched_ready || c->sched_frame % c->sched_period == 0);
     ++c->sched_frame;
     F.order = (c->sched_enabled && c->sched_ready) ? c->d_order : nullptr;
     F.cost = measure ? c->d_cost : nullptr;
@@ -3012,6 +3110,25 @@ extern "C" int rtx_cull_info(rtx_ctx* c, uint32_t* enabled, uint64_t* camera_upd
     if (!c) return RTX_E_INVALID;
     if (enabled) *enabled = c->dev.cull_stride ? 1u : 0u;
     if (camera_updates) *camera_updates = c->cull_updates;
+    return RTX_OK;
+}
+
+extern "C" int rtx_cull_dump(rtx_ctx* c, uint32_t anchor, uint32_t* n_slots, uint32_t* n_tris, float* anchor_p,
+                             float* records, uint32_t* ranges, float* nodes, float* tris) {
+    if (!c || anchor >= static_cast<uint32_t>(kMaxViews + kMaxCullLights)) return RTX_E_INVALID;
+    if (!c->dev.cull_stride) return fail(c, RTX_E_INVALID, "the uploaded scene has no cull records");
+    if (n_slots) *n_slots = c->cull_nslots;
+    if (n_tris) *n_tris = c->cull_ntris;
+    if (anchor_p) std::memcpy(anchor_p, c->cull_anchor[anchor], sizeof c->cull_anchor[anchor]);
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const size_t ns = c->cull_nslots;
+    if (records)
+        HIP_TRY(c, hipMemcpy(records, reinterpret_cast<const char*>(c->dev.cull) + static_cast<size_t>(anchor) * c->dev.cull_stride,
+                             ns * 32, hipMemcpyDeviceToHost));
+    if (ranges) HIP_TRY(c, hipMemcpy(ranges, c->cull_rng, ns * 8, hipMemcpyDeviceToHost));
+    if (nodes) HIP_TRY(c, hipMemcpy(nodes, c->dev.nodes, ns * 32, hipMemcpyDeviceToHost));
+    if (tris) HIP_TRY(c, hipMemcpy(tris, c->dev.tris, static_cast<size_t>(c->cull_ntris) * 64, hipMemcpyDeviceToHost));
     return RTX_OK;
 }
 

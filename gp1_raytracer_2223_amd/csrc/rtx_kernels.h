@@ -138,7 +138,12 @@ constexpr size_t kOctantMaxNodeBytes = RTX_OCT_MAX_BYTES;   // octant node copie
 constexpr size_t kOctantDeviceMinBytes = size_t(64) << 10;   // from this size copies 1..7 are written on the device
 constexpr int kMaxViews = 8;   // views (camera positions) rendered by one launch
 constexpr int kMaxCullLights = 32;   // lights with a cull anchor (more: the scene renders without the cull)
-constexpr uint32_t kCullBigTris = 64;   // node ranges above this many triangles reduce with a wave (rtx_cull_nodes_big)
+// The records' range reductions run over segment trees of the per-triangle values (rtx_cull_tris_*):
+// kCullTreeWG leaves per workgroup; the last workgroup of a tree builds the levels above the
+// workgroups' roots in LDS when there are at most kCullTopLds of them (else in global memory).
+constexpr uint32_t kCullTreeWG = 256;
+constexpr uint32_t kCullMaxAnchors = kMaxViews > kMaxCullLights ? kMaxViews : kMaxCullLights;   // per record launch
+constexpr uint32_t kCullTopLds = 1024;
 
 struct ViewCam {
     float origin[3];

@@ -89,8 +89,14 @@ class HostScene:
         abi.check(self._lib.rtx_host_camera_set(self._h, o, fov_degrees, pitch, yaw), "rtx_host_camera_set")
 
     def view(self) -> tuple[abi.Scene, abi.Camera]:
+        """The flat scene (pointers into this object's arrays, valid until its next update) and
+        the camera.  Both hold a reference to this HostScene, so `HostScene(name).view()` keeps the
+        arrays alive as long as the returned Scene (the reference's Scene owns its vectors,
+        Scene.h:36-43)."""
         s, cam = abi.Scene(), abi.Camera()
         abi.check(self._lib.rtx_host_scene_view(self._h, C.byref(s), C.byref(cam)), "rtx_host_scene_view")
+        s._owner = self
+        cam._owner = self
         return s, cam
 
     # ---- inspection helpers (tests) -----------------------------------------------

@@ -248,6 +248,15 @@ int rtx_split_info(rtx_ctx* ctx, uint32_t* heavy_tiles, uint32_t* parts);
  * many times a camera's records were (re)built.  Environment: RTX_NO_CULL=1 disables;
  * RTX_CULL_MIN_SA, RTX_CULL_RATIO tune the enabling test and the per-node flag (tests). */
 int rtx_cull_info(rtx_ctx* ctx, uint32_t* enabled, uint64_t* camera_updates);
+/* Diagnostics of the exact cull (tests): waits for the context stream, then copies the current
+ * image's records of record copy `anchor` (view v < 8: its camera; 8 + l: light l) — n_slots x
+ * 8 floats, {c, E.x}, {E.y, E.z, dt, flag bits} — and their inputs: per slot the triangle range
+ * [first, end) (2 x u32), node copy 0 (8 floats per slot), the triangle records (16 floats
+ * each: {v0, n.x}, {E1, n.y}, {E2, n.z}, {mat}), and the anchor the copy was last built for
+ * (x, y, z, w = 0 camera / tmax bound of a light, bt).  Null pointers are skipped; sizes via
+ * *n_slots / *n_tris.  RTX_E_INVALID when the scene has no records. */
+int rtx_cull_dump(rtx_ctx* ctx, uint32_t anchor, uint32_t* n_slots, uint32_t* n_tris, float* anchor_p,
+                  float* records, uint32_t* ranges, float* nodes, float* tris);
 /* Diagnostics of the cost-ordered dispatch (tests): after a measured frame, the dispatch
  * permutation of the first n tiles' slots (`order`) and the one-piece tile costs it was
  * sorted by (`cost`).  *n_tiles = tiles of the current schedule (0 = none measured yet;

@@ -61,8 +61,12 @@ def plain_ctx():
 
 
 def _same(a, b, what):
+    """uint32 frames equal, colour planes equal bit for bit (a NaN equal to any NaN: the light on
+    a shadow-ray origin gives 0/0 directions, whose NaN payload is the CPU's or the GPU's own)."""
     assert np.array_equal(a[0], b[0]), f"{what}: {(a[0] != b[0]).sum()} pixels differ"
-    assert np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32)), f"{what}: colour planes differ"
+    na, nb = np.isnan(a[1]), np.isnan(b[1])
+    assert np.array_equal(na, nb), f"{what}: NaN positions differ"
+    assert np.array_equal(a[1].view(np.uint32)[~na], b[1].view(np.uint32)[~nb]), f"{what}: colour planes differ"
 
 
 def _check(gpu_ctx, plain_ctx, s, cam, p, what, exact_oracle):
@@ -73,7 +77,9 @@ def _check(gpu_ctx, plain_ctx, s, cam, p, what, exact_oracle):
     q = plain_ctx.render(cam, p)
     _same(g, q, f"{what} cull vs no cull")
     r = oracle_bind.render(s, cam, p)
-    d = float(np.abs(g[1] - r[1]).max(initial=0.0))
+    assert np.array_equal(np.isnan(g[1]), np.isnan(r[1])), f"{what}: NaN positions differ from the oracle's"
+    ok = ~np.isnan(r[1])
+    d = float(np.abs(g[1][ok] - r[1][ok]).max(initial=0.0))
     assert d <= 1e-4, f"{what}: max-abs {d} vs the oracle"
     if exact_oracle:
         _same(g, r, f"{what} vs oracle")
@@ -184,28 +190,124 @@ def test_cull_enabled_where_it_pays(product_ctx, name, on):
     assert product_ctx.cull_info()[0] == on
 
 
-def test_cull_skipped_for_animated_uploads(plain_ctx):
-    """An animated loop re-uploads every frame and renders it once: after two such uploads the
-    records are not built (they would cost more than the one frame gains), and an upload rendered
-    twice or more turns the cull back on.  Every frame equals the unculled walk's and the reference's."""
+def _animated_loop(ctx, plain_ctx, renders_per_upload):
+    hs = HostScene("W4_Optional")
+    p = abi.make_params(96, 64)
+    seen = []
+    for k, renders in enumerate(renders_per_upload):
+        hs.update(0.05 * k)
+        s, cam = hs.view()
+        ctx.upload(s)
+        seen.append(ctx.cull_info()[0])
+        for _ in range(renders):
+            px, rgb = ctx.render(cam, p)
+        plain_ctx.upload(s)
+        _same((px, rgb), plain_ctx.render(cam, p), f"upload {k + 1}")   # bit for bit, both planes
+        assert np.array_equal(px, oracle_bind.render(s, cam, p)[0]), k   # (Cook-Torrance: powf in rgb)
+    return seen
+
+
+def test_cull_records_built_for_animated_uploads(plain_ctx):
+    """An animated loop re-uploads every frame and renders it once; the segment-tree records
+    cost tens of microseconds, so every upload gets them (round 4 skipped them after two such
+    uploads).  Every frame equals the unculled walk's and the reference's."""
     ctx = _ctx_env()
     try:
-        hs = HostScene("W4_Optional")
-        p = abi.make_params(96, 64)
-        seen = []
-        for k, renders in enumerate([1, 1, 1, 1, 3, 1, 1]):
-            hs.update(0.05 * k)
-            s, cam = hs.view()
-            ctx.upload(s)
-            seen.append(ctx.cull_info()[0])
-            for _ in range(renders):
-                px, rgb = ctx.render(cam, p)
-            plain_ctx.upload(s)
-            _same((px, rgb), plain_ctx.render(cam, p), f"upload {k + 1}")   # bit for bit, both planes
-            assert np.array_equal(px, oracle_bind.render(s, cam, p)[0]), k   # (Cook-Torrance: powf in rgb)
+        assert _animated_loop(ctx, plain_ctx, [1, 1, 1, 1, 3, 1, 1]) == [True] * 7
+    finally:
+        ctx.close()
+
+
+def test_cull_animated_skip_rule_opt_in(plain_ctx):
+    """RTX_CULL_ANIMATED=0 keeps round 4's rule: after two consecutive uploads rendered at most
+    once each the records are not built, and an upload rendered twice or more turns them back on."""
+    ctx = _ctx_env(RTX_CULL_ANIMATED="0")
+    try:
+        seen = _animated_loop(ctx, plain_ctx, [1, 1, 1, 1, 3, 1, 1])
         # uploads 1-2 follow at most one short upload, 3-5 two or more; 6 follows an upload rendered
         # three times, 7 one short upload
         assert seen == [True, True, False, False, False, True, True], seen
+    finally:
+        ctx.close()
+
+
+# ---------------------------------------------------------------- the records themselves
+_REF = None
+
+
+def _records_ref():
+    global _REF
+    if _REF is None:
+        from pathlib import Path
+        so = Path(__file__).resolve().parents[1] / "tools" / "bin" / "libcull_records_ref.so"
+        if not so.exists():
+            pytest.fail(f"{so} missing: run __graft_entry__.build()")
+        _REF = C.CDLL(str(so))
+        VP = C.c_void_p
+        _REF.cull_records_ref.argtypes = [C.c_uint32, C.c_uint32, VP, VP, VP, VP, C.c_float, C.c_int, VP]
+        _REF.cull_records_ref.restype = C.c_int
+    return _REF
+
+
+def _dump(ctx, anchor):
+    ns, nt = C.c_uint32(), C.c_uint32()
+    abi.check(ctx.lib.rtx_cull_dump(ctx.h, anchor, C.byref(ns), C.byref(nt), None, None, None, None, None), "dump",
+              ctx.h)
+    a = np.zeros(5, np.float32)
+    rec = np.zeros(8 * ns.value, np.float32)
+    rng = np.zeros(2 * ns.value, np.uint32)
+    nodes = np.zeros(8 * ns.value, np.float32)
+    tris = np.zeros(16 * nt.value, np.float32)
+    abi.check(ctx.lib.rtx_cull_dump(ctx.h, anchor, C.byref(ns), C.byref(nt), a.ctypes.data, rec.ctypes.data,
+                                    rng.ctypes.data, nodes.ctypes.data, tris.ctypes.data), "dump", ctx.h)
+    return a, rec, rng, nodes, tris, nt.value
+
+
+@pytest.mark.parametrize("name", ["Synthetic100k", "W4_Optional"])
+@pytest.mark.parametrize("top", ["lds", "global"])
+def test_cull_records_equal_brute_force(name, top):
+    """Every record of the segment-tree build (rtx_cull_tris_*, rtx_cull_nodes) equals, value for
+    value, the direct fold of every triangle of the slot's range (tools/cull_records_ref.c, the
+    same double-precision bound, rtx_cull.h): camera anchors of two views, at upload and after a
+    camera move, and every light anchor.  "global": the trees' top levels built in global memory
+    (RTX_CULL_TOP_LDS=0) instead of LDS."""
+    env = {"RTX_CULL_MIN_SA": "0"}
+    if top == "global":
+        env["RTX_CULL_TOP_LDS"] = "0"
+    ctx = _ctx_env(**env)
+    try:
+        hs = HostScene(name)
+        s, cam = hs.view()
+        ctx.upload(s)
+        W, H = 64, 48
+        views = (abi.Camera * 2)()
+        for f in range(2):
+            C.memmove(C.byref(views[f]), C.byref(cam), C.sizeof(abi.Camera))
+            views[f].origin[0] = cam.origin[0] + 0.6 * f
+        p = abi.make_params(W, H)
+        abi.check(ctx.lib.rtx_render_views_async(ctx.h, views, 2, C.byref(p), 0), "views", ctx.h)
+        ref = _records_ref()
+        anchors = [0, 1] + [8 + l for l in range(s.n_lights)]
+        checked = 0
+        for step in range(2):
+            if step == 1:   # move view 0's camera: its records are rebuilt alone
+                views[0].origin[2] = cam.origin[2] + 0.7
+                abi.check(ctx.lib.rtx_render_views_async(ctx.h, views, 2, C.byref(p), 0), "views", ctx.h)
+                anchors = [0]
+            for j in anchors:
+                a, rec, rng, nodes, tris, nt = _dump(ctx, j)
+                if j < 8:
+                    assert tuple(a[:3]) == tuple(np.float32(x) for x in views[j].origin), j
+                want = np.zeros_like(rec)
+                ref.cull_records_ref(len(rng) // 2, nt, rng.ctypes.data, nodes.ctypes.data, tris.ctypes.data,
+                                     a.ctypes.data, 1.5, 0, want.ctypes.data)
+                r8, w8 = rec.reshape(-1, 8), want.reshape(-1, 8)
+                bad = np.nonzero(~np.all((r8[:, :7] == w8[:, :7]) & (r8[:, 7:].view(np.uint32) ==
+                                                                     w8[:, 7:].view(np.uint32)), axis=1))[0]
+                assert bad.size == 0, (f"{name} anchor {j} step {step}: {bad.size} of {len(r8)} records differ, "
+                                       f"first slot {bad[0]}: {r8[bad[0]]} vs {w8[bad[0]]}")
+                checked += 1
+        assert checked == 3 + s.n_lights
     finally:
         ctx.close()
 
@@ -253,3 +355,161 @@ def test_cull_ordered_walk_ties(cull_ctx, plain_ctx, tmp_path):
     s, cam = hs.view()
     for mode in (3, 0):
         _check(cull_ctx, plain_ctx, s, cam, abi.make_params(256, 192, mode, 1), f"dup/m{mode}", True)
+
+
+# ---------------------------------------------------------------- W4_Optional and light anchors
+def _optional_geometry():
+    hs = HostScene("W4_Optional")
+    a = hs.arrays()["meshes"][0]
+    P = a["tpositions"].reshape(-1, 3)
+    I = a["indices"].reshape(-1, 3)
+    N = a["tnormals"].reshape(-1, 3)
+    return P, I, N
+
+
+def _optional_cameras():
+    P, I, _ = _optional_geometry()
+    v0, v1, v2 = P[I[1234, 0]], P[I[1234, 1]], P[I[1234, 2]]
+    e1, e2 = (v1 - v0).astype(np.float32), (v2 - v0).astype(np.float32)
+    in_plane = (v0 + np.float32(3.0) * e1 - np.float32(2.0) * e2).astype(np.float32)
+    lo, hi = P.min(0), P.max(0)
+    mid = (0.5 * (lo + hi)).astype(np.float32)
+    return [
+        ("reference", (0.0, 2.0, -9.0), 45.0, 0.0, 0.0),
+        ("in_a_triangle_plane", tuple(float(x) for x in in_plane), 60.0, -0.3, 0.4),
+        ("at_a_vertex", tuple(float(x) for x in v0), 70.0, -0.2, 0.5),
+        ("inside_the_mesh", tuple(float(x) for x in mid), 90.0, 0.1, 0.0),
+        ("grazing_the_top", (float(mid[0]), float(hi[1]) + 1e-3, float(lo[2]) - 2.0), 40.0, -0.0005, 0.0),
+        ("grazing_a_side", (float(hi[0]) + 1e-3, float(mid[1]), float(lo[2]) - 2.0), 40.0, 0.0, 0.0005),
+    ]
+
+
+@pytest.mark.parametrize("cam_case", _optional_cameras(), ids=lambda c: c[0])
+def test_cull_adversarial_cameras_optional(cull_ctx, plain_ctx, cam_case):
+    """W4_Optional (the other scene the product culls: Cook-Torrance, the irregular Assignment3D1
+    mesh with slivers) from cameras in a triangle's plane, at a vertex, inside the mesh and
+    grazing it.  Combined mode: bit for bit against the unculled walk, within 1e-4 of the oracle;
+    ObservedArea (no powf): bit for bit against the oracle too."""
+    what, origin, fov, pitch, yaw = cam_case
+    hs = HostScene("W4_Optional")
+    hs.set_camera(origin, fov, pitch, yaw)
+    s, cam = hs.view()
+    _check(cull_ctx, plain_ctx, s, cam, abi.make_params(240, 160), what, False)
+    _check(cull_ctx, plain_ctx, s, cam, abi.make_params(240, 160, 0, 1), what + "/observed", True)
+
+
+def _light_cases():
+    P, I, N = _optional_geometry()
+    k = 2021
+    v0, v1, v2 = P[I[k, 0]], P[I[k, 1]], P[I[k, 2]]
+    e1, e2 = (v1 - v0).astype(np.float32), (v2 - v0).astype(np.float32)
+    n = N[k] / np.linalg.norm(N[k])
+    cen = ((v0 + v1 + v2) / np.float32(3)).astype(np.float32)
+    # the centre pixel's shadow-ray origin for a camera at (0, 6, -5) looking along +z: the back
+    # wall (z = 10, normal -z) hit at (0, 6, 10), offset by 0.0001f along the normal
+    on_origin = (0.0, 6.0, float(np.float32(10.0) - np.float32(0.0001)))
+    return [
+        ("in_a_triangle_plane", tuple(float(x) for x in (v0 + np.float32(3) * e1 - np.float32(2) * e2))),
+        ("1e-3_from_a_face", tuple(float(x) for x in (cen + np.float32(1e-3) * n.astype(np.float32)))),
+        ("on_a_vertex", tuple(float(x) for x in v0)),
+        ("next_to_the_mesh", tuple(float(x) for x in (cen + np.float32(0.05) * n.astype(np.float32)))),
+        ("on_a_shadow_origin", on_origin),
+    ]
+
+
+@pytest.mark.parametrize("light_case", _light_cases(), ids=lambda c: c[0])
+def test_cull_adversarial_lights(cull_ctx, plain_ctx, light_case):
+    """The light-anchor bound (rtx_cull_light_bounds) at its edges: a point light in a mesh
+    triangle's plane, 1e-3 from a face, on a vertex, next to the mesh (its cull bound T = 4 x the
+    farthest mesh-box corner + 1 is small, so shadow rays from the walls are longer than T and must
+    pass unculled), and exactly on the centre pixel's shadow-ray origin (|L - o| = 0, outside the
+    bound's domain).  Light 0 of W4_Optional moves there; the camera looks at the mesh (and, for
+    the last case, at the back wall along +z with an odd-sized frame so the centre ray is exactly
+    +z).  Bit for bit against the unculled walk, ObservedArea bit for bit against the oracle."""
+    what, L = light_case
+    hs = HostScene("W4_Optional")
+    if what == "on_a_shadow_origin":
+        hs.set_camera((0.0, 6.0, -5.0), 45.0, 0.0, 0.0)
+        W, H = 161, 121
+    else:
+        W, H = 240, 160
+    s, cam = hs.view()
+    for k in range(3):
+        s.lights[0].origin[k] = L[k]
+    if what == "on_a_shadow_origin":
+        assert tuple(cam.forward) == (0.0, 0.0, 1.0)
+    _check(cull_ctx, plain_ctx, s, cam, abi.make_params(W, H), what, False)
+    _check(cull_ctx, plain_ctx, s, cam, abi.make_params(W, H, 0, 1), what + "/observed", True)
+    ok = C.c_uint32()
+    abi.check(cull_ctx.lib.rtx_cull_info(cull_ctx.h, C.byref(ok), None), "info", cull_ctx.h)
+    assert ok.value == 1
+
+
+def test_cull_ordered_walk_tie_break_is_observable(cull_ctx, plain_ctx, tmp_path):
+    """The tie test above cannot see a wrong tie-break: duplicate faces shade identically.  Here
+    each duplicate pair gets DIFFERENT normals (the stored per-triangle normals are a separate
+    input; the copy's is tilted, same side as the original's so back-face culling is unchanged
+    for the view), so the pixel shows which triangle won.  The frame must equal the unculled walk's
+    and the oracle's, and must differ from the oracle's frame with each pair's normals swapped —
+    what a walk resolving ties to the higher index would show."""
+    rng = np.random.default_rng(11)
+    n = 20
+    lines = []
+    for j in range(n + 1):
+        for i in range(n + 1):
+            lines.append(f"v {-2 + 4 * i / n:.6f} {0.2 + 0.6 * rng.random():.6f} {-1 + 3 * j / n:.6f}")
+    for j in range(n):
+        for i in range(n):
+            a, b, c, d = j * (n + 1) + i + 1, j * (n + 1) + i + 2, (j + 1) * (n + 1) + i + 1, (j + 1) * (n + 1) + i + 2
+            for tri in ((a, c, b), (b, c, d)):
+                lines.append("f %d %d %d" % tri)
+                lines.append("f %d %d %d" % tri)
+    (tmp_path / "dup_grid.obj").write_text("\n".join(lines) + "\n")
+    scene = tmp_path / "dup.rtxscene"
+    scene.write_text("camera 0 3 -7 45\nmaterial lambert 1 1 1 1\nmaterial lambert 0.49 0.57 0.57 1\n"
+                     "mesh dup_grid 1 back\nplane 0 0 0 0 1 0 2\nlight point 0 5 -2 50 1 0.61 0.45\n"
+                     "light point -3 4 1 40 1 0.8 0.45\n")
+    hs = HostScene(f"file:{scene}", asset_dir=str(tmp_path))
+    s, cam = hs.view()
+    m = s.meshes[0]
+    nt = m.n_indices // 3
+    idx = np.ctypeslib.as_array(m.indices, shape=(3 * nt,)).reshape(-1, 3)
+    nrm = np.ctypeslib.as_array(m.normals, shape=(3 * nt,)).reshape(-1, 3).copy()
+    # duplicate pairs in the BVH's (permuted) triangle order
+    first = {}
+    pairs = []
+    for t in range(nt):
+        key = tuple(idx[t])
+        if key in first:
+            pairs.append((first.pop(key), t))
+        else:
+            first[key] = t
+    assert len(pairs) == nt // 2
+    tilted = nrm.copy()
+    for lo, hi in pairs:   # the later copy's normal tilted ~25 degrees about x
+        x, y, z = nrm[hi]
+        c, sn = np.float32(0.906), np.float32(0.423)
+        tilted[hi] = (x, y * c - z * sn, y * sn + z * c)
+
+    def with_normals(arr):
+        buf = np.ascontiguousarray(arr.astype(np.float32).reshape(-1))
+        mm = abi.Mesh()
+        C.memmove(C.byref(mm), C.byref(m), C.sizeof(abi.Mesh))
+        mm.normals = buf.ctypes.data_as(C.POINTER(C.c_float))
+        sc = abi.Scene()
+        C.memmove(C.byref(sc), C.byref(s), C.sizeof(abi.Scene))
+        marr = (abi.Mesh * 1)(mm)
+        sc.meshes = C.cast(marr, C.POINTER(abi.Mesh))
+        sc._keep = (buf, marr, s)
+        return sc
+
+    sA = with_normals(tilted)
+    swapped = tilted.copy()
+    for lo, hi in pairs:
+        swapped[[lo, hi]] = swapped[[hi, lo]]
+    sB = with_normals(swapped)
+    p = abi.make_params(256, 192, 0, 1)   # ObservedArea: the normal shows directly
+    _check(cull_ctx, plain_ctx, sA, cam, p, "tilted duplicates", True)
+    ra = oracle_bind.render(sA, cam, p)[0]
+    rb = oracle_bind.render(sB, cam, p)[0]
+    assert (ra != rb).sum() > 1000, "the swapped tie-break must be visible"

@@ -151,3 +151,27 @@ def test_scene_file_errors(tmp_path, text, msg):
     f.write_text(text)
     with pytest.raises(RuntimeError, match=re.escape(msg) if msg.startswith(":") else msg):
         HostScene(f"file:{f}")
+
+
+def test_view_keeps_its_scene_alive():
+    """`HostScene(name).view()` with no other reference to the HostScene: the returned Scene
+    holds the owner, so its pointers stay valid after a garbage collection (round 4 uploaded
+    freed memory this way)."""
+    import ctypes as C
+    import gc
+
+    import numpy as np
+
+    ref_s, _ = HostScene("Synthetic100k").view()   # noqa: F841 (kept alive by the Scene itself)
+    keep = HostScene("Synthetic100k")
+    want = keep.arrays()["meshes"][0]
+    s, cam = HostScene("Synthetic100k").view()
+    gc.collect()
+    junk = [HostScene("W4_Bunny") for _ in range(3)]   # reuse freed memory if it were freed
+    m = s.meshes[0]
+    got = np.ctypeslib.as_array(m.positions, shape=(m.n_positions * 3,)).copy()
+    idx = np.ctypeslib.as_array(m.indices, shape=(m.n_indices,)).copy()
+    assert np.array_equal(got, want["tpositions"]) and np.array_equal(idx, want["indices"])
+    assert tuple(cam.origin) == tuple(keep.view()[1].origin)
+    assert C.cast(m.positions, C.c_void_p).value is not None
+    del junk
