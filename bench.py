@@ -84,10 +84,16 @@ LIB_HIP = ROOT / "gp1_raytracer_2223_amd" / "lib" / "librtx_hip.so"
 # 1469598103934665603; SURVEY §8(c)'s recorded hashes use the same one.
 FNV_BASIS = 1469598103934665603
 COST = [41, 19, 14, 12, 63, 9, 15, 1, 26, 6, 31, 103]   # SURVEY §8(d) FLOP per counted unit
+# the exact cull's box test per lane (cull_nf + cull_pass, rtx_hip.hip): (c - o) * inv 6, three fma
+# 6, n / f 6 add + 4 min/max, n - dt 1 — counted only in the executed-work model (frac_executed)
+COST_CULL_TEST = 23
 K_KERNEL_LAUNCHES = 1000   # launches averaged for the headline's roofline.kernel_ms
 
 # BASELINE.json's multi-GPU workloads: one image per step, tiled over the ranks (steps per run)
-MULTI_GPU_CONFIGS = [("Synthetic100k", 1920, 1080, 100), ("Bunny8Lights", 3840, 2160, 300)]
+# (+ W4_Optional: with Synthetic100k the scene the exact cull runs on, so its line carries the
+# executed-work roofline, frac_executed, beside the reference-equivalent one)
+MULTI_GPU_CONFIGS = [("Synthetic100k", 1920, 1080, 100), ("Bunny8Lights", 3840, 2160, 300),
+                     ("W4_Optional", 1920, 1080, 300)]
 # parity_configs: (scene, W, H, bit-exact required).  Cook-Torrance / Phong use powf, where the
 # device libm may differ from glibc by an ulp: those are held to the north star's tolerance.
 PARITY_CONFIGS = [("W1", 640, 480, True), ("W3", 1280, 720, False), ("W4_Bunny", 1920, 1080, True),
@@ -468,6 +474,19 @@ class Workload:
         step_flop, step_pixels = self.d.sum_i64([flop, pixels])
         return flop, pixels, step_flop, step_pixels
 
+    def flop_executed(self) -> tuple[int, list]:
+        """The same model over the walk the product executes (rtx_count_work_culled: the exact
+        cull's pruned, ordered walk, one-piece frame) plus its cull box tests: (flop of this
+        rank's launch, the 15 counters)."""
+        N, r = self.d.world, self.d.rank
+        counts = np.zeros(15, np.uint64)
+        for f in range(self.nviews):
+            pv = abi.make_params(self.W, self.H, stripe_rows=16 if self.striped else 0,
+                                 stripe_first=(r - f) % N if self.mode == "views" else r, stripe_step=N)
+            counts += self.ctxs[0].count_work_culled(self.views[f], pv)
+        flop = int(sum(int(c) * w for c, w in zip(counts[:12], COST))) + int(counts[14]) * COST_CULL_TEST
+        return flop, [int(x) for x in counts]
+
     def run(self, steps: int, warmup: int, launches: int, gather: bool, tag: str) -> dict:
         d, W, H = self.d, self.W, self.H
         kernel_ms = self.kernel_ms(launches)
@@ -517,6 +536,13 @@ class Workload:
         return {"kernel_ms": kernel_ms, "elapsed": elapsed, "gathered": gathered, "flop": flop, "pixels": pixels,
                 "step_flop": step_flop, "step_pixels": step_pixels, "px0": px0, "rgb0": rgb0,
                 "value": self.frame_pixels * steps / elapsed / 1e6, "ms_per_step": elapsed / steps * 1e3}
+
+
+def wl_ref_counts(wl: "Workload") -> list:
+    """The reference traversal's counters of the workload's rank-0 view (rtx_count_work)."""
+    N, r = wl.d.world, wl.d.rank
+    pv = abi.make_params(wl.W, wl.H, stripe_rows=16 if wl.striped else 0, stripe_first=r, stripe_step=N)
+    return [int(x) for x in wl.ctxs[0].count_work(wl.views[0], pv)]
 
 
 def stripe_predictor(ctx: DeviceContext, wl: "Workload", lib_hash: str, steps=(2, 4, 8), launches: int = 30) -> dict:
@@ -669,7 +695,19 @@ def main() -> int:
                 #  proves most of those slab and triangle tests unnecessary and skips them
                 entry["roofline_rank0"]["flop_basis"] = (
                     "reference-equivalent: the model's FLOP of the reference's traversal over the measured time; "
-                    "the exact cull skips most of those tests, so this is an effective rate, not executed FLOP")
+                    "the exact cull skips most of those tests, so this is an effective rate, not executed FLOP; "
+                    "frac_executed: the same model over the tests the culled walk executes")
+                fx, cx = wl.flop_executed()
+                ach = fx / (r["kernel_ms"] * 1e-3) / 1e12 if r["kernel_ms"] > 0 else 0.0
+                entry["roofline_rank0"].update({
+                    "flop_executed_per_launch": fx, "achieved_executed": round(ach, 4),
+                    "frac_executed": round(ach / FP32_PEAK_TFLOPS, 5),
+                    "executed_vs_reference": {"slab_tests": round(cx[3] / max(1, wl_ref_counts(wl)[3]), 4),
+                                              "triangle_tests": round(cx[4] / max(1, wl_ref_counts(wl)[4]), 4),
+                                              "cull_box_tests": cx[14]},
+                    "flop_executed_basis": ("rtx_count_work_culled: per-lane slab / triangle / cull-box tests of the "
+                                            "culled ordered walk (one-piece frame: the split launches' repeated path "
+                                            "tests are not counted), SURVEY §8(d) costs + 23 FLOP per cull box test")})
             if d.rank == 0:
                 entry["parity"] = parity_report(r["px0"], r["rgb0"], scene, mw, mh, with_fnv=False)
             if N == 1:

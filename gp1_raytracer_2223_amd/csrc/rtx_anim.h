@@ -95,9 +95,11 @@ struct MeshDev {
 // update (the mesh stays disabled); 8.. phase stamps (s_memrealtime, 100 MHz, low 32 bits):
 // 8 build start, 9 set-up done, 10 root split, 11 first subtree start, 12 last subtree end,
 // 13 output start, 14 numbering known (frontier workgroup), 15 frontier done; 16-19 the first
-// four task splits' sizes, 20-27 their start / end
+// four task splits' sizes, 20-27 their start / end; 28 completeness: bit 0 = every triangle reached
+// a final leaf (the tree is complete), bit 1 = a worker timed out although it was (a spurious
+// timeout: reported nowhere else, the mesh stays enabled)
 enum : uint32_t { kStTop0 = 8, kStSetup = 9, kStTopDone = 10, kStSub0 = 11, kStSubEnd = 12, kStOut0 = 13,
-                  kStRanks = 14, kStFrontier = 15 };
+                  kStRanks = 14, kStFrontier = 15, kStComplete = 28 };
 
 struct Image {                   // sections of the destination scene image
     int4* meshes;                // mesh records {root byte offset, nodesUsed, cull, material}
@@ -123,14 +125,23 @@ struct Launch {
     uint32_t cut;                // nodes above this many triangles are split as tasks, smaller ones are subtrees
     uint32_t frontier_max;       // meshes up to this many triangles select the frontier in parallel (else serially)
     uint64_t wait_ticks;         // a worker's wait for a queue entry, s_memrealtime ticks (100 MHz): 200 ms; tests lower it
+    uint32_t debug;              // tests only (RTX_ANIM_DEBUG): kDbgDropEntry, kDbgLateTimeout
 };
+// RTX_ANIM_DEBUG bits (tests of the timeout path): kDbgDropEntry — the worker that takes queue entry
+// 0 drops it as if it had timed out before it was published (the tree is then incomplete);
+// kDbgLateTimeout — workers that leave because the tree is complete also report a timeout (as a
+// worker whose wait ran out just as the last triangles were placed would)
+enum : uint32_t { kDbgDropEntry = 1u, kDbgLateTimeout = 2u };
 constexpr uint32_t kTopLdsTris = 3136;   // the largest top_lds (rtx_anim.hip's LDS budget)
 constexpr uint32_t kFrontierHistMax = 4096;   // the largest frontier_max (the count histogram's bins)
 
 // kErrTimeout: a worker gave up waiting for a queue entry (Launch::wait_ticks); kErrCapacity: a
-// task-queue or subtree-table guard fired.  Both leave the tree incomplete: the output launch then
-// writes none of it and disables the mesh in the image (no frontier parts, node count 0), as for
-// kErrDepth.
+// task-queue or subtree-table guard fired.  A timeout leaves the tree incomplete only when the entry
+// the worker claimed was a real task (published later, then never run); a worker waiting on an
+// index no task ever takes gives up harmlessly.  The output launch tells the two apart by whether
+// every triangle reached a final leaf (status word kStComplete): an incomplete tree (and any
+// capacity error) is not written and the mesh is disabled in the image (no frontier parts, node
+// count 0), as for kErrDepth; a complete one is written as usual and the timeout bit is cleared.
 enum : uint32_t { kErrNaN = 1u, kErrDepth = 2u, kErrTimeout = 4u, kErrCapacity = 8u };
 constexpr uint64_t kWaitTicks = 20000000ull;   // Launch::wait_ticks' default: 200 ms at 100 MHz
 

@@ -35,6 +35,13 @@
 #include "rtx_kernels.h"
 
 namespace rtxa {
+
+// Triangles placed in final leaves: the counter the workers stop on (kQDone), and the mark that
+// the tree is complete once it reaches T (status word kStComplete, read by rtx_anim_out).
+__device__ __forceinline__ void done_add(const MeshDev& M, uint32_t n) {
+    const uint32_t o = atomicAdd(&M.q[kQDone], n);
+    if (o < M.T && o + n >= M.T) atomicOr(&M.status[kStComplete], 1u);
+}
 namespace {
 
 __device__ __forceinline__ float rmin(float m, float x) { return (x < m) ? x : m; }   // std::min(m, x)
@@ -1125,7 +1132,7 @@ __device__ __forceinline__ void dispatch_children(const Launch& L, const MeshDev
     }
     if (K == 0u) {
         atomicMax(&M.status[1], d);
-        atomicAdd(&M.q[kQDone], n);
+        done_add(M, n);
         return;
     }
     atomicMax(&M.status[1], d + 1u);
@@ -1133,7 +1140,7 @@ __device__ __forceinline__ void dispatch_children(const Launch& L, const MeshDev
     for (uint32_t c = c0; c < c0 + 2u; ++c) {
         const uint32_t nc = M.tmp[c].count;
         if (3u * nc <= 8u) {
-            atomicAdd(&M.q[kQDone], nc);
+            done_add(M, nc);
             continue;
         }
         if (nc > L.cut) {
@@ -1258,6 +1265,7 @@ __device__ __forceinline__ void top_phase(const Launch& L, const MeshDev& M, Lev
         M.status[1] = 0u;
         M.status[4] = 0u;
         M.status[6] = 0u;
+        M.status[kStComplete] = 0u;   // before the first task is published (release on push)
         M.status[kStSub0] = 0xffffffffu;
         M.status[kStSubEnd] = 0u;
         M.q[kQSubIds] = kMaxTop;
@@ -1498,7 +1506,7 @@ __device__ __forceinline__ void run_task(const Launch& L, const MeshDev& M, uint
         if (!ranks_ok) atomicOr(&M.status[0], kErrDepth);
         atomicMax(&M.status[kStSubEnd], stamp());
         __threadfence();
-        atomicAdd(&M.q[kQDone], n);
+        done_add(M, n);
     }
 }
 
@@ -1510,8 +1518,10 @@ __device__ __forceinline__ void run_task(const Launch& L, const MeshDev& M, uint
 // blockIdx.x fastest).  One launch with the waits in it instead of a kernel per level: a kernel
 // boundary cost ~100 us before the next workgroups ran (the idle XCDs' start-up, profiles/r03).
 // A waiting worker gives up after Launch::wait_ticks (kWaitTicks = 200 ms of s_memrealtime by
-// default, rtx_anim.h): a stuck build reports, never hangs.  (A worker that gives up leaves the entry it claimed unbuilt, so the tree is
-// incomplete: kErrTimeout, and the output launch disables the mesh, see rtx_anim_out)
+// default, rtx_anim.h): a stuck build reports, never hangs.  (A worker that gives up on a real task
+// leaves it unbuilt, so the tree is incomplete: kErrTimeout, and the output launch disables the
+// mesh; one that gave up on an index no task takes lost nothing: the output launch sees every
+// triangle placed, kStComplete, and keeps the mesh, see rtx_anim_out)
 __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
     const MeshDev& M = L.meshes[blockIdx.x];
     extern __shared__ float s_dyn[];
@@ -1526,7 +1536,10 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
         // triangles is no longer the reference's (each build permutes the previous order,
         // DataTypes.h:335-363), so no later update can be exact.  Build nothing; the output launch
         // keeps the mesh disabled and every update reports the error (re-register to recover).
-        if (blockIdx.y == 0 && tid == 0) M.status[0] = M.status[7];
+        if (blockIdx.y == 0 && tid == 0) {
+            M.status[0] = M.status[7];
+            M.status[kStComplete] = 0u;
+        }
         return;
     }
     if (blockIdx.y == 0) {
@@ -1553,12 +1566,19 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_build(const Launch L) {
             for (;;) {
                 if (i < kQCap && __hip_atomic_load(&e[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == L.epoch) {
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    if ((L.debug & kDbgDropEntry) && i == 0u) {   // tests: lose a real task
+                        atomicOr(&M.status[0], kErrTimeout);
+                        break;
+                    }
                     go = 1;
                     s_task[0] = e[0];
                     s_task[1] = e[1];
                     break;
                 }
-                if (__hip_atomic_load(&M.q[kQDone], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= M.T) break;
+                if (__hip_atomic_load(&M.q[kQDone], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= M.T) {
+                    if (L.debug & kDbgLateTimeout) atomicOr(&M.status[0], kErrTimeout);   // tests
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(RTX_ANIM_POLL_SLEEP);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > L.wait_ticks) {
                     atomicOr(&M.status[0], kErrTimeout);
@@ -1818,6 +1838,10 @@ __device__ __forceinline__ void out_frontier(const Launch& L, const MeshDev& M, 
     }
     if (lane == 0) {
         uint32_t err = M.status[0];
+        if (err & kErrTimeout) {   // (complete, or rtx_anim_out would not have come here): spurious
+            err &= ~kErrTimeout;
+            M.status[kStComplete] |= 2u;
+        }
         if (too_deep) err |= kErrDepth;
         const uint32_t used = nused;   // nodesUsed
         M.status[0] = err;
@@ -1839,11 +1863,17 @@ __global__ void __launch_bounds__(kAnimThreads) rtx_anim_out(const Launch L) {
     const MeshDev& M = L.meshes[blockIdx.y];
     const uint32_t g = blockIdx.x, tid = threadIdx.x;
     const uint32_t T = M.T;
-    if (M.status[0] & (kErrTimeout | kErrCapacity)) {
-        // The build left the tree incomplete (an entry claimed by a worker that gave up, or a
-        // capacity guard): none of its numbering, records or frontier is written — their inputs
-        // may be stale — and the mesh is disabled in the image (the update's template copy leaves
-        // its node region empty): no frontier parts, node count 0, so the render kernel skips it.
+    // Incomplete: a capacity guard fired, or a worker gave up and not every triangle reached a
+    // final leaf (kStComplete: a timeout on an index no task takes loses nothing).  Every workgroup
+    // decides alike: kStComplete is final once the build launch has ended, and the frontier
+    // workgroup clears the timeout bit only when the tree is complete (then either reading of
+    // status word 0 keeps the mesh).
+    const uint32_t err0 = M.status[0];
+    if ((err0 & kErrCapacity) || ((err0 & kErrTimeout) && !(M.status[kStComplete] & 1u))) {
+        // The build left the tree incomplete: none of its numbering, records or frontier is
+        // written — their inputs may be stale — and the mesh is disabled in the image (the
+        // update's template copy leaves its node region empty): no frontier parts, node count 0,
+        // so the render kernel skips it.
         if (g == kOutGroups) {
             for (uint32_t k = tid; k < M.part_cap; k += kAnimThreads) L.img.parts[M.part0 + k] = make_int4(-1, 0, 0, 0);
             if (tid == 0) {

@@ -25,6 +25,7 @@
 #include <new>
 #include <string>
 #include <type_traits>
+#include <array>
 #include <vector>
 
 #include "rtx.h"
@@ -541,11 +542,14 @@ constexpr int kPlaneCache = 8;   // planes whose shadow-ray numerators are kept 
 // order, because left-then-right DFS order is increasing triangle index (the scene has the cull
 // only when that holds, upload_scene; the split launches' key minimum rests on the same fact) — so
 // nearer subtrees lower sc_t before farther ones are tested and cull_pass prunes those.
-template <bool ANY, int SLAB, bool CB = false, bool CULL = false>
+// COUNT (the counting variant of the culled walk, rtx_count_work_culled): per lane, the slab,
+// exact-cull and triangle tests this walk executes for the lane (a lane in the node's mask is
+// tested against both children), in `cp` — the executed work beside the reference's (bvh_walk).
+template <bool ANY, int SLAB, bool CB = false, bool CULL = false, bool COUNT = false>
 __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, const Ray& r, uint32_t link,
                               uint32_t ntri, unsigned long long m, unsigned long long mask, uint32_t lane, uint4* stk,
                               float& sc_t, uint32_t& sc_tri, unsigned long long& live, const uint32_t* occ_word,
-                              uint32_t occ_bit, const CullRay& cq = CullRay{}) {
+                              uint32_t occ_bit, const CullRay& cq = CullRay{}, Counts* cp = nullptr) {
     constexpr bool FAST = SLAB != kSlabExact;
     constexpr bool ORD = CULL && (!ANY || RTX_CULL_ORDER_ANY);
     uint32_t sp = 0;
@@ -553,6 +557,10 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
         while (ntri == 0) {
             NodePair P;
             ldcb64(nb, link, P.l0, P.l1, P.r0, P.r1);
+            if constexpr (COUNT) {
+                if ((m >> lane) & 1ull) cp->c[kSlab] += 2;
+                if (lane == 0) cp->c[kWaveNodeTests]++;
+            }
             unsigned long long ml = slab_mask<SLAB>(P.l0, P.l1, r) & m;
             unsigned long long mr = slab_mask<SLAB>(P.r0, P.r1, r) & m;
             [[maybe_unused]] bool rfirst = false;
@@ -562,6 +570,9 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                 // only pairs whose records are flagged worth testing (cull_write), and only when
                 // some lane entered a child
                 if ((__float_as_uint(Q.l1.w) | __float_as_uint(Q.r1.w)) && (ml | mr)) {
+                    if constexpr (COUNT) {
+                        if ((m >> lane) & 1ull) cp->c[kCullTests] += 2;
+                    }
                     float nl, nr;
                     ml &= cull_pass<ANY>(Q.l0, Q.l1, r, cq, sc_t, nl);
                     mr &= cull_pass<ANY>(Q.r0, Q.r1, r, cq, sc_t, nr);
@@ -614,6 +625,10 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
                 const uint32_t ti = link + k * 64u;
                 Tri T;
                 ldcb64(S.tris, ti, T.a, T.b, T.c, T.d);
+                if constexpr (COUNT) {
+                    if (((ANY ? (m & live) : m) >> lane) & 1ull) cp->c[kTri]++;
+                    if (lane == 0) cp->c[kWaveTriTests]++;
+                }
                 float t;
                 float rej;
                 if (!tri_t_wave<FAST, CB, ANY>(T.a, T.b, T.c, cs, r, ANY ? (m & live) : m, rej, t)) continue;
@@ -654,7 +669,7 @@ template <bool ANY, int SLAB, bool COUNT, bool CB = false, bool CULL = false>
 __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int oct, unsigned long long mask,
                               uint32_t lane, uint4* stk, unsigned long long* sT, float& sc_t, uint32_t& sc_tri,
                               unsigned long long& live, Counts& cnt, const CullRay& cq = CullRay{}) {
-    static_assert(!CULL || (SLAB != kSlabExact && !COUNT), "the cull runs in FAST batches of the lean walk only");
+    static_assert(!CULL || SLAB != kSlabExact, "the cull runs in FAST batches of the lean walk only");
     constexpr bool FAST = SLAB != kSlabExact;
     if (M.y == 0) return;
     const bool OCT = SLAB == kSlabOct && !COUNT && !RTX_STAMPS_WALK;
@@ -671,13 +686,16 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
         float4 c0, c1;
         ldcb32(cq.base, static_cast<uint32_t>(M.x), c0, c1);
         float n;
-        if (__float_as_uint(c1.w)) m &= cull_pass<ANY>(c0, c1, r, cq, sc_t, n);
+        if (__float_as_uint(c1.w)) {
+            if (COUNT && ((m >> lane) & 1ull)) cnt.c[kCullTests]++;
+            m &= cull_pass<ANY>(c0, c1, r, cq, sc_t, n);
+        }
     }
     if (m == 0) return;
-    if (!COUNT && !RTX_STAMPS_WALK)
-        bvh_walk_lean<ANY, OCT ? kSlabOct : (FAST ? kSlabFast : kSlabExact), CB, CULL>(
+    if ((!COUNT || CULL) && !RTX_STAMPS_WALK)
+        bvh_walk_lean<ANY, OCT ? kSlabOct : (FAST ? kSlabFast : kSlabExact), CB, CULL, COUNT>(
             S, nb, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask, lane, stk, sc_t,
-            sc_tri, live, nullptr, 0u, cq);
+            sc_tri, live, nullptr, 0u, cq, &cnt);
     else
         bvh_walk<ANY, FAST, COUNT>(S, cull_sign(M.z, ANY), r, __float_as_uint(b1.z), __float_as_uint(b1.w), m, mask,
                                    lane, stk, sT, sc_t, sc_tri, live, cnt);
@@ -692,11 +710,13 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
 // SLAB = kSlabOct: `oct` is the batch's octant (batch_octant) and the part walks that copy.
 // CB: kSpecCullBack (tri_t_wave).
 // CULL: as mesh_traverse, on the part's path and below it.
+// walk_dt (motion mode, FrameArgs::part_cost): gets the duration of the walk below E (0 when no
+// lane reaches E), the part's share of the tile's one-piece cost.
 template <bool ANY, int SLAB, bool CB = false, bool CULL = false>
 __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int oct, unsigned long long mask,
                               uint32_t lane, uint4* stk, float& sc_t, uint32_t& sc_tri, unsigned long long& live,
                               Counts& cnt, const uint32_t* occ_word = nullptr, uint32_t occ_bit = 0,
-                              const CullRay& cq = CullRay{}) {
+                              const CullRay& cq = CullRay{}, unsigned long long* walk_dt = nullptr) {
     static_assert(!CULL || SLAB != kSlabExact, "the cull runs in FAST batches only");
     constexpr bool FAST = SLAB != kSlabExact;
     if (E.x < 0) return;   // unused entry of a device-animated mesh's reserved frontier
@@ -731,12 +751,14 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int
         ntri = __float_as_uint(c1.w);
     }
     if (m == 0) return;
+    const unsigned long long t0 = walk_dt ? __builtin_amdgcn_s_memtime() : 0ull;
     if (!RTX_STAMPS_WALK)
         bvh_walk_lean<ANY, SLAB, CB, CULL>(S, nb, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, sc_t,
                                            sc_tri, live, occ_word, occ_bit, cq);
     else
         bvh_walk<ANY, FAST, false>(S, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, nullptr, sc_t, sc_tri,
                                    live, cnt, occ_word, occ_bit);
+    if (walk_dt) *walk_dt = __builtin_amdgcn_s_memtime() - t0;
 }
 
 struct RGB {
@@ -799,6 +821,16 @@ __device__ __forceinline__ RGB shade(const DevScene& S, uint32_t mi, float nx, f
         c.b = (m0.w * kb) / RTX_PI + ((Fb * D) * G) / den;
     }
     return c;
+}
+
+// motion mode (FrameArgs::part_cost): a split launch's wave adds the duration of its walk below
+// its frontier part (cycles) to its tile's cost, in the tile cost's unit (16 cycles).  The parts'
+// walks partition the one-piece walk, so their sum stands for the tile's one-piece cost without
+// each part wave's fixed work (ray, planes, the part's path), which would keep a tile that stopped
+// being heavy in the split set.
+__device__ __forceinline__ void part_cost_add(uint32_t* cost, unsigned long long dt) {
+    dt >>= 4;
+    atomicAdd(cost, static_cast<uint32_t>(dt < 0xffffffffull ? dt : 0xffffffffull));
 }
 
 __device__ __forceinline__ uint32_t q8(float c) {
@@ -942,7 +974,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
     const int poct = (fast && S.oct_bytes && PHASE == 0) ? batch_octant(vr, active) : -1;
     // exact cull of the view's camera anchor (FAST waves; a direction normalised from a magnitude
     // of at least 2^-30 has |d| = 1 +- 3u, which the bound assumes)
-    constexpr bool kCull = CULLK && !COUNT && !RTX_STAMPS_WALK;
+    constexpr bool kCull = CULLK && !RTX_STAMPS_WALK;   // (with COUNT: rtx_count_work_culled)
     const bool pcull = kCull && S.cull_stride && fast && (PHASE == 0 || PHASE == 1);
     CullRay pq{};
     if (pcull)
@@ -1038,20 +1070,26 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         uint32_t sc_tri = 0;
         unsigned long long unused = 0;
         const int oct = (fast && S.oct_bytes) ? batch_octant(vr, active) : -1;
+        unsigned long long wdt = 0;
+        unsigned long long* const wp = (F.part_cost && F.cost) ? &wdt : nullptr;
         if (oct >= 0 && pcull)
             part_traverse<false, kSlabOct, kCullBack, kCull>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri, unused,
-                                                             cnt, nullptr, 0u, pq);
+                                                             cnt, nullptr, 0u, pq, wp);
         else if (oct >= 0)
-            part_traverse<false, kSlabOct, kCullBack>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri, unused, cnt);
+            part_traverse<false, kSlabOct, kCullBack>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri, unused, cnt,
+                                                      nullptr, 0u, CullRay{}, wp);
         else if (fast && pcull)
             part_traverse<false, kSlabFast, kCullBack, kCull>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused,
-                                                              cnt, nullptr, 0u, pq);
+                                                              cnt, nullptr, 0u, pq, wp);
         else if (fast)
-            part_traverse<false, kSlabFast, kCullBack>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused, cnt);
+            part_traverse<false, kSlabFast, kCullBack>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused, cnt,
+                                                       nullptr, 0u, CullRay{}, wp);
         else
-            part_traverse<false, kSlabExact, kCullBack>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused, cnt);
+            part_traverse<false, kSlabExact, kCullBack>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused, cnt,
+                                                        nullptr, 0u, CullRay{}, wp);
         if (valid && sc_t < sc0)   // accepted t >= tmin > 0: the float bits order like the values
             atomicMin(&F.hit_key[slot], (static_cast<unsigned long long>(__float_as_uint(sc_t)) << 32) | sc_tri);
+        if (wp && lane == 0 && wdt) part_cost_add(F.cost + tile, wdt);
         RTX_SPLIT_STAMP();
         return;
     } else {
@@ -1204,22 +1242,25 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                     float st = 0.f;
                     uint32_t stri = 0;
                     const int poct2 = (sfast && S.oct_bytes) ? batch_octant(sr, hitmask) : -1;
+                    unsigned long long wdt = 0;
+                    unsigned long long* const wp = (F.part_cost && F.cost) ? &wdt : nullptr;
                     if (poct2 >= 0 && scull)
                         part_traverse<true, kSlabOct, kCullBack, kCull>(S, E, sr, poct2, live, lane, stk, st, stri, live,
-                                                                        cnt, &F.occ_bits[slot], 1u << li, sq);
+                                                                        cnt, &F.occ_bits[slot], 1u << li, sq, wp);
                     else if (poct2 >= 0)
                         part_traverse<true, kSlabOct, kCullBack>(S, E, sr, poct2, live, lane, stk, st, stri, live, cnt,
-                                                                 &F.occ_bits[slot], 1u << li);
+                                                                 &F.occ_bits[slot], 1u << li, CullRay{}, wp);
                     else if (sfast && scull)
                         part_traverse<true, kSlabFast, kCullBack, kCull>(S, E, sr, 0, live, lane, stk, st, stri, live,
-                                                                         cnt, &F.occ_bits[slot], 1u << li, sq);
+                                                                         cnt, &F.occ_bits[slot], 1u << li, sq, wp);
                     else if (sfast)
                         part_traverse<true, kSlabFast, kCullBack>(S, E, sr, 0, live, lane, stk, st, stri, live, cnt,
-                                                                  &F.occ_bits[slot], 1u << li);
+                                                                  &F.occ_bits[slot], 1u << li, CullRay{}, wp);
                     else
                         part_traverse<true, kSlabExact, kCullBack>(S, E, sr, 0, live, lane, stk, st, stri, live, cnt,
-                                                                   &F.occ_bits[slot], 1u << li);
+                                                                   &F.occ_bits[slot], 1u << li, CullRay{}, wp);
                     if (did && !((live >> lane) & 1ull)) atomicOr(&F.occ_bits[slot], 1u << li);
+                    if (wp && lane == 0 && wdt) part_cost_add(F.cost + tile, wdt);
                     continue;
                 }
                 occ = did & !((live >> lane) & 1ull);
@@ -1373,14 +1414,14 @@ __global__ void __launch_bounds__(256) rtx_octant_expand(float4* __restrict__ no
 // work O(N) for the trees and O(S log N) for S slots; critical path O(log N) — the round-4 kernels
 // re-reduced each slot's whole range (the root's wave walked every triangle once per anchor:
 // 0.57-1.47 ms for Synthetic100k).  Launches, all on the context stream before the frames:
-//   rtx_cull_tris_box    at upload: per triangle the box of (v0, v0 + E1, v0 + E2), rounded
-//                        outward, and its tree
-//   rtx_cull_tris_marg   per (anchor, triangle): rtx_cull.h's (margin, dt) and the anchor's tree
-//   rtx_cull_nodes<BOX>  per node slot: the box (queried at upload, then kept per context) widened
-//                        by the range's largest margin and the kernel test's own padding -> the
-//                        anchors' records
-// Light anchors at upload; a view's camera anchor when a frame's view origin is not the one its
-// records were made for.  A NaN, infinite or huge (> 2^40) coordinate anywhere gives +inf (the
+//   rtx_cull_tris        per triangle: the box of (v0, v0 + E1, v0 + E2), rounded outward (after an
+//                        upload), and per (anchor, triangle) rtx_cull.h's (margin, dt); the trees
+//   rtx_cull_nodes<BOX>  per node slot: the box (queried after an upload, then kept per context)
+//                        widened by the range's largest margin and the kernel test's own padding
+//                        -> the anchors' records
+// Built before the first frame after an upload (the box, every light's anchor and the frame's
+// camera anchors: two launches), then again for a view's camera anchor when a frame's view origin
+// is not the one its records were made for.  A NaN, infinite or huge (> 2^40) coordinate anywhere gives +inf (the
 // record then always passes: the bound's finite-arithmetic domain, rtx_cull.h).
 struct CullAnchors {
     float p[kMaxViews + kMaxCullLights][4];   // xyz: the anchor point; w = 0: camera origin, > 0: light with tmax <= w
@@ -1497,43 +1538,40 @@ __device__ __forceinline__ V cull_tree_query(const V* __restrict__ t, uint32_t n
     return acc;
 }
 
-__global__ void __launch_bounds__(kCullTreeWG) rtx_cull_tris_box(const Tri* __restrict__ tris, uint32_t nt,
-                                                                 CullBox* __restrict__ tree, uint32_t* arrive,
-                                                                 uint32_t top_lds) {
-    const uint32_t i = blockIdx.x * kCullTreeWG + threadIdx.x;
-    CullBox v = cull_ident(static_cast<CullBox*>(nullptr));
-    if (i < nt) {
-        const float4 a = tris[i].a, b = tris[i].b, c = tris[i].c;
-        const float v0[3] = {a.x, a.y, a.z}, e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
-        bool ok = true;
-        for (int k = 0; k < 3; ++k) {
-            ok = ok && cull_domain(v0[k]) && cull_domain(e1[k]) && cull_domain(e2[k]);
-            const double p = v0[k], q = p + static_cast<double>(e1[k]), r = p + static_cast<double>(e2[k]);
-            const double mn = fmin(p, fmin(q, r)), mx = fmax(p, fmax(q, r));
-            // the double sums are exact unless the exponents differ by > 29: widen by 2^-40 anyway
-            v.lo[k] = f_rd(mn - fabs(mn) * 0x1p-40);
-            v.hi[k] = f_ru(mx + fabs(mx) * 0x1p-40);
-        }
-        if (!ok)   // out of the domain: every box holding it passes every ray
-            for (int k = 0; k < 3; ++k) { v.lo[k] = -INFINITY; v.hi[k] = INFINITY; }
-    }
-    cull_tree_build(v, tree, arrive, top_lds);
-}
-
-// grid (n / kCullTreeWG, A.n): tree j at trees + 2n j, counter arrive[j]
-__global__ void __launch_bounds__(kCullTreeWG) rtx_cull_tris_marg(const Tri* __restrict__ tris, uint32_t nt,
-                                                                  const CullAnchors A, CullMD* __restrict__ trees,
-                                                                  uint32_t* arrive, uint32_t top_lds) {
+// grid (n / kCullTreeWG, A.n + box): blockIdx.y = j < A.n builds anchor j's (margin, dt) tree at
+// trees + 2n j (counter arrive[j]); j = A.n (when `box`) the box tree (counter arrive[kCullMaxAnchors]).
+__global__ void __launch_bounds__(kCullTreeWG) rtx_cull_tris(const Tri* __restrict__ tris, uint32_t nt,
+                                                             const CullAnchors A, CullMD* __restrict__ trees,
+                                                             CullBox* __restrict__ btree, uint32_t* arrive,
+                                                             uint32_t top_lds) {
     const uint32_t i = blockIdx.x * kCullTreeWG + threadIdx.x, j = blockIdx.y;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a;
+    if (i < nt) { a = tris[i].a; b = tris[i].b; c = tris[i].c; }
+    const float v0[3] = {a.x, a.y, a.z}, e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
+    if (j == A.n) {   // the per-triangle box of (v0, v0 + E1, v0 + E2), rounded outward
+        CullBox v = cull_ident(static_cast<CullBox*>(nullptr));
+        if (i < nt) {
+            bool ok = true;
+            for (int k = 0; k < 3; ++k) {
+                ok = ok && cull_domain(v0[k]) && cull_domain(e1[k]) && cull_domain(e2[k]);
+                const double p = v0[k], q = p + static_cast<double>(e1[k]), r = p + static_cast<double>(e2[k]);
+                const double mn = fmin(p, fmin(q, r)), mx = fmax(p, fmax(q, r));
+                // the double sums are exact unless the exponents differ by > 29: widen by 2^-40 anyway
+                v.lo[k] = f_rd(mn - fabs(mn) * 0x1p-40);
+                v.hi[k] = f_ru(mx + fabs(mx) * 0x1p-40);
+            }
+            if (!ok)   // out of the domain: every box holding it passes every ray
+                for (int k = 0; k < 3; ++k) { v.lo[k] = -INFINITY; v.hi[k] = INFINITY; }
+        }
+        cull_tree_build(v, btree, arrive + kCullMaxAnchors, top_lds);
+        return;
+    }
     CullMD v{0.f, 0.f};
-    if (i < nt) {
-        const float4 a = tris[i].a, b = tris[i].b, c = tris[i].c;
-        const float v0[3] = {a.x, a.y, a.z}, e1[3] = {b.x, b.y, b.z}, e2[3] = {c.x, c.y, c.z};
+    if (i < nt) {   // anchor j's bound for triangle i (rtx_cull.h), NaN -> inf
         rtx_cull_tri T;
         rtx_cull_tri_setup(&T, v0, e1, e2);
         const float* p = A.p[j];
         const rtx_cull_bound bd = p[3] > 0.f ? rtx_cull_light_bounds(&T, p, p[3]) : rtx_cull_point_bounds(&T, p, A.bt[j]);
-        // NaN -> inf
         v.m = (bd.margin >= 0.0 && bd.margin < 0x1p100) ? f_ru(bd.margin) : INFINITY;
         v.dt = (bd.dt >= 0.0 && bd.dt < 0x1p100) ? f_ru(bd.dt) : INFINITY;
     }
@@ -1624,13 +1662,15 @@ __device__ __forceinline__ uint32_t cost_class(uint32_t cst) {   // heavier -> s
 }
 
 // A tile rendered split this frame has no fresh one-piece cost: it keeps the one it had
-// when it was last rendered whole (kept in `saved`).
+// when it was last rendered whole (kept in `saved`) — or, with `parts` (motion mode: the camera
+// moves, so that cost goes stale), the sum of its split waves' durations, which lets a tile that
+// stopped being heavy leave the split set.
 __global__ void __launch_bounds__(kReorderThreads) rtx_sched_count(uint32_t* __restrict__ cost, uint32_t n,
                                                                    const uint32_t* __restrict__ was_heavy,
                                                                    uint32_t* __restrict__ saved,
                                                                    uint32_t* __restrict__ hist,
                                                                    unsigned long long* __restrict__ csum,
-                                                                   uint32_t nchunks) {
+                                                                   uint32_t nchunks, uint32_t parts) {
     __shared__ uint32_t h[kCostBuckets];
     __shared__ unsigned long long tot;
     const uint32_t tid = threadIdx.x, base = blockIdx.x * kSchedChunk;
@@ -1642,7 +1682,7 @@ __global__ void __launch_bounds__(kReorderThreads) rtx_sched_count(uint32_t* __r
         const uint32_t t = base + k * kReorderThreads + tid;   // coalesced; counting ignores order
         if (t >= n) break;
         uint32_t c = cost[t];
-        if (was_heavy && was_heavy[t]) {
+        if (was_heavy && was_heavy[t] && !parts) {
             c = saved[t];
             cost[t] = c;
         } else {
@@ -1826,6 +1866,11 @@ struct rtx_ctx {
     uint32_t split_slots = 0;        // concurrent render waves on this device
     uint32_t split_permille = kSplitPermille;   // RTX_SPLIT_FACTOR (tuning)
     uint32_t sched_period = kSchedPeriod;       // RTX_SCHED_PERIOD (tuning)
+    // motion mode (kMotionFrames): frames left, and the previous frame's cameras it compares
+    uint32_t motion_left = 0;
+    bool motion_off = false;                    // RTX_MOTION=0: always the static schedule (A/B)
+    int prev_views = 0;
+    ViewCam prev_cam[kMaxViews] = {};
     uint32_t split_parts = kPartsPerMesh;            // RTX_SPLIT_PARTS (tuning)
     bool split_ok = false;           // the uploaded scene admits split rendering
     bool deep_stack = false;         // the uploaded scene needs rtx_render_kernel<..., DEEP = true>
@@ -1868,6 +1913,8 @@ struct rtx_ctx {
     double cull_bmin[3] = {}, cull_bmax[3] = {};   // the meshes' box (a camera anchor's t bound, cull_bt)
     uint64_t cull_updates = 0;            // camera-anchor record launches so far (rtx_cull_info)
     float cull_anchor[kMaxViews + kMaxCullLights][5] = {};   // per record copy: anchor xyz, w, bt (rtx_cull_dump)
+    std::vector<std::array<float, 4>> cull_lights;   // the uploaded lights' anchors {origin, T}
+    bool cull_boxes_pending = false;      // an upload's boxes and light records wait for its first frame
     rtx_render_params last{};
     int last_views = 1;
     bool last_valid = false, last_rgb = false;
@@ -1991,6 +2038,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     c->device = device_id;
     // RTX_TILE_ORDER=0 disables cost-ordered tile dispatch (identity order every frame)
     if (const char* e = std::getenv("RTX_TILE_ORDER")) c->sched_enabled = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RTX_MOTION")) c->motion_off = std::strcmp(e, "0") == 0;
     if (const char* e = std::getenv("RTX_SCHED_PERIOD"))
         c->sched_period = std::max<uint32_t>(1u, static_cast<uint32_t>(std::strtoul(e, nullptr, 10)));
     // RTX_SPLIT=0 renders heavy tiles in one piece; RTX_SPLIT=force splits every tile
@@ -2164,15 +2212,12 @@ int cull_launch(rtx_ctx* c, const CullAnchors& A, bool boxes) {
     float4* rec = const_cast<float4*>(c->dev.cull);
     const uint32_t stride4 = c->dev.cull_stride / 16u;
     const CullParams P{c->dev.nodes, c->cull_ratio, c->cull_leaves ? 1u : 0u};
-    if (A.n) {
-        hipLaunchKernelGGL(rtx_cull_tris_marg, dim3(nwg, A.n), dim3(kCullTreeWG), 0, c->stream, c->dev.tris, nt, A,
-                           c->d_cull_mtree, c->d_cull_arrive, c->cull_top_lds);
+    if (A.n || boxes) {
+        hipLaunchKernelGGL(rtx_cull_tris, dim3(nwg, A.n + (boxes ? 1u : 0u)), dim3(kCullTreeWG), 0, c->stream,
+                           c->dev.tris, nt, A, c->d_cull_mtree, c->d_cull_btree, c->d_cull_arrive, c->cull_top_lds);
         HIP_TRY(c, hipGetLastError());
     }
     if (boxes) {
-        hipLaunchKernelGGL(rtx_cull_tris_box, dim3(nwg), dim3(kCullTreeWG), 0, c->stream, c->dev.tris, nt,
-                           c->d_cull_btree, c->d_cull_arrive + kCullMaxAnchors, c->cull_top_lds);
-        HIP_TRY(c, hipGetLastError());
         hipLaunchKernelGGL(rtx_cull_nodes<true>, dim3(sb), dim3(256), 0, c->stream, c->cull_rng, c->cull_nslots, nt, n,
                            c->d_cull_btree, c->d_cull_nbox, c->d_cull_mtree, A, rec, stride4, P);
     } else if (A.n) {
@@ -2183,23 +2228,29 @@ int cull_launch(rtx_ctx* c, const CullAnchors& A, bool boxes) {
     return RTX_OK;
 }
 
-// At upload: the per-triangle boxes and every light's records (tmax bound T[l]).
-int cull_records(rtx_ctx* c, const std::vector<float>& T, const rtx_light* lights, uint32_t n_lights, bool boxes) {
-    CullAnchors A{};
-    for (uint32_t l = 0; l < n_lights; ++l) {
-        for (int k = 0; k < 3; ++k) A.p[A.n][k] = lights[l].origin[k];
-        A.p[A.n][3] = T[l] > 0.f ? T[l] : 1.f;   // T = 0: never culled (cull_ray), any bound will do
-        A.bt[A.n] = A.p[A.n][3];
-        A.idx[A.n] = static_cast<uint32_t>(kMaxViews) + l;
-        ++A.n;
-    }
-    return cull_launch(c, A, boxes);
+// At upload: the light anchors (tmax bound T[l]) the first frame's record launches build, with the
+// per-triangle boxes (cull_views).
+void cull_records(rtx_ctx* c, const std::vector<float>& T, const rtx_light* lights, uint32_t n_lights) {
+    c->cull_lights.clear();
+    for (uint32_t l = 0; l < n_lights; ++l)
+        c->cull_lights.push_back({lights[l].origin[0], lights[l].origin[1], lights[l].origin[2],
+                                  T[l] > 0.f ? T[l] : 1.f});   // T = 0: never culled (cull_ray), any bound will do
+    c->cull_boxes_pending = true;
 }
 
-// Before a frame: the records of every view whose camera origin is not the one its records of
-// the current image were made for (bitwise).
+// Before a frame: after an upload the boxes and the lights' records, and the records of every view
+// whose camera origin is not the one its records of the current image were made for (bitwise).
 int cull_views(rtx_ctx* c, const FrameArgs& F) {
     CullAnchors A{};
+    const bool boxes = c->cull_boxes_pending;
+    if (boxes) {
+        for (size_t l = 0; l < c->cull_lights.size(); ++l) {
+            for (int k = 0; k < 4; ++k) A.p[A.n][k] = c->cull_lights[l][k];
+            A.bt[A.n] = A.p[A.n][3];
+            A.idx[A.n] = static_cast<uint32_t>(kMaxViews + l);
+            ++A.n;
+        }
+    }
     for (uint32_t v = 0; v < F.n_views && v < static_cast<uint32_t>(kMaxViews); ++v) {
         const float* o = F.cam[v].origin;
         if ((c->cull_view_valid >> v) & 1u && std::memcmp(c->cull_view[v], o, 12) == 0) continue;
@@ -2211,9 +2262,10 @@ int cull_views(rtx_ctx* c, const FrameArgs& F) {
         A.idx[A.n] = v;
         ++A.n;
     }
-    if (A.n == 0) return RTX_OK;
-    ++c->cull_updates;
-    return cull_launch(c, A, false);
+    if (A.n == 0 && !boxes) return RTX_OK;
+    if (A.n > (boxes ? c->cull_lights.size() : 0u)) ++c->cull_updates;
+    c->cull_boxes_pending = false;
+    return cull_launch(c, A, boxes);
 }
 }  // namespace
 
@@ -2569,10 +2621,8 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
     }
     c->cull_view_valid = 0;
     c->dev = d;
-    if (cull_on) {   // per-triangle boxes, then the lights' records (cameras: at their first frame)
-        const int rc = cull_records(c, cull_T, s->lights, s->n_lights, true);
-        if (rc != RTX_OK) return rc;
-    }
+    c->cull_boxes_pending = false;
+    if (cull_on) cull_records(c, cull_T, s->lights, s->n_lights);   // (built before the first frame)
     // a BVH kStackDepth or more levels deep renders with the deep-stack variant, unsplit;
     // kStackDepthDeep or more with its stacks in HBM
     c->deep_stack = max_depth >= kStackDepth;
@@ -2746,6 +2796,19 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
                       "s" + std::to_string(p->stripe_rows) + "/" + std::to_string(p->stripe_first) + "/" +
                       std::to_string(p->stripe_step) + "g" + c->scene_sig + "m" +
                       std::to_string(p->lighting_mode) + std::to_string(p->shadows_enabled);
+    // Motion mode: a camera differs from the previous frame's (any field), so the tile costs go
+    // stale quickly.  For kMotionFrames frames from then on, every frame is measured whose previous
+    // measurement has completed (adopted without waiting), and split tiles are costed by their
+    // split waves (FrameArgs::part_cost).  Otherwise: one measurement every sched_period frames,
+    // adopted at the next frame (one host wait per measurement).
+    bool moved = c->prev_views != n_views;
+    for (int v = 0; !moved && v < n_views; ++v) {
+        const ViewCam &a = F.cam[v], &b = c->prev_cam[v];
+        moved = std::memcmp(a.origin, b.origin, 12) || std::memcmp(a.right, b.right, 12) ||
+                std::memcmp(a.up, b.up, 12) || std::memcmp(a.forward, b.forward, 12) || a.fov != b.fov;
+    }
+    std::memcpy(c->prev_cam, F.cam, sizeof(ViewCam) * static_cast<size_t>(n_views));
+    c->prev_views = n_views;
     if (key != c->sched_key) {   // new shape or scene: identity order, fresh costs, no split
         if (c->heavy_pending) HIP_TRY(c, hipEventSynchronize(c->ev_heavy));
         c->heavy_pending = false;
@@ -2753,13 +2816,29 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         c->sched_key = key;
         c->sched_ready = false;
         c->sched_frame = 0;
+        c->motion_left = 0;
         HIP_TRY(c, hipMemsetAsync(c->d_cost, 0, ntiles * 4, c->stream));
-    } else if (c->heavy_pending) {
-        // adopt the heavy set the last measured frame selected (one sync per measurement)
-        HIP_TRY(c, hipEventSynchronize(c->ev_heavy));
-        c->heavy_pending = false;
-        c->heavy_n = std::min<uint32_t>(*c->h_heavy_n, kMaxHeavyTiles);
-        c->heavy_cur ^= 1;
+    } else if (moved && !c->motion_off) {
+        c->motion_left = kMotionFrames;
+    }
+    const bool motion = c->motion_left > 0;
+    if (motion) --c->motion_left;
+    if (c->heavy_pending) {
+        bool ready = true;
+        if (motion) {   // no host wait: adopt only a measurement that has completed
+            const hipError_t q = hipEventQuery(c->ev_heavy);
+            (void)hipGetLastError();   // (a not-ready query is no error for the launches' checks)
+            if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(c, q);
+            ready = q == hipSuccess;
+        } else {
+            // adopt the heavy set the last measured frame selected (one sync per measurement)
+            HIP_TRY(c, hipEventSynchronize(c->ev_heavy));
+        }
+        if (ready) {
+            c->heavy_pending = false;
+            c->heavy_n = std::min<uint32_t>(*c->h_heavy_n, kMaxHeavyTiles);
+            c->heavy_cur ^= 1;
+        }
     }
     const bool split = c->split_mode != 0 && c->split_ok && c->sched_enabled && c->heavy_n > 0;
     F.heavy_flag = split ? c->d_heavy_flag[c->heavy_cur] : nullptr;
@@ -2769,10 +2848,12 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     F.occ_bits = c->d_occ;
     // Measure tile costs on the first frame of a shape and then every kSchedPeriod frames;
     // the frames in between reuse the last order and pay nothing for scheduling.
-    const bool measure = c->sched_enabled && (!c->sched_ready || c->sched_frame % c->sched_period == 0);
+    const bool measure = c->sched_enabled && !c->heavy_pending &&
+                         (!c->sched_ready || motion || c->sched_frame % c->sched_period == 0);
     ++c->sched_frame;
     F.order = (c->sched_enabled && c->sched_ready) ? c->d_order : nullptr;
     F.cost = measure ? c->d_cost : nullptr;
+    F.part_cost = (measure && motion) ? 1u : 0u;
     return RTX_OK;
 }
 
@@ -2830,7 +2911,9 @@ int ensure_hbm_stacks(rtx_ctx* c, uint32_t groups) {
     return RTX_OK;
 }
 
-int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
+// count: 1 = the reference's traversal counted (the instrumented kernel), 2 = the culled walk's
+// executed tests (its counting variant, rtx_count_work_culled; the plain one without records)
+int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
     if (grid.x == 0 || grid.y == 0) return RTX_OK;
     if (c->hbm_stack) {
         const int rc = ensure_hbm_stacks(c, grid.x);
@@ -2841,7 +2924,12 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         G.order = nullptr;
         G.cost = nullptr;
         G.heavy_flag = nullptr;
-        if (c->hbm_stack)
+        if (count == 2 && c->dev.cull_stride && !c->hbm_stack && !c->deep_stack) {
+            const int rc = cull_views(c, F);   // the views' camera records, as a frame would
+            if (rc != RTX_OK) return rc;
+            hipLaunchKernelGGL((rtx_render_kernel<true, 0, false, 0, false, true>), grid, dim3(kBlockThreads), 0,
+                               c->stream, c->dev, G);
+        } else if (c->hbm_stack)
             hipLaunchKernelGGL((rtx_render_kernel<true, 0, true, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, G);
         else if (c->deep_stack)
             hipLaunchKernelGGL((rtx_render_kernel<true, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, G);
@@ -2891,7 +2979,7 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, bool count) {
         const int stage = c->heavy_cur ^ 1;
         const uint32_t nch = (F.n_tiles + kSchedChunk - 1) / kSchedChunk;
         hipLaunchKernelGGL(rtx_sched_count, dim3(nch), dim3(kReorderThreads), 0, c->stream, F.cost, F.n_tiles,
-                           F.heavy_flag, c->d_saved_cost, c->d_hist, c->d_csum, nch);
+                           F.heavy_flag, c->d_saved_cost, c->d_hist, c->d_csum, nch, F.part_cost);
         HIP_TRY(c, hipGetLastError());
         hipLaunchKernelGGL(rtx_sched_scan, dim3(1), dim3(kScanThreads), 0, c->stream, c->d_hist, nch,
                            c->d_csum,
@@ -2924,7 +3012,7 @@ extern "C" int rtx_render_views_async(rtx_ctx* c, const rtx_camera* cams, int n_
     dim3 grid;
     int rc = prepare(c, cams, n_views, p, want_rgb != 0, F, grid);
     if (rc != RTX_OK) return rc;
-    rc = launch(c, F, grid, false);
+    rc = launch(c, F, grid, 0);
     if (rc != RTX_OK) return rc;
     remember(c, p, n_views, want_rgb != 0);
     return RTX_OK;
@@ -3066,16 +3154,31 @@ extern "C" int rtx_time_frames(rtx_ctx* c, const rtx_camera* cam, const rtx_rend
 }
 
 // Instrumented variant: the same traversal with per-lane work counters.
-extern "C" int rtx_count_work_ex(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* counts,
-                                 int n_counts);
-
-extern "C" int rtx_count_work(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* counts) {
-    return rtx_count_work_ex(c, cam, p, counts, kModelCounters);
+namespace {
+int count_work(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* counts, int n_counts,
+               int mode);
 }
 
-// Same with the per-wave diagnostic counters appended (up to kNumCounters values).
 extern "C" int rtx_count_work_ex(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* counts,
                                  int n_counts) {
+    return count_work(c, cam, p, counts, n_counts, 1);
+}
+
+extern "C" int rtx_count_work(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* counts) {
+    return count_work(c, cam, p, counts, kModelCounters, 1);
+}
+
+extern "C" int rtx_count_work_culled(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* counts,
+                                     int n_counts) {
+    return count_work(c, cam, p, counts, n_counts, 2);
+}
+
+namespace {
+// The counters of one render (mode 1: the reference's traversal; 2: the culled walk's executed
+// tests), up to kNumCounters values: the kModelCounters of the FLOP model, then the per-wave
+// diagnostics and the cull tests.
+int count_work(rtx_ctx* c, const rtx_camera* cam, const rtx_render_params* p, uint64_t* counts, int n_counts,
+               int mode) {
     if (!counts || n_counts <= 0) return RTX_E_INVALID;
     if (n_counts > kNumCounters) n_counts = kNumCounters;
     FrameArgs F;
@@ -3083,7 +3186,7 @@ extern "C" int rtx_count_work_ex(rtx_ctx* c, const rtx_camera* cam, const rtx_re
     int rc = prepare(c, cam, 1, p, false, F, grid);
     if (rc != RTX_OK) return rc;
     HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long) * kNumCounters, c->stream));
-    rc = launch(c, F, grid, true);
+    rc = launch(c, F, grid, mode);
     if (rc != RTX_OK) return rc;
     unsigned long long tmp[kNumCounters];
     HIP_TRY(c, hipMemcpyAsync(tmp, c->d_counters, sizeof(unsigned long long) * kNumCounters, hipMemcpyDeviceToHost,
@@ -3093,6 +3196,7 @@ extern "C" int rtx_count_work_ex(rtx_ctx* c, const rtx_camera* cam, const rtx_re
     remember(c, p, 1, false);
     return RTX_OK;
 }
+}  // namespace
 
 extern "C" int rtx_schedule_state(rtx_ctx* c, uint32_t* order, uint32_t* cost, uint32_t n, uint32_t* n_tiles) {
     if (!c) return RTX_E_INVALID;
@@ -3213,6 +3317,7 @@ struct rtx_anim {
     uint32_t cut = kAnimCut;              // RTX_ANIM_CUT: nodes above this many triangles split as queue tasks
     uint32_t epoch = 0;                   // updates so far (the build's publication flag)
     uint64_t wait_ticks = rtxa::kWaitTicks;   // rtxa::Launch::wait_ticks (RTX_ANIM_WAIT_TICKS: tests of the timeout path)
+    uint32_t debug = 0;                       // rtxa::Launch::debug (RTX_ANIM_DEBUG: tests of the timeout path)
     std::vector<double> obj_radius;       // per registered mesh: max |object-space position|
 };
 
@@ -3313,6 +3418,7 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
         const long long v = std::strtoll(e, nullptr, 10);
         if (v >= 0) a->wait_ticks = static_cast<uint64_t>(v);
     }
+    if (const char* e = std::getenv("RTX_ANIM_DEBUG")) a->debug = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RTX_ANIM_DEPTH_LIMIT")) {
         const int v = std::atoi(e);
         if (v >= 1 && v < kStackDepth) a->depth_limit = static_cast<uint32_t>(v);
@@ -3466,6 +3572,7 @@ extern "C" int rtx_anim_update(rtx_anim* a, rtx_ctx* c, const float* transforms)
     L.frontier_max = a->serial_frontier ? 0u : rtxa::kFrontierHistMax;
     L.cut = a->cut;
     L.wait_ticks = a->wait_ticks;
+    L.debug = a->debug;
     L.epoch = ++a->epoch;
     ANIM_TRY(a, rtxa::launch_build(L, s));
     ANIM_TRY(a, hipEventRecord(a->ev, s));

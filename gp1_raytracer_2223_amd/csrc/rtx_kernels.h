@@ -23,6 +23,9 @@ constexpr int kSchedChunk = 1024;      // tiles per scheduling workgroup (4 per 
 constexpr int kScanThreads = 1024;     // rtx_sched_scan (one workgroup)
 constexpr int kCostBuckets = 32;
 constexpr int kSchedPeriod = 64;      // frames between tile-cost measurements
+// A frame whose camera differs from the previous frame's starts (or extends) motion mode for this
+// many frames: every frame is measured whose previous measurement has completed (no host wait).
+constexpr int kMotionFrames = 64;
 
 // Split rendering of heavy tiles: a wave tile whose measured cost exceeds
 // kSplitPermille/1000 x (frame cost / concurrent wave slots) is rendered by three extra
@@ -77,7 +80,9 @@ enum Counter {
     kShadeBase, kShadeLambert, kShadePhong, kShadeCT,
     // diagnostics (not part of the FLOP model): per-WAVE packet work, counted once per
     // wave by lane 0 — node-pair tests and triangle tests the wave executed
-    kWaveNodeTests, kWaveTriTests, kNumCounters
+    kWaveNodeTests, kWaveTriTests,
+    // the culled walk's counting variant (rtx_count_work_culled): per-lane exact-cull box tests
+    kCullTests, kNumCounters
 };
 constexpr int kModelCounters = 12;
 
@@ -142,7 +147,7 @@ constexpr int kMaxCullLights = 32;   // lights with a cull anchor (more: the sce
 // kCullTreeWG leaves per workgroup; the last workgroup of a tree builds the levels above the
 // workgroups' roots in LDS when there are at most kCullTopLds of them (else in global memory).
 constexpr uint32_t kCullTreeWG = 256;
-constexpr uint32_t kCullMaxAnchors = kMaxViews > kMaxCullLights ? kMaxViews : kMaxCullLights;   // per record launch
+constexpr uint32_t kCullMaxAnchors = kMaxViews + kMaxCullLights;   // per record launch (after an upload: lights + views)
 constexpr uint32_t kCullTopLds = 1024;
 
 struct ViewCam {
@@ -172,6 +177,9 @@ struct FrameArgs {
     uint32_t n_tiles;             // wave tiles in the launch (all views)
     const uint32_t* __restrict__ order;   // dispatch permutation of the tiles (null = identity)
     uint32_t* __restrict__ cost;          // per-tile cost of this frame (null = not measured)
+    // camera in motion (a measured frame of rtx_ctx::motion_left): the split launches add their
+    // waves' durations to their tile's cost, which then replaces the tile's saved one-piece cost
+    uint32_t part_cost;
     uint32_t* __restrict__ out_px;   // view v at out_px + v * width * height
     float* __restrict__ out_rgb;     // may be null
     unsigned long long* __restrict__ counters;  // COUNT variant only

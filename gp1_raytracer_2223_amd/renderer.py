@@ -105,6 +105,14 @@ class DeviceContext:
         abi.check(self.lib.rtx_count_work(self.h, C.byref(cam), C.byref(params), out), "rtx_count_work", self.h)
         return np.array(list(out), dtype=np.uint64)
 
+    def count_work_culled(self, cam, params) -> np.ndarray:
+        """The 15 counters of the walk the product executes (rtx_count_work_culled): the 12 model
+        counters, per-wave node-pair and triangle steps, exact-cull box tests."""
+        out = (C.c_uint64 * 15)()
+        abi.check(self.lib.rtx_count_work_culled(self.h, C.byref(cam), C.byref(params), out, 15),
+                  "rtx_count_work_culled", self.h)
+        return np.array(list(out), dtype=np.uint64)
+
 
 class DeviceGroup:
     """Owns one rtx_group: one frame tiled over several contexts (GPUs) by this process,
@@ -202,6 +210,13 @@ class DeviceAnimation:
         st = (C.c_uint32 * 4)()
         self._check(self.lib.rtx_anim_status(self.h, i, st), "rtx_anim_status")
         return np.array(list(st), np.uint32)
+
+    def stamps(self, i: int = 0) -> np.ndarray:
+        """The last update's 128 status words of registered mesh i (rtx_anim.h: errors, counts,
+        phase stamps, completeness word 28); no error check."""
+        out = (C.c_uint32 * 128)()
+        self._check(self.lib.rtx_anim_stamps(self.h, i, out), "rtx_anim_stamps")
+        return np.array(list(out), np.uint32)
 
     def download(self, i: int = 0) -> dict:
         """Registered mesh i in the reference's form (TriangleMesh after UpdateTransforms)."""

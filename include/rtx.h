@@ -235,6 +235,13 @@ int rtx_count_work(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params*
  * [13] triangle tests executed per WAVE (packet work, one count per wave per step). */
 int rtx_count_work_ex(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
                       uint64_t* counts, int n_counts);
+/* The same counters for the walk the product executes when the scene has exact-cull records
+ * (otherwise identical to rtx_count_work_ex): slab [3] and triangle [4] tests the
+ * culled, ordered walk performs per lane (a lane in a node's mask is tested against both
+ * children), [12]/[13] per-wave steps, and [14] the exact-cull box tests.  One-piece frame (the
+ * split launches' extra path tests not included).  Not timed. */
+int rtx_count_work_culled(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
+                          uint64_t* counts, int n_counts);
 /* Split rendering of heavy tiles (no reference counterpart: a scheduling detail of this
  * path).  Tiles whose measured cost exceeds their share of the frame are re-rendered with
  * their BVH traversals cut into `parts` subtree pieces run by separate workgroups; the

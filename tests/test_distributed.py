@@ -192,3 +192,7 @@ def test_bench_one_gpu_contract(tmp_path):
             assert abs(x["efficiency"] - sp["t_full_ms"] / (s * max(x["share_ms"]))) < 1e-3
     assert "flop_basis" in scenes["Synthetic100k"]["roofline_rank0"]
     assert "flop_basis" not in scenes["Bunny8Lights"]["roofline_rank0"]
+    for name in ("Synthetic100k", "W4_Optional"):   # the culled scenes: executed-work roofline too
+        rr = scenes[name]["roofline_rank0"]
+        assert 0 < rr["frac_executed"] < rr["frac"], (name, rr)
+        assert abs(rr["frac_executed"] - rr["achieved_executed"] / rr["peak"]) < 1e-3

@@ -250,38 +250,70 @@ def test_device_update_too_deep_tree_is_disabled_not_rendered(monkeypatch):
     b.close()
 
 
-def test_device_update_timeout_disables_the_mesh(monkeypatch):
-    """A worker that gives up waiting for a queue entry (Launch::wait_ticks) leaves the entry it
-    claimed unbuilt: the tree is incomplete.  The output launch must then write none of it and
-    disable the mesh (node count 0, no frontier parts), and the update report kErrTimeout.  Forced
-    with a zero wait (RTX_ANIM_WAIT_TICKS=0, read at rtx_anim_create): W4_Optional's 65 workers
-    mostly claim entries not published yet and give up at once.  Either outcome is checked: if no
-    worker timed out, the build is complete and the frames equal the host Update's.  The error is
-    sticky: an incomplete build breaks the chain of permutations every later Update starts from,
-    so once it happened every later Update reports it and keeps the mesh disabled."""
-    monkeypatch.setenv("RTX_ANIM_WAIT_TICKS", "0")
+def _timeout_run(monkeypatch, env, times):
+    """Updates of W4_Optional under `env`; per update (error text or None, status word 28), with
+    every frame checked against a host upload of the same Update — the mesh's BVH absent when the
+    update reported an error (the disabled mesh)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     dev_scene, host_scene = _scene("W4_Optional"), _scene("W4_Optional")
     a, b = DeviceContext(0), DeviceContext(0)
     anim = DeviceAnimation(dev_scene, a)
-    timed_out = 0
-    for t in TIMES[:3]:
-        anim.update(t, a)
-        host_scene.update(t)
-        s, cam = host_scene.view()
-        try:
-            anim.status(0)
-            assert timed_out == 0, "the error must be sticky"
-        except RuntimeError as e:
-            assert "timed out" in str(e), e
-            timed_out += 1
-            s.meshes[0].n_nodes = 0   # the disabled mesh: triangles present, no tree to walk
-        b.upload(s)
-        p = abi.make_params(320, 180)
-        for _ in range(3):
-            apx, _ = a.render(cam, p)
-            bpx, _ = b.render(cam, p)
-            assert np.array_equal(apx, bpx), (t, timed_out)
-    assert timed_out > 0, "a zero wait should make some worker give up"
-    anim.close()
-    a.close()
-    b.close()
+    out = []
+    try:
+        for t in times:
+            anim.update(t, a)
+            host_scene.update(t)
+            s, cam = host_scene.view()
+            try:
+                anim.status(0)
+                err = None
+            except RuntimeError as e:
+                err = str(e)
+                s.meshes[0].n_nodes = 0   # the disabled mesh: triangles present, no tree to walk
+            out.append((err, int(anim.stamps(0)[28])))
+            b.upload(s)
+            p = abi.make_params(320, 180)
+            for _ in range(3):
+                apx, _ = a.render(cam, p)
+                bpx, _ = b.render(cam, p)
+                assert np.array_equal(apx, bpx), (t, err)
+    finally:
+        anim.close()
+        a.close()
+        b.close()
+    return out
+
+
+def test_device_update_lost_task_disables_the_mesh(monkeypatch):
+    """A worker that gives up on a real task (claimed, then never run) leaves the tree incomplete.
+    Made deterministic with RTX_ANIM_DEBUG=1 (the worker that takes queue entry 0 drops it) and a
+    1 ms wait: every update must report the timeout, write none of the tree and disable the mesh
+    (node count 0, no frontier parts), and stay disabled — the error is sticky, because an
+    incomplete build breaks the chain of permutations every later Update starts from."""
+    out = _timeout_run(monkeypatch, {"RTX_ANIM_DEBUG": "1", "RTX_ANIM_WAIT_TICKS": "100000"}, TIMES[:3])
+    assert all(err is not None and "timed out" in err for err, _ in out), out
+    assert not (out[0][1] & 1), "the tree must not be marked complete"
+
+
+def test_device_update_spurious_timeout_keeps_the_mesh(monkeypatch):
+    """A worker whose wait ran out on an index no task takes lost nothing: the tree is complete.
+    Forced with RTX_ANIM_DEBUG=2 (workers leaving because every triangle is placed report a
+    timeout too): no update may report an error or disable the mesh; status word 28 records the
+    complete tree (bit 0) and the spurious timeout (bit 1); the frames equal the host Update's."""
+    out = _timeout_run(monkeypatch, {"RTX_ANIM_DEBUG": "2"}, TIMES[:3])
+    assert all(err is None and w == 3 for err, w in out), out
+
+
+def test_device_update_zero_wait(monkeypatch):
+    """A zero wait (RTX_ANIM_WAIT_TICKS=0): most of W4_Optional's 65 workers give up at once, some
+    on real tasks (then the tree is incomplete: reported, disabled, sticky), some on indices no task
+    takes (harmless).  Whichever happens, the frames equal the host Update's with or without the
+    mesh's BVH, matching what the update reported, and a reported error is sticky."""
+    out = _timeout_run(monkeypatch, {"RTX_ANIM_WAIT_TICKS": "0"}, TIMES[:3])
+    first = next((k for k, (err, _) in enumerate(out) if err is not None), None)
+    if first is not None:
+        assert all(err is not None for err, _ in out[first:]), out
+        assert all(w & 1 for err, w in out[:first]), out
+    else:
+        assert all(w & 1 for _, w in out), out

@@ -266,7 +266,7 @@ def _dump(ctx, anchor):
 @pytest.mark.parametrize("name", ["Synthetic100k", "W4_Optional"])
 @pytest.mark.parametrize("top", ["lds", "global"])
 def test_cull_records_equal_brute_force(name, top):
-    """Every record of the segment-tree build (rtx_cull_tris_*, rtx_cull_nodes) equals, value for
+    """Every record of the segment-tree build (rtx_cull_tris, rtx_cull_nodes) equals, value for
     value, the direct fold of every triangle of the slot's range (tools/cull_records_ref.c, the
     same double-precision bound, rtx_cull.h): camera anchors of two views, at upload and after a
     camera move, and every light anchor.  "global": the trees' top levels built in global memory
@@ -513,3 +513,36 @@ def test_cull_ordered_walk_tie_break_is_observable(cull_ctx, plain_ctx, tmp_path
     ra = oracle_bind.render(sA, cam, p)[0]
     rb = oracle_bind.render(sB, cam, p)[0]
     assert (ra != rb).sum() > 1000, "the swapped tie-break must be visible"
+
+
+# ---------------------------------------------------------------- executed work (rtx_count_work_culled)
+def _counts(ctx, s, cam, p, culled):
+    ctx.upload(s)
+    fn = ctx.lib.rtx_count_work_culled if culled else ctx.lib.rtx_count_work_ex
+    out = (C.c_uint64 * 15)()
+    abi.check(fn(ctx.h, C.byref(cam), C.byref(p), out, 15), "count", ctx.h)
+    return np.array(list(out), np.uint64)
+
+
+@pytest.mark.parametrize("name", ["Synthetic100k", "W4_Optional", "W4_Bunny"])
+def test_executed_work_counts(product_ctx, name):
+    """The culled walk's counting variant (bench.py's roofline.frac_executed): every counter
+    outside the BVH walk equals the reference traversal's count (same rays, hits, shadows,
+    shading), the culled walk tests at most the reference's triangles, and for Synthetic100k it
+    executes a small fraction of the reference's slab and triangle tests (the CPU cost model,
+    tools/cull_probe.c: 0.066 and 0.015).  A scene without records counts exactly as
+    rtx_count_work_ex."""
+    hs = HostScene(name)
+    s, cam = hs.view()
+    p = abi.make_params(320, 180)
+    ref = _counts(product_ctx, s, cam, p, False)
+    got = _counts(product_ctx, s, cam, p, True)
+    walk = [3, 4, 12, 13, 14]   # slab, tri, per-wave steps, cull tests
+    same = [k for k in range(12) if k not in walk]
+    assert np.array_equal(got[same], ref[same]), (got, ref)
+    if not product_ctx.cull_info()[0]:
+        assert np.array_equal(got, ref)
+        return
+    assert got[14] > 0 and got[4] <= ref[4], (got, ref)
+    if name == "Synthetic100k":
+        assert got[3] < 0.25 * ref[3] and got[4] < 0.1 * ref[4], (got[3] / ref[3], got[4] / ref[4])

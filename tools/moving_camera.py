@@ -1,11 +1,13 @@
 """Moving-camera frame loop: the camera origin changes every frame, so the
-exact cull's camera-anchor records are rebuilt before every frame.  Per setting
-(product default, RTX_NO_CULL=1, and any extra NAME=VAR:value,... arguments) one context renders
-K frames of a scene along a fixed camera path (render_async back to back on the context stream,
-HIP-serialized like the reference's loop), wall-clock timed; the last frame of every setting is
-checked bit for bit against the unculled one.  Prints one JSON line per (scene, setting).
+exact cull's camera-anchor records are rebuilt before every frame and the tile
+schedule runs in motion mode (rtx_hip.hip, kMotionFrames).  Per setting (product default,
+RTX_NO_CULL=1, and any extra NAME=VAR:value,... arguments) K frames of a scene along a fixed camera
+path, wall-clock timed, with F frames in flight (MC_INFLIGHT, default 2: frame k on context k mod F,
+which first waits for its previous frame — the bench's and the CLI's frame loop; 1 = the
+reference's serial loop, each frame complete before the next is queued).  The last frame of every
+setting is checked bit for bit against the unculled one.  One JSON line per (scene, setting).
 
-Usage (GPU box): python tools/moving_camera.py [K] [scene,...] [setting ...]
+Usage (GPU box): [MC_INFLIGHT=F] python tools/moving_camera.py [K] [scene,...] [setting ...]
 """
 import ctypes as C
 import json
@@ -26,7 +28,7 @@ from gp1_raytracer_2223_amd.scene import HostScene  # noqa: E402
 
 SIZES = {"Synthetic100k": (1920, 1080), "W4_Optional": (1920, 1080), "W4_Bunny": (1920, 1080)}
 KNOBS = ("RTX_NO_CULL", "RTX_CULL_ANIMATED", "RTX_CULL_MIN_SA", "RTX_CULL_RATIO", "RTX_CULL_TOP_LDS", "RTX_SCHED_PERIOD",
-         "RTX_SPLIT", "RTX_SPLIT_FACTOR")
+         "RTX_SPLIT", "RTX_SPLIT_FACTOR", "RTX_MOTION")
 
 
 def ctx_with(env: dict) -> DeviceContext:
@@ -59,23 +61,32 @@ def run(name: str, K: int, settings) -> None:
     p = abi.make_params(W, H)
     cams = [path(cam0, k) for k in range(K)]
     base = None
+    nf = int(os.environ.get("MC_INFLIGHT", "2"))
     for tag, env in settings:
-        ctx = ctx_with(env)
-        ctx.upload(s)
-        for k in range(8):   # warm-up: cost-ordered and split state live
-            ctx.render_async(cams[k], p)
-        ctx.synchronize()
-        n0 = ctx.cull_info()[1]
+        ctxs = [ctx_with(env) for _ in range(nf)]
+        for ctx in ctxs:
+            ctx.upload(s)
+        for k in range(8 * nf):   # warm-up: cost-ordered and split state live
+            ctxs[k % nf].render_async(cams[k // nf], p)
+        for ctx in ctxs:
+            ctx.synchronize()
+        n0 = sum(ctx.cull_info()[1] for ctx in ctxs)
         t0 = time.perf_counter()
+        still = tag.startswith("static")   # the same loop with the camera standing still
         for k in range(K):
-            ctx.render_async(cams[k], p)
-        ctx.synchronize()
+            ctx = ctxs[k % nf]
+            ctx.synchronize()   # its previous frame (k - nf) is complete
+            ctx.render_async(cams[0] if still else cams[k], p)
+        for ctx in ctxs:
+            ctx.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / K
-        rebuilds = ctx.cull_info()[1] - n0
-        px, rgb = ctx.render(cams[K - 1], p)
-        ctx.close()
-        row = {"scene": f"{name} {W}x{H}", "setting": tag, "frames": K, "ms_per_frame": round(ms, 4),
-               "camera_record_rebuilds": rebuilds, "cull": ctx_cull_flag(env)}
+        rebuilds = sum(ctx.cull_info()[1] for ctx in ctxs) - n0
+        heavy = ctxs[(K - 1) % nf].split_info()[0]
+        px, rgb = ctxs[0].render(cams[K - 1], p)   # (the check frame: the path's last camera for every setting)
+        for ctx in ctxs:
+            ctx.close()
+        row = {"scene": f"{name} {W}x{H}", "setting": tag, "frames": K, "inflight": nf, "ms_per_frame": round(ms, 4),
+               "camera_record_rebuilds": rebuilds, "heavy_tiles_last": heavy, "cull": ctx_cull_flag(env)}
         if base is None:
             base = (px, rgb, ms)
         else:
@@ -96,7 +107,7 @@ def main() -> None:
     for a in sys.argv[3:]:
         tag, _, rest = a.partition("=")
         extra.append((tag, dict(kv.split(":", 1) for kv in rest.split(",") if kv)))
-    settings = [("no_cull", {"RTX_NO_CULL": "1"}), ("cull", {})] + extra
+    settings = [("no_cull", {"RTX_NO_CULL": "1"}), ("cull", {}), ("static_cull", {})] + extra
     for name in scenes:
         run(name, K, settings)
 

@@ -67,6 +67,34 @@ def main():
         all_w = [sum(v for _, v in g) for g in wr]
         mean = lambda xs: sum(xs) / len(xs)  # noqa: E731
         kb = 1024.0
+        # per phase (main kernel, split phases 1-3): HBM bytes per frame and their ratio to the
+        # phase's algorithmic bytes = what it must write (uint32 frame 4 B/px for the main kernel
+        # and PHASE 3, the 8-B hit key per heavy pixel for PHASE 1, the 4-B occlusion word for
+        # PHASE 2) plus one read of the scene image
+        phases = {}
+        state = {}
+        log = Path(base + "_FETCH_SIZE.log")
+        if log.exists():
+            for line in log.read_text().splitlines():
+                if line.startswith("STATE "):
+                    state = {k: int(v) for k, v in (kv.split("=") for kv in line.split()[1:])}
+        rows = H if step == 1 else 16 * ((H // 16 + step - 1) // step)
+        px = W * rows
+        hp = 64 * state.get("heavy_tiles", 0)
+        out_bytes = {0: 4 * max(0, px - hp), 1: 8 * hp, 2: 4 * hp, 3: 4 * hp}
+        for ph in range(4):
+            tag = f"void rtx_render_kernel<false, {ph}"
+            pf = [sum(v for n, v in g if n.startswith(tag)) for g in fr]
+            pw = [sum(v for n, v in g if n.startswith(tag)) for g in wr]
+            nl = mean([sum(1 for n, _ in g if n.startswith(tag)) for g in fr])
+            if nl == 0:
+                continue
+            b = int(round((2 * mean(pf) + mean(pw)) * kb))
+            alg = out_bytes[ph] + state.get("scene_bytes", 0)
+            phases[["main", "p1", "p2", "p3"][ph]] = {
+                "hbm_bytes_per_frame": b, "launches_per_frame": round(nl, 2),
+                "algorithmic_bytes": alg if state else None,
+                "ratio_to_algorithmic": round(b / alg, 2) if state and alg else None}
         recs.append({
             "config": {"scene": scene, "width": W, "height": H, "views": 1, "stripe_step": step},
             "stripes": "rank 0's 16-row stripes" if step > 1 else "whole frame",
@@ -75,6 +103,7 @@ def main():
             "hbm_bytes_per_launch": int(round((2 * mean(main_f) + mean(main_w)) * kb)),
             "hbm_bytes_per_frame": int(round((2 * mean(all_f) + mean(all_w)) * kb)),
             "split_launches_per_frame": round(mean([len(g) - 1 for g in fr]), 2),
+            "phases": phases, "state": state,
             "lib_sha256": lib_hash,
         })
     print(json.dumps({"command": "bash tools/pmc_configs.sh (rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE, one pass each, "

@@ -29,8 +29,13 @@ def main() -> int:
     for _ in range(frames):
         abi.check(ctx.lib.rtx_render_views_async(ctx.h, C.byref(cam), 1, C.byref(p), 0), "render", ctx.h)
         ctx.synchronize()
+    heavy, parts = ctx.split_info()
+    nb = C.c_uint64()
+    abi.check(ctx.lib.rtx_scene_bytes(ctx.h, C.byref(nb)), "scene bytes", ctx.h)
     ctx.close()
     print(f"rendered {frames} frames of {scene} {W}x{H} stripe_step {step}")
+    # (read by tools/pmc_configs.py: the per-phase algorithmic bytes)
+    print(f"STATE heavy_tiles={heavy} parts={parts} scene_bytes={nb.value} lights={s.n_lights}")
     return 0
 
 

@@ -15,7 +15,7 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output
 timeout -k 10 200 python3 tools/moving_camera.py 400 > $OUT/moving_camera.txt 2>&1 || { echo "moving camera failed"; tail -20 $OUT/moving_camera.txt; exit 1; }
 cat $OUT/moving_camera.txt
 EXE=gp1_raytracer_2223_amd/lib/rtx_render
-for f in 1 3; do
+for f in 1 3 1 3; do
   for c in cull no_cull; do
     echo "== W4_Optional 1920x1080 inflight $f $c" >> $OUT/anim.txt
     if [ $c = no_cull ]; then export RTX_NO_CULL=1; else unset RTX_NO_CULL; fi
