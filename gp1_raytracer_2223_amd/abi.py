@@ -148,6 +148,7 @@ HIP_SYMBOLS = ["rtx_abi_version", "rtx_create", "rtx_destroy", "rtx_last_error",
                "rtx_render", "rtx_render_async", "rtx_synchronize", "rtx_download", "rtx_device_buffers",
                "rtx_time_frames", "rtx_scene_bytes", "rtx_count_work",
                "rtx_render_views_async", "rtx_time_views", "rtx_count_work_ex", "rtx_count_work_culled", "rtx_split_info",
+               "rtx_split_tune_info",
                "rtx_gather_async", "rtx_host_register", "rtx_host_unregister",
                "rtx_group_create", "rtx_group_destroy", "rtx_group_last_error", "rtx_group_size",
                "rtx_group_context", "rtx_group_upload_scene", "rtx_group_render", "rtx_schedule_state",
@@ -212,6 +213,10 @@ def load_hip() -> C.CDLL:
             lib.rtx_cull_dump.argtypes = [VP, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), VP, VP, VP,
                                           VP, VP]
             lib.rtx_cull_dump.restype = C.c_int
+        if hasattr(lib, "rtx_split_tune_info"):   # absent only in older experiment builds (RTX_HIP_LIB)
+            lib.rtx_split_tune_info.argtypes = [VP, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                                C.POINTER(C.c_uint32)]
+            lib.rtx_split_tune_info.restype = C.c_int
         if hasattr(lib, "rtx_split_info"):   # absent only in older experiment builds (RTX_HIP_LIB)
             lib.rtx_split_info.argtypes = [VP, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
             lib.rtx_split_info.restype = C.c_int

@@ -710,16 +710,17 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
 // SLAB = kSlabOct: `oct` is the batch's octant (batch_octant) and the part walks that copy.
 // CB: kSpecCullBack (tri_t_wave).
 // CULL: as mesh_traverse, on the part's path and below it.
-// walk_dt (motion mode, FrameArgs::part_cost): gets the duration of the walk below E (0 when no
-// lane reaches E), the part's share of the tile's one-piece cost.
+// Returns, when `timed` (motion mode, FrameArgs::part_cost), the duration of the walk below E in
+// cycles (0 when no lane reaches E): the part's share of the tile's one-piece cost; else 0.
 template <bool ANY, int SLAB, bool CB = false, bool CULL = false>
-__device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int oct, unsigned long long mask,
-                              uint32_t lane, uint4* stk, float& sc_t, uint32_t& sc_tri, unsigned long long& live,
-                              Counts& cnt, const uint32_t* occ_word = nullptr, uint32_t occ_bit = 0,
-                              const CullRay& cq = CullRay{}, unsigned long long* walk_dt = nullptr) {
+__device__ unsigned long long part_traverse(const DevScene& S, const int4 E, const Ray& r, int oct,
+                                            unsigned long long mask, uint32_t lane, uint4* stk, float& sc_t,
+                                            uint32_t& sc_tri, unsigned long long& live, Counts& cnt,
+                                            const uint32_t* occ_word = nullptr, uint32_t occ_bit = 0,
+                                            const CullRay& cq = CullRay{}, bool timed = false) {
     static_assert(!CULL || SLAB != kSlabExact, "the cull runs in FAST batches only");
     constexpr bool FAST = SLAB != kSlabExact;
-    if (E.x < 0) return;   // unused entry of a device-animated mesh's reserved frontier
+    if (E.x < 0) return 0;   // unused entry of a device-animated mesh's reserved frontier
     const int4 M = ldcb16i(S.meshes, static_cast<uint32_t>(E.x) * 16u);
     const float4* nb = SLAB == kSlabOct ? reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.nodes) +
                                                                           static_cast<uint32_t>(oct) * S.oct_bytes)
@@ -750,15 +751,16 @@ __device__ void part_traverse(const DevScene& S, const int4 E, const Ray& r, int
         link = __float_as_uint(c1.z);
         ntri = __float_as_uint(c1.w);
     }
-    if (m == 0) return;
-    const unsigned long long t0 = walk_dt ? __builtin_amdgcn_s_memtime() : 0ull;
+    if (m == 0) return 0;
+    // (read unconditionally: a `timed` test here made the compiler version the walk loop)
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     if (!RTX_STAMPS_WALK)
         bvh_walk_lean<ANY, SLAB, CB, CULL>(S, nb, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, sc_t,
                                            sc_tri, live, occ_word, occ_bit, cq);
     else
         bvh_walk<ANY, FAST, false>(S, cull_sign(M.z, ANY), r, link, ntri, m, mask, lane, stk, nullptr, sc_t, sc_tri,
                                    live, cnt, occ_word, occ_bit);
-    if (walk_dt) *walk_dt = __builtin_amdgcn_s_memtime() - t0;
+    return timed ? __builtin_amdgcn_s_memtime() - t0 : 0ull;   // (timed: the caller's use only)
 }
 
 struct RGB {
@@ -1070,26 +1072,26 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         uint32_t sc_tri = 0;
         unsigned long long unused = 0;
         const int oct = (fast && S.oct_bytes) ? batch_octant(vr, active) : -1;
-        unsigned long long wdt = 0;
-        unsigned long long* const wp = (F.part_cost && F.cost) ? &wdt : nullptr;
+        const bool timed = F.part_cost && F.cost;
+        unsigned long long wdt;
         if (oct >= 0 && pcull)
-            part_traverse<false, kSlabOct, kCullBack, kCull>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri, unused,
-                                                             cnt, nullptr, 0u, pq, wp);
+            wdt = part_traverse<false, kSlabOct, kCullBack, kCull>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri,
+                                                                   unused, cnt, nullptr, 0u, pq, timed);
         else if (oct >= 0)
-            part_traverse<false, kSlabOct, kCullBack>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri, unused, cnt,
-                                                      nullptr, 0u, CullRay{}, wp);
+            wdt = part_traverse<false, kSlabOct, kCullBack>(S, E, vr, oct, active, lane, stk, sc_t, sc_tri, unused,
+                                                            cnt, nullptr, 0u, CullRay{}, timed);
         else if (fast && pcull)
-            part_traverse<false, kSlabFast, kCullBack, kCull>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused,
-                                                              cnt, nullptr, 0u, pq, wp);
+            wdt = part_traverse<false, kSlabFast, kCullBack, kCull>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri,
+                                                                    unused, cnt, nullptr, 0u, pq, timed);
         else if (fast)
-            part_traverse<false, kSlabFast, kCullBack>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused, cnt,
-                                                       nullptr, 0u, CullRay{}, wp);
+            wdt = part_traverse<false, kSlabFast, kCullBack>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused,
+                                                             cnt, nullptr, 0u, CullRay{}, timed);
         else
-            part_traverse<false, kSlabExact, kCullBack>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused, cnt,
-                                                        nullptr, 0u, CullRay{}, wp);
+            wdt = part_traverse<false, kSlabExact, kCullBack>(S, E, vr, 0, active, lane, stk, sc_t, sc_tri, unused,
+                                                              cnt, nullptr, 0u, CullRay{}, timed);
         if (valid && sc_t < sc0)   // accepted t >= tmin > 0: the float bits order like the values
             atomicMin(&F.hit_key[slot], (static_cast<unsigned long long>(__float_as_uint(sc_t)) << 32) | sc_tri);
-        if (wp && lane == 0 && wdt) part_cost_add(F.cost + tile, wdt);
+        if (timed && lane == 0 && wdt) part_cost_add(F.cost + tile, wdt);
         RTX_SPLIT_STAMP();
         return;
     } else {
@@ -1242,25 +1244,27 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                     float st = 0.f;
                     uint32_t stri = 0;
                     const int poct2 = (sfast && S.oct_bytes) ? batch_octant(sr, hitmask) : -1;
-                    unsigned long long wdt = 0;
-                    unsigned long long* const wp = (F.part_cost && F.cost) ? &wdt : nullptr;
+                    const bool timed = F.part_cost && F.cost;
+                    unsigned long long wdt;
                     if (poct2 >= 0 && scull)
-                        part_traverse<true, kSlabOct, kCullBack, kCull>(S, E, sr, poct2, live, lane, stk, st, stri, live,
-                                                                        cnt, &F.occ_bits[slot], 1u << li, sq, wp);
+                        wdt = part_traverse<true, kSlabOct, kCullBack, kCull>(S, E, sr, poct2, live, lane, stk, st, stri,
+                                                                              live, cnt, &F.occ_bits[slot], 1u << li, sq,
+                                                                              timed);
                     else if (poct2 >= 0)
-                        part_traverse<true, kSlabOct, kCullBack>(S, E, sr, poct2, live, lane, stk, st, stri, live, cnt,
-                                                                 &F.occ_bits[slot], 1u << li, CullRay{}, wp);
+                        wdt = part_traverse<true, kSlabOct, kCullBack>(S, E, sr, poct2, live, lane, stk, st, stri, live,
+                                                                       cnt, &F.occ_bits[slot], 1u << li, CullRay{}, timed);
                     else if (sfast && scull)
-                        part_traverse<true, kSlabFast, kCullBack, kCull>(S, E, sr, 0, live, lane, stk, st, stri, live,
-                                                                         cnt, &F.occ_bits[slot], 1u << li, sq, wp);
+                        wdt = part_traverse<true, kSlabFast, kCullBack, kCull>(S, E, sr, 0, live, lane, stk, st, stri,
+                                                                               live, cnt, &F.occ_bits[slot], 1u << li, sq,
+                                                                               timed);
                     else if (sfast)
-                        part_traverse<true, kSlabFast, kCullBack>(S, E, sr, 0, live, lane, stk, st, stri, live, cnt,
-                                                                  &F.occ_bits[slot], 1u << li, CullRay{}, wp);
+                        wdt = part_traverse<true, kSlabFast, kCullBack>(S, E, sr, 0, live, lane, stk, st, stri, live, cnt,
+                                                                        &F.occ_bits[slot], 1u << li, CullRay{}, timed);
                     else
-                        part_traverse<true, kSlabExact, kCullBack>(S, E, sr, 0, live, lane, stk, st, stri, live, cnt,
-                                                                   &F.occ_bits[slot], 1u << li, CullRay{}, wp);
+                        wdt = part_traverse<true, kSlabExact, kCullBack>(S, E, sr, 0, live, lane, stk, st, stri, live,
+                                                                         cnt, &F.occ_bits[slot], 1u << li, CullRay{}, timed);
                     if (did && !((live >> lane) & 1ull)) atomicOr(&F.occ_bits[slot], 1u << li);
-                    if (wp && lane == 0 && wdt) part_cost_add(F.cost + tile, wdt);
+                    if (timed && lane == 0 && wdt) part_cost_add(F.cost + tile, wdt);
                     continue;
                 }
                 occ = did & !((live >> lane) & 1ull);
@@ -1864,7 +1868,22 @@ struct rtx_ctx {
     bool heavy_pending = false;
     uint32_t split_mode = 1;         // 0 off, 1 auto, 2 force (RTX_SPLIT=0 / unset / force)
     uint32_t split_slots = 0;        // concurrent render waves on this device
-    uint32_t split_permille = kSplitPermille;   // RTX_SPLIT_FACTOR (tuning)
+    uint32_t split_permille = kSplitPermille;   // RTX_SPLIT_FACTOR (fixes it: no tuner)
+    // Split-threshold tuner: the frame is max(main kernel, split chain), and the
+    // threshold that balances the two is the fastest (Synthetic100k: factor 2.0, W4_Optional 1.5).
+    // A measured frame with split tiles times both (ev_tune: fork, main kernel end, chain end); at
+    // its adoption the factor the timed set was selected with moves toward the balance, by steps
+    // that shrink when the direction flips, until the two are within 4 % or the step is < 1.5 %.
+    bool tune_on = true;                        // RTX_SPLIT_TUNE=0 / RTX_SPLIT_FACTOR: off
+    bool tune_done = false;
+    bool tune_rec = false;                      // the measured frame in flight recorded ev_tune
+    uint32_t tune_rec_permille = 0;             // ... and the factor its (current) heavy set was selected with
+    uint32_t set_permille[2] = {0, 0};          // per heavy set: the factor the schedule selected it with
+    uint32_t tune_steps = 0;
+    int tune_dir = 0;
+    float tune_step = 1.15f;
+    float tune_main_ms = 0.f, tune_chain_ms = 0.f;   // the last timed frame (rtx_split_tune_info)
+    hipEvent_t ev_tune[3] = {nullptr, nullptr, nullptr};
     uint32_t sched_period = kSchedPeriod;       // RTX_SCHED_PERIOD (tuning)
     // motion mode (kMotionFrames): frames left, and the previous frame's cameras it compares
     uint32_t motion_left = 0;
@@ -2063,8 +2082,9 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     }
     if (const char* e = std::getenv("RTX_SPLIT_FACTOR")) {
         const double f = std::atof(e);
-        if (f > 0 && f < 1e6) c->split_permille = static_cast<uint32_t>(f * 1000.0);
+        if (f > 0 && f < 1e6) { c->split_permille = static_cast<uint32_t>(f * 1000.0); c->tune_on = false; }
     }
+    if (const char* e = std::getenv("RTX_SPLIT_TUNE")) c->tune_on = c->tune_on && std::strcmp(e, "0") != 0;
     const size_t heavy_px = static_cast<size_t>(kMaxHeavyTiles) * 64;   // pixels of the heavy wave tiles
     int cus = 0, lo_prio = 0, hi_prio = 0;
 #define RTX_CREATE_TRY(call)                                                             \
@@ -2085,6 +2105,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     RTX_CREATE_TRY(hipEventCreateWithFlags(&c->sb[1].done, hipEventDisableTiming));
     RTX_CREATE_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     RTX_CREATE_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    for (auto& e : c->ev_tune) RTX_CREATE_TRY(hipEventCreate(&e));
     RTX_CREATE_TRY(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
     RTX_CREATE_TRY(hipStreamCreateWithPriority(&c->split_stream, hipStreamNonBlocking, hi_prio));
     RTX_CREATE_TRY(hipMalloc(&c->d_counters, sizeof(unsigned long long) * kNumCounters));
@@ -2138,6 +2159,8 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     if (c->ev_heavy) (void)hipEventDestroy(c->ev_heavy);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    for (auto& e : c->ev_tune)
+        if (e) (void)hipEventDestroy(e);
     if (c->split_stream) {
         (void)hipStreamSynchronize(c->split_stream);
         (void)hipStreamDestroy(c->split_stream);
@@ -2679,6 +2702,30 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
 
 namespace {
 
+// One step of the split-threshold tuner (rtx_ctx::tune_*): the timed frame rendered the heavy set
+// selected with factor tune_rec_permille; main = its main kernel, chain = the split launches (both
+// from the fork).  The next factor is a step away from THAT factor (a set selected with an older
+// factor is not evidence about the current one), toward the balance of the two.
+void split_tune(rtx_ctx* c, float main_ms, float chain_ms) {
+    const uint32_t base = c->tune_rec_permille;
+    if (!base || main_ms <= 0.f || chain_ms <= 0.f) return;
+    if (base != c->split_permille) return;   // a set from before the last step: wait for the current one
+    const float r = chain_ms / main_ms;
+    const int dir = r > 1.04f ? 1 : (r < 0.96f ? -1 : 0);
+    if (dir == 0 || ++c->tune_steps > 16) {
+        c->tune_done = true;
+        return;
+    }
+    if (c->tune_dir != 0 && dir != c->tune_dir) c->tune_step = std::sqrt(c->tune_step);   // overshot
+    if (c->tune_step < 1.015f) {
+        c->tune_done = true;
+        return;
+    }
+    c->tune_dir = dir;
+    const double f = static_cast<double>(base) * (dir > 0 ? c->tune_step : 1.0 / c->tune_step);
+    c->split_permille = static_cast<uint32_t>(std::min(4000.0, std::max(1000.0, f)));
+}
+
 int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_params* p, bool want_rgb, FrameArgs& F,
             dim3& grid) {
     if (!c || !cams || !p) return RTX_E_INVALID;
@@ -2817,6 +2864,14 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         c->sched_ready = false;
         c->sched_frame = 0;
         c->motion_left = 0;
+        if (c->tune_on) {   // a new shape: tune again from the default
+            c->split_permille = kSplitPermille;
+            c->tune_done = false;
+            c->tune_steps = 0;
+            c->tune_dir = 0;
+            c->tune_step = 1.15f;
+        }
+        c->tune_rec = false;
         HIP_TRY(c, hipMemsetAsync(c->d_cost, 0, ntiles * 4, c->stream));
     } else if (moved && !c->motion_off) {
         c->motion_left = kMotionFrames;
@@ -2838,6 +2893,18 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
             c->heavy_pending = false;
             c->heavy_n = std::min<uint32_t>(*c->h_heavy_n, kMaxHeavyTiles);
             c->heavy_cur ^= 1;
+            // nothing to balance while no tile is heavy at the default factor (the tuner only
+            // raises the factor from there when the split chain is the longer)
+            if (c->heavy_n == 0 && c->split_permille == kSplitPermille) c->tune_done = true;
+            if (c->tune_rec) {   // the measured frame's timings: complete (they precede ev_heavy)
+                c->tune_rec = false;
+                float mm = 0.f, ch = 0.f;
+                HIP_TRY(c, hipEventElapsedTime(&mm, c->ev_tune[0], c->ev_tune[1]));
+                HIP_TRY(c, hipEventElapsedTime(&ch, c->ev_tune[0], c->ev_tune[2]));
+                c->tune_main_ms = mm;
+                c->tune_chain_ms = ch;
+                split_tune(c, mm, ch);
+            }
         }
     }
     const bool split = c->split_mode != 0 && c->split_ok && c->sched_enabled && c->heavy_n > 0;
@@ -2848,8 +2915,10 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     F.occ_bits = c->d_occ;
     // Measure tile costs on the first frame of a shape and then every kSchedPeriod frames;
     // the frames in between reuse the last order and pay nothing for scheduling.
+    // while the split threshold is being tuned (a scene with split tiles), every other frame is measured
+    const bool tuning = c->tune_on && !c->tune_done && c->heavy_n > 0 && c->split_mode == 1 && c->split_ok;
     const bool measure = c->sched_enabled && !c->heavy_pending &&
-                         (!c->sched_ready || motion || c->sched_frame % c->sched_period == 0);
+                         (!c->sched_ready || motion || c->sched_frame % (tuning ? 2u : c->sched_period) == 0);
     ++c->sched_frame;
     F.order = (c->sched_enabled && c->sched_ready) ? c->d_order : nullptr;
     F.cost = measure ? c->d_cost : nullptr;
@@ -2953,6 +3022,8 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         // main kernel, so the two run side by side and the join closes the frame.
         const uint32_t nh = (c->heavy_n + kWavesPerBlock - 1) / kWavesPerBlock, np = c->dev.n_parts;   // heavy wave tiles per workgroup
         hipStream_t s2 = c->split_stream;
+        const bool timed = F.cost && c->tune_on && !c->tune_done && c->split_mode == 1;   // split_tune
+        if (timed) HIP_TRY(c, hipEventRecord(c->ev_tune[0], c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
         launch_phase<1>(v, dim3(nh, np, 1), s2, c->dev, F);
@@ -2963,6 +3034,11 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         }
         launch_phase<3>(v, dim3(nh, 1, 1), s2, c->dev, F);
         HIP_TRY(c, hipGetLastError());
+        if (timed) {   // (before ev_join: the frame's completion then implies this event's)
+            HIP_TRY(c, hipEventRecord(c->ev_tune[2], s2));
+            c->tune_rec = true;
+            c->tune_rec_permille = c->set_permille[c->heavy_cur];
+        }
         HIP_TRY(c, hipEventRecord(c->ev_join, s2));
     }
     if (c->hbm_stack)   // (the deep variants walk without the cull)
@@ -2972,11 +3048,13 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
     else
         launch_phase<0>(v, grid, c->stream, c->dev, F);
     HIP_TRY(c, hipGetLastError());
+    if (F.heavy_flag && c->tune_rec && F.cost) HIP_TRY(c, hipEventRecord(c->ev_tune[1], c->stream));
     if (F.heavy_flag) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     if (F.cost) {
         const uint32_t slots = (c->split_mode == 0 || !c->split_ok) ? 0u
                                : (c->split_mode == 2 ? 0xffffffffu : c->split_slots);
         const int stage = c->heavy_cur ^ 1;
+        c->set_permille[stage] = c->split_permille;
         const uint32_t nch = (F.n_tiles + kSchedChunk - 1) / kSchedChunk;
         hipLaunchKernelGGL(rtx_sched_count, dim3(nch), dim3(kReorderThreads), 0, c->stream, F.cost, F.n_tiles,
                            F.heavy_flag, c->d_saved_cost, c->d_hist, c->d_csum, nch, F.part_cost);
@@ -3233,6 +3311,15 @@ extern "C" int rtx_cull_dump(rtx_ctx* c, uint32_t anchor, uint32_t* n_slots, uin
     if (ranges) HIP_TRY(c, hipMemcpy(ranges, c->cull_rng, ns * 8, hipMemcpyDeviceToHost));
     if (nodes) HIP_TRY(c, hipMemcpy(nodes, c->dev.nodes, ns * 32, hipMemcpyDeviceToHost));
     if (tris) HIP_TRY(c, hipMemcpy(tris, c->dev.tris, static_cast<size_t>(c->cull_ntris) * 64, hipMemcpyDeviceToHost));
+    return RTX_OK;
+}
+
+extern "C" int rtx_split_tune_info(rtx_ctx* c, float* factor, float* main_ms, float* chain_ms, uint32_t* done) {
+    if (!c) return RTX_E_INVALID;
+    if (factor) *factor = static_cast<float>(c->split_permille) / 1000.f;
+    if (main_ms) *main_ms = c->tune_main_ms;
+    if (chain_ms) *chain_ms = c->tune_chain_ms;
+    if (done) *done = (!c->tune_on ? 2u : (c->tune_done ? 1u : 0u));
     return RTX_OK;
 }
 

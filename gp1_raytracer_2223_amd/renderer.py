@@ -94,6 +94,14 @@ class DeviceContext:
         abi.check(self.lib.rtx_split_info(self.h, C.byref(h), C.byref(p)), "rtx_split_info", self.h)
         return h.value, p.value
 
+    def split_tune_info(self) -> dict:
+        """The split threshold's tuner: factor, last timed main kernel / split chain (ms), state."""
+        f, m, ch, d = C.c_float(), C.c_float(), C.c_float(), C.c_uint32()
+        abi.check(self.lib.rtx_split_tune_info(self.h, C.byref(f), C.byref(m), C.byref(ch), C.byref(d)),
+                  "rtx_split_tune_info", self.h)
+        return {"factor": round(f.value, 4), "main_ms": round(m.value, 5), "chain_ms": round(ch.value, 5),
+                "state": ["tuning", "converged", "off"][d.value]}
+
     def cull_info(self) -> tuple[bool, int]:
         """(the uploaded scene renders with the exact cull, camera-record rebuilds so far)."""
         on, n = C.c_uint32(), C.c_uint64()

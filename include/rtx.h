@@ -249,6 +249,11 @@ int rtx_count_work_culled(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_
  * and the frontier size of the uploaded scene (0 = the scene is rendered unsplit).
  * Environment: RTX_SPLIT=0 disables, RTX_SPLIT=force splits every tile (tests). */
 int rtx_split_info(rtx_ctx* ctx, uint32_t* heavy_tiles, uint32_t* parts);
+/* The split threshold's tuner: the current factor (a tile is split when its cost
+ * exceeds factor x its share of the frame), the last timed frame's main kernel and split chain
+ * (ms, from the fork), and the tuner's state (0 tuning, 1 converged, 2 off: RTX_SPLIT_TUNE=0 or a
+ * fixed RTX_SPLIT_FACTOR).  Re-tuned for every new launch shape. */
+int rtx_split_tune_info(rtx_ctx* ctx, float* factor, float* main_ms, float* chain_ms, uint32_t* done);
 /* Exact cull (no reference counterpart: a pruning of the reference's own BVH walk that never
  * changes a pixel).  Reports whether the uploaded scene renders with it (on for
  * host uploads whose reference boxes are inflated enough to pay, see upload_scene) and how
