@@ -709,7 +709,8 @@ def main() -> int:
                                             "culled ordered walk (one-piece frame: the split launches' repeated path "
                                             "tests are not counted), SURVEY §8(d) costs + 23 FLOP per cull box test")})
             if d.rank == 0:
-                entry["parity"] = parity_report(r["px0"], r["rgb0"], scene, mw, mh, with_fnv=False)
+                exact = next((x for sc, w_, h_, x in PARITY_CONFIGS if (sc, w_, h_) == (scene, mw, mh)), True)
+                entry["parity"] = parity_report(r["px0"], r["rgb0"], scene, mw, mh, exact=exact, with_fnv=False)
             if N == 1:
                 entry["strong_scaling_predictor"] = stripe_predictor(ctxs[0], wl, lib_hash)
             multi.append(entry)

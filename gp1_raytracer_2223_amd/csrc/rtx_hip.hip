@@ -37,7 +37,7 @@
 
 using namespace rtxd;
 
-[[maybe_unused]] constexpr int kStampWords = 6;
+[[maybe_unused]] constexpr int kStampWords = 8;   // + primary-hit time, shadow-walk time (RTX_STAMPS)
 #if RTX_STAMPS
 #define RTX_SPLIT_STAMP()                                                                          \
     if (lane == 0 && F.split_stamps) {                                                             \
@@ -900,6 +900,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
 #if RTX_STAMPS
     // diagnostic build only: per-wave {start, end, hw_id} in the counters buffer
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_prim = t_start, t_shadow = 0;   // primary hit done; shadow mesh walks
 #endif
     uint4* stk = stkE[wave];
     unsigned long long* sT = stkT[COUNT ? wave : 0];
@@ -1065,6 +1066,9 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                                                                    unused, cnt);
             if (sc_t < best_t) { best_t = sc_t; best_kind = 3; best_idx = sc_tri; }
         }
+#if RTX_STAMPS
+        t_prim = __builtin_amdgcn_s_memrealtime();
+#endif
     } else if (PHASE == 1) {
         // one frontier part; sc0 = the scratch t the reference enters the meshes with
         const int4 E = ldc(S.parts, part);
@@ -1218,6 +1222,9 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                         live &= ~(ballot(t >= sr.tmin) & ballot(t < sr.tmax) & cand);
                     }
                 }
+#if RTX_STAMPS
+                const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
                 for (uint32_t mi = 0; mi < ((RTX_ABL_SMESH || PHASE != 0) ? 0u : n_mesh); ++mi) {
                     if (!live) break;
                     float st = 0.f;
@@ -1239,6 +1246,9 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                         mesh_traverse<true, kSlabExact, COUNT, kCullBack>(S, M, sr, 0, live, lane, stk, sT, st, stri,
                                                                           live, cnt);
                 }
+#if RTX_STAMPS
+                t_shadow += __builtin_amdgcn_s_memrealtime() - ts0;
+#endif
                 if (PHASE == 2) {
                     const int4 E = ldc(S.parts, part);
                     float st = 0.f;
@@ -1345,6 +1355,8 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         st[3] = cnt.c[kWaveNodeTests];
         st[4] = cnt.c[kWaveTriTests];
         st[5] = (static_cast<unsigned long long>(cnt.c[kSlab]) << 32) | cnt.c[kTri];
+        st[6] = t_prim - t_start;
+        st[7] = t_shadow;
     }
 #endif
     if (COUNT) {
@@ -1475,10 +1487,38 @@ __device__ __forceinline__ CullBox cull_xor(const CullBox& a, int o) {
     return r;
 }
 
+// Write-through (sc1) 8-byte stores and loads of tree values: the workgroup roots are handed to
+// the last workgroup INSIDE the launch, across XCDs whose L2s are not coherent.  A plain store
+// stays in the writer's L2 (a release fence writes it back, but the reader's L2 may still hold an
+// older copy of the line: an acquire invalidates only L1), so the roots are stored write-through
+// by the one lane that then adds to the arrival counter after its stores drained, and the last
+// workgroup reads them write-through too (MI355X_MICROARCH.md, inter-workgroup visibility: the
+// "one lane per storing workgroup, last arriver by the add's value" form).
+template <class V>
+__device__ __forceinline__ void cull_st_wt(V* p, const V& v) {
+    static_assert(sizeof(V) % 8 == 0, "8-byte pieces");
+    unsigned long long w[sizeof(V) / 8];
+    __builtin_memcpy(w, &v, sizeof(V));
+    for (size_t k = 0; k < sizeof(V) / 8; ++k)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(p) + k, w[k], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class V>
+__device__ __forceinline__ V cull_ld_wt(const V* p) {
+    unsigned long long w[sizeof(V) / 8];
+    for (size_t k = 0; k < sizeof(V) / 8; ++k)
+        w[k] = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p) + k, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    V v;
+    __builtin_memcpy(&v, w, sizeof(V));
+    return v;
+}
+
 // Leaf i = blockIdx.x * kCullTreeWG + threadIdx.x holds v; writes the tree levels of `t` (2n
 // entries, n = gridDim.x * kCullTreeWG).  `arrive`: the tree's arrival counter (0 before the
 // launch, 0 again after it); `top_lds` (<= kCullTopLds): the most workgroup roots the last
-// workgroup combines in LDS (tests lower it to exercise the global-memory path).
+// workgroup combines in LDS (tests lower it to exercise the global-memory path).  Levels below
+// the workgroup roots are read only by later launches (plain stores).
 template <class V>
 __device__ void cull_tree_build(V v, V* __restrict__ t, uint32_t* arrive, uint32_t top_lds) {
     __shared__ V part[kCullTreeWG / 64];
@@ -1493,23 +1533,22 @@ __device__ void cull_tree_build(V v, V* __restrict__ t, uint32_t* arrive, uint32
     }
     if ((tid & 63u) == 0u) part[tid >> 6] = v;
     __syncthreads();
-    if (tid == 0) {   // levels 7 and 8 (kCullTreeWG = 256 = 4 waves)
+    if (tid == 0) {   // levels 7 and 8 (kCullTreeWG = 256 = 4 waves); the root write-through
         const V a = cull_comb(part[0], part[1]), b = cull_comb(part[2], part[3]), r = cull_comb(a, b);
         t[leaf >> 7] = a;
         t[(leaf >> 7) + 1u] = b;
-        t[leaf >> 8] = r;
-        __threadfence();   // release: this workgroup's nodes before its arrival
+        cull_st_wt(t + (leaf >> 8), r);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the root has left before the arrival
         last = atomicAdd(arrive, 1u) == nwg - 1u ? 1u : 0u;
     }
     __syncthreads();
     if (!last) return;
-    __threadfence();   // acquire: every other workgroup's root is visible
     // levels above 8: the workgroup roots are nodes [nwg, 2 nwg); node j of a level = comb(2j, 2j + 1)
     if (nwg == 1u) {
         // the workgroup's root is the tree's
     } else if (nwg <= top_lds) {
         for (uint32_t w = tid; w < nwg / 2u; w += kCullTreeWG)
-            top[w] = cull_comb(t[nwg + 2u * w], t[nwg + 2u * w + 1u]);
+            top[w] = cull_comb(cull_ld_wt(t + nwg + 2u * w), cull_ld_wt(t + nwg + 2u * w + 1u));
         for (uint32_t c = nwg / 2u;; c >>= 1) {   // `top` holds level-nodes [c, 2c)
             __syncthreads();
             for (uint32_t w = tid; w < c; w += kCullTreeWG) t[c + w] = top[w];
@@ -1521,14 +1560,16 @@ __device__ void cull_tree_build(V v, V* __restrict__ t, uint32_t* arrive, uint32
             q = 0;
             for (uint32_t w = tid; w < c / 2u; w += kCullTreeWG) top[w] = r[q++];
         }
-    } else {
+    } else {   // level by level through memory, every access write-through (this workgroup's own
+               // stores are read back by its other waves: past their L1s)
         for (uint32_t c = nwg / 2u; c >= 1u; c >>= 1) {
-            for (uint32_t w = tid; w < c; w += kCullTreeWG) t[c + w] = cull_comb(t[2u * (c + w)], t[2u * (c + w) + 1u]);
-            __threadfence();
+            for (uint32_t w = tid; w < c; w += kCullTreeWG)
+                cull_st_wt(t + c + w, cull_comb(cull_ld_wt(t + 2u * (c + w)), cull_ld_wt(t + 2u * (c + w) + 1u)));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
     }
-    if (tid == 0) *arrive = 0u;   // for the next launch (stream order)
+    if (tid == 0) __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
 }
 
 // the combination of the leaves [x, y) (x <= y <= n)
@@ -2118,6 +2159,9 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     RTX_CREATE_TRY(hipMalloc(&c->d_occ, 4 * heavy_px));
     RTX_CREATE_TRY(hipMemset(c->d_hit_key, 0xff, 8 * heavy_px));
     RTX_CREATE_TRY(hipMemset(c->d_occ, 0, 4 * heavy_px));
+    // (null-stream memsets are asynchronous to the host and the context's non-blocking streams do
+    // not wait for them: finish them before any launch can read these buffers)
+    RTX_CREATE_TRY(hipStreamSynchronize(nullptr));
     RTX_CREATE_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id));
 #undef RTX_CREATE_TRY
     // waves resident at once: 7 per SIMD, 4 SIMDs per CU at the render kernel's occupancy
@@ -2224,7 +2268,10 @@ int cull_launch(rtx_ctx* c, const CullAnchors& A, bool boxes) {
         }
         if (!c->d_cull_arrive) {
             HIP_TRY(c, hipMalloc(&c->d_cull_arrive, (kCullMaxAnchors + 1) * sizeof(uint32_t)));
-            HIP_TRY(c, hipMemset(c->d_cull_arrive, 0, (kCullMaxAnchors + 1) * sizeof(uint32_t)));
+            // on the context stream: a plain hipMemset runs on the null stream, which this
+            // non-blocking stream does not wait for (the first tree launch then read whatever the
+            // recycled allocation held as its arrival counts)
+            HIP_TRY(c, hipMemsetAsync(c->d_cull_arrive, 0, (kCullMaxAnchors + 1) * sizeof(uint32_t), c->stream));
         }
     }
     for (uint32_t j = 0; j < A.n; ++j) {

@@ -546,3 +546,41 @@ def test_executed_work_counts(product_ctx, name):
     assert got[14] > 0 and got[4] <= ref[4], (got, ref)
     if name == "Synthetic100k":
         assert got[3] < 0.25 * ref[3] and got[4] < 0.1 * ref[4], (got[3] / ref[3], got[4] / ref[4])
+
+
+@pytest.mark.parametrize("top", ["lds", "global"])
+def test_cull_records_across_uploads(top):
+    """The record trees hand their workgroup roots to the last workgroup inside the launch, across
+    XCDs whose L2s are not coherent; a stale line shows only with warm caches and uneven load.  One
+    context alternates uploads of different scenes and states (the same tree scratch rewritten
+    each time, frames rendered in between) and after every upload the camera and light records
+    must equal the brute-force fold (tools/cull_records_ref.c)."""
+    env = {"RTX_CULL_MIN_SA": "0"}
+    if top == "global":
+        env["RTX_CULL_TOP_LDS"] = "0"
+    ctx = _ctx_env(**env)
+    ref = _records_ref()
+    try:
+        seq = [("W4_Optional", -1.0), ("Synthetic100k", -1.0), ("W4_Optional", 1.3), ("W4_Optional", 2.9),
+               ("Synthetic100k", -1.0), ("W4_Optional", 0.4)]
+        for k, (name, t) in enumerate(seq):
+            hs = HostScene(name)
+            if t >= 0:
+                hs.update(t)
+            s, cam = hs.view()
+            ctx.upload(s)
+            p = abi.make_params(320, 180)
+            for _ in range(2):
+                ctx.render_async(cam, p)
+            ctx.synchronize()
+            for j in (0, 8 + k % s.n_lights):
+                a, rec, rng, nodes, tris, nt = _dump(ctx, j)
+                want = np.zeros_like(rec)
+                ref.cull_records_ref(len(rng) // 2, nt, rng.ctypes.data, nodes.ctypes.data, tris.ctypes.data,
+                                     a.ctypes.data, 1.5, 0, want.ctypes.data)
+                r8, w8 = rec.reshape(-1, 8), want.reshape(-1, 8)
+                bad = np.nonzero(~np.all((r8[:, :7] == w8[:, :7]) & (r8[:, 7:].view(np.uint32) ==
+                                                                     w8[:, 7:].view(np.uint32)), axis=1))[0]
+                assert bad.size == 0, f"upload {k} ({name}@{t}) anchor {j}: {bad.size} records differ, slot {bad[0]}"
+    finally:
+        ctx.close()

@@ -39,10 +39,15 @@ def test_specialised_equals_generic(gpu_ctx, generic_ctx, name, t):
     p = abi.make_params(480, 270)
     gpu_ctx.upload(s)
     generic_ctx.upload(s)
-    for _ in range(3):   # frame 1 measures tile costs, frames 2+ run cost-ordered
+    for k in range(3):   # frame 1 measures tile costs, frames 2+ run cost-ordered
         apx, argb = gpu_ctx.render(cam, p)
         bpx, brgb = generic_ctx.render(cam, p)
-        assert np.array_equal(apx, bpx), f"{name}: {(apx != bpx).sum()} pixels differ"
+        if not np.array_equal(apx, bpx):   # which one is wrong, and in what scheduler state
+            r = oracle_bind.render(s, cam, p)[0]
+            raise AssertionError(f"{name} frame {k}: {(apx != bpx).sum()} pixels differ; vs oracle: specialised "
+                                 f"{(apx != r).sum()}, generic {(bpx != r).sum()}; split {gpu_ctx.split_info()} / "
+                                 f"{generic_ctx.split_info()}, tuner {gpu_ctx.split_tune_info()} / "
+                                 f"{generic_ctx.split_tune_info()}, cull {gpu_ctx.cull_info()} / {generic_ctx.cull_info()}")
         assert np.array_equal(argb.view(np.uint32), brgb.view(np.uint32))
 
 

@@ -31,13 +31,13 @@ for _ in range(5):
     ctx.time_frames(cam, p, 20)
 heavy, nparts = ctx.split_info()
 print(f'heavy tiles {heavy}, parts {nparts}')
-cap = 6 * ((W + 15) // 16) * ((H + 15) // 16) * 4 + 6 * 1024
+cap = 8 * ((W + 7) // 8) * ((H + 7) // 8) + 6 * 1024
 buf = np.zeros(cap, np.uint64)
 nw = C.c_uint64()
 abi.check(lib.rtx_debug_stamps(ctx.h, C.byref(cam), C.byref(p), buf.ctypes.data_as(C.POINTER(C.c_uint64)),
                                cap, C.byref(nw)), "stamps", ctx.h)
-st = buf[: 6 * nw.value].reshape(-1, 6)
-split = buf[6 * nw.value: 6 * nw.value + 6 * 1024].reshape(2, 1024, 3)
+st = buf[: 8 * nw.value].reshape(-1, 8)
+split = buf[8 * nw.value: 8 * nw.value + 6 * 1024].reshape(2, 1024, 3)
 wave_id = np.arange(len(st))
 keep = st[:, 1] > 0   # heavy tiles' main-kernel waves exit at once (split rendering)
 st, wave_id = st[keep], wave_id[keep]
@@ -71,14 +71,17 @@ print(f"  wave node-pair steps: mean {nodes.mean():.0f} p50 {np.median(nodes):.0
       f"tri steps: mean {tris.mean():.0f} max {tris.max()}")
 tiles_x = (W + 7) // 8
 order = np.argsort(-dur)[:12]
-print("  slowest waves: dur_us  start_us  node_steps  tri_steps  slab_eff  tri_eff  (px0, py0)")
+prim = st[:, 6] / 100.0
+shad = st[:, 7] / 100.0
+print("  slowest waves: dur_us  start_us  node_steps  tri_steps  slab_eff  tri_eff  prim_us  shadow_walk_us  rest_us  (px0, py0)")
 for w in order:
     ty, tx = divmod(int(wave_id[w]), tiles_x)
     x0 = tx * 8
     y0 = ty * 8
     se = lane_slab[w] / max(1, 128 * nodes[w])
     te = lane_tri[w] / max(1, 64 * tris[w])
-    print(f"    {dur[w]:9.1f} {start[w]:9.1f} {nodes[w]:10d} {tris[w]:10d} {se:9.3f} {te:8.3f}  ({x0}, {y0})")
+    print(f"    {dur[w]:9.1f} {start[w]:9.1f} {nodes[w]:10d} {tris[w]:10d} {se:9.3f} {te:8.3f} {prim[w]:8.1f} "
+          f"{shad[w]:15.1f} {dur[w] - prim[w] - shad[w]:8.1f}  ({x0}, {y0})")
 us_per_step = dur / np.maximum(1, nodes + tris)
 print(f"  us per (node+tri) step: p50 {np.median(us_per_step):.3f}  slowest-wave {us_per_step[order[0]]:.3f}")
 for ph in range(2):
