@@ -1656,9 +1656,11 @@ __device__ __forceinline__ void cull_write(float4* __restrict__ cull, uint32_t s
     r[1] = make_float4(Ef[1], Ef[2], (bad || !(dt < 0x1p100f)) ? INFINITY : dt, __uint_as_float(worth ? 1u : 0u));
 }
 
-// One thread per node slot.  BOX (at upload): the slot's box from the box tree, kept in `nbox`
+// One thread per node slot.  BOX (after an upload): the slot's box from the box tree, kept in `nbox`
 // for the camera anchors' later launches; else read from `nbox`.  An empty range (padding slot)
 // or a box with an infinite bound (an out-of-domain triangle below) gives the always-pass record.
+// (Reducing the box and several anchors' trees in one walk up the levels, their loads issued
+// together, measured slower: Synthetic100k camera records 11.2 -> 34.8 us, profiles/r05.)
 template <bool BOX>
 __global__ void __launch_bounds__(256) rtx_cull_nodes(const uint2* __restrict__ rng, uint32_t nslots, uint32_t ntris,
                                                       uint32_t n, const CullBox* __restrict__ btree,
@@ -1924,10 +1926,13 @@ struct rtx_ctx {
     int tune_dir = 0;
     float tune_step = 1.15f;
     float tune_main_ms = 0.f, tune_chain_ms = 0.f;   // the last timed frame (rtx_split_tune_info)
+    float tune_best_span = 0.f;                 // the fastest max(main, chain) seen, and its factor
+    uint32_t tune_best_permille = 0;
     hipEvent_t ev_tune[3] = {nullptr, nullptr, nullptr};
     uint32_t sched_period = kSchedPeriod;       // RTX_SCHED_PERIOD (tuning)
     // motion mode (kMotionFrames): frames left, and the previous frame's cameras it compares
     uint32_t motion_left = 0;
+    bool frame_motion = false;                  // the frame being prepared / launched is in motion mode
     bool motion_off = false;                    // RTX_MOTION=0: always the static schedule (A/B)
     int prev_views = 0;
     ViewCam prev_cam[kMaxViews] = {};
@@ -2753,10 +2758,22 @@ namespace {
 // selected with factor tune_rec_permille; main = its main kernel, chain = the split launches (both
 // from the fork).  The next factor is a step away from THAT factor (a set selected with an older
 // factor is not evidence about the current one), toward the balance of the two.
+// The frame span max(main, chain) of every factor tried is kept: a step that makes it 5 % worse
+// than the best seen returns to the best and stops (a GPU that cannot run the chain beside the main
+// kernel — a profiler serialising dispatches, another process — would otherwise drift the factor).
 void split_tune(rtx_ctx* c, float main_ms, float chain_ms) {
     const uint32_t base = c->tune_rec_permille;
     if (!base || main_ms <= 0.f || chain_ms <= 0.f) return;
     if (base != c->split_permille) return;   // a set from before the last step: wait for the current one
+    const float span = std::max(main_ms, chain_ms);
+    if (c->tune_best_permille == 0 || span < c->tune_best_span) {
+        c->tune_best_span = span;
+        c->tune_best_permille = base;
+    } else if (span > 1.05f * c->tune_best_span) {
+        c->split_permille = c->tune_best_permille;
+        c->tune_done = true;
+        return;
+    }
     const float r = chain_ms / main_ms;
     const int dir = r > 1.04f ? 1 : (r < 0.96f ? -1 : 0);
     if (dir == 0 || ++c->tune_steps > 16) {
@@ -2917,6 +2934,8 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
             c->tune_steps = 0;
             c->tune_dir = 0;
             c->tune_step = 1.15f;
+            c->tune_best_span = 0.f;
+            c->tune_best_permille = 0;
         }
         c->tune_rec = false;
         HIP_TRY(c, hipMemsetAsync(c->d_cost, 0, ntiles * 4, c->stream));
@@ -2925,6 +2944,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     }
     const bool motion = c->motion_left > 0;
     if (motion) --c->motion_left;
+    c->frame_motion = motion;
     if (c->heavy_pending) {
         bool ready = true;
         if (motion) {   // no host wait: adopt only a measurement that has completed
@@ -2963,7 +2983,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     // Measure tile costs on the first frame of a shape and then every kSchedPeriod frames;
     // the frames in between reuse the last order and pay nothing for scheduling.
     // while the split threshold is being tuned (a scene with split tiles), every other frame is measured
-    const bool tuning = c->tune_on && !c->tune_done && c->heavy_n > 0 && c->split_mode == 1 && c->split_ok;
+    const bool tuning = c->tune_on && !c->tune_done && c->heavy_n > 0 && c->split_mode == 1 && c->split_ok && !motion;
     const bool measure = c->sched_enabled && !c->heavy_pending &&
                          (!c->sched_ready || motion || c->sched_frame % (tuning ? 2u : c->sched_period) == 0);
     ++c->sched_frame;
@@ -3069,7 +3089,8 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         // main kernel, so the two run side by side and the join closes the frame.
         const uint32_t nh = (c->heavy_n + kWavesPerBlock - 1) / kWavesPerBlock, np = c->dev.n_parts;   // heavy wave tiles per workgroup
         hipStream_t s2 = c->split_stream;
-        const bool timed = F.cost && c->tune_on && !c->tune_done && c->split_mode == 1;   // split_tune
+        // split_tune: static cameras only (a moving one changes the frame under the measurement)
+        const bool timed = F.cost && c->tune_on && !c->tune_done && c->split_mode == 1 && !c->frame_motion;
         if (timed) HIP_TRY(c, hipEventRecord(c->ev_tune[0], c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fork, 0));

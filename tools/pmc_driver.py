@@ -7,6 +7,7 @@ Rank 0's stripes of a `stripe_step`-way tiled frame (16-row stripes; step 1 = th
 one frame at a time (synchronised), exactly the launches bench.py times: the first frame
 measures tile costs, later ones run cost-ordered and split the heavy tiles."""
 import ctypes as C
+import os
 import sys
 from pathlib import Path
 
@@ -19,8 +20,16 @@ from gp1_raytracer_2223_amd.renderer import DeviceContext  # noqa: E402
 from gp1_raytracer_2223_amd.scene import HostScene  # noqa: E402
 
 
+# The split threshold the context's tuner converges to without a profiler (profiles/r05/
+# split_tune_probe.txt).  Under PMC collection every dispatch is serialized, so the split chain
+# can no longer run beside the main kernel and the tuner (which balances the two) would drift to
+# its upper bound: the PMC runs fix the factor instead (RTX_SPLIT_FACTOR turns the tuner off).
+TUNED_SPLIT_FACTOR = {"Synthetic100k": "2.0", "W4_Optional": "1.5"}
+
+
 def main() -> int:
     scene, W, H, step, frames = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+    factor = os.environ.setdefault("RTX_SPLIT_FACTOR", TUNED_SPLIT_FACTOR.get(scene, "1.5"))
     ctx = DeviceContext(0)
     hs = HostScene(scene)   # owns the arrays the view points into: keep it alive
     s, cam = hs.view()
@@ -35,7 +44,8 @@ def main() -> int:
     ctx.close()
     print(f"rendered {frames} frames of {scene} {W}x{H} stripe_step {step}")
     # (read by tools/pmc_configs.py: the per-phase algorithmic bytes)
-    print(f"STATE heavy_tiles={heavy} parts={parts} scene_bytes={nb.value} lights={s.n_lights}")
+    print(f"STATE heavy_tiles={heavy} parts={parts} scene_bytes={nb.value} lights={s.n_lights} "
+          f"split_permille={int(round(float(factor) * 1000))}")
     return 0
 
 
