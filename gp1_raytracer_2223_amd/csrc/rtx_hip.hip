@@ -557,6 +557,10 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
         while (ntri == 0) {
             NodePair P;
             ldcb64(nb, link, P.l0, P.l1, P.r0, P.r1);
+            // the pair's cull records at the same offset, loaded beside the pair (one memory
+            // latency per step, not two: the shadow walk had issued it only after the slab tests)
+            [[maybe_unused]] NodePair Q;
+            if (CULL) ldcb64(cq.base, link, Q.l0, Q.l1, Q.r0, Q.r1);
             if constexpr (COUNT) {
                 if ((m >> lane) & 1ull) cp->c[kSlab] += 2;
                 if (lane == 0) cp->c[kWaveNodeTests]++;
@@ -565,8 +569,6 @@ __device__ void bvh_walk_lean(const DevScene& S, const float4* nb, float cs, con
             unsigned long long mr = slab_mask<SLAB>(P.r0, P.r1, r) & m;
             [[maybe_unused]] bool rfirst = false;
             if (CULL) {
-                NodePair Q;
-                ldcb64(cq.base, link, Q.l0, Q.l1, Q.r0, Q.r1);
                 // only pairs whose records are flagged worth testing (cull_write), and only when
                 // some lane entered a child
                 if ((__float_as_uint(Q.l1.w) | __float_as_uint(Q.r1.w)) && (ml | mr)) {
