@@ -681,12 +681,12 @@ __device__ void mesh_traverse(const DevScene& S, const int4 M, const Ray& r, int
     // root (odd global index; every child pair starts at an even one, 64-B aligned)
     float4 b0, b1;
     ldcb32(nb, static_cast<uint32_t>(M.x), b0, b1);   // M.x: the root's byte offset
+    [[maybe_unused]] float4 c0, c1;   // the root's cull record, loaded beside it
+    if (CULL) ldcb32(cq.base, static_cast<uint32_t>(M.x), c0, c1);
     if (COUNT && ((mask >> lane) & 1ull)) cnt.c[kSlab]++;
     unsigned long long m =
         (OCT ? slab_mask<kSlabOct>(b0, b1, r) : slab_mask<FAST ? kSlabFast : kSlabExact>(b0, b1, r)) & mask;
     if (CULL && m) {
-        float4 c0, c1;
-        ldcb32(cq.base, static_cast<uint32_t>(M.x), c0, c1);
         float n;
         if (__float_as_uint(c1.w)) {
             if (COUNT && ((m >> lane) & 1ull)) cnt.c[kCullTests]++;
@@ -729,10 +729,10 @@ __device__ unsigned long long part_traverse(const DevScene& S, const int4 E, con
                                         : S.nodes;
     float4 b0, b1;
     ldcb32(nb, static_cast<uint32_t>(M.x), b0, b1);   // M.x: the root's byte offset
+    [[maybe_unused]] float4 q0, q1;   // cull records loaded beside their nodes (one latency per step)
+    if (CULL) ldcb32(cq.base, static_cast<uint32_t>(M.x), q0, q1);
     unsigned long long m = slab_mask<SLAB>(b0, b1, r) & mask;
     if (CULL && m) {
-        float4 q0, q1;
-        ldcb32(cq.base, static_cast<uint32_t>(M.x), q0, q1);
         float n;
         if (__float_as_uint(q1.w)) m &= cull_pass<ANY>(q0, q1, r, cq, sc_t, n);
     }
@@ -742,11 +742,10 @@ __device__ unsigned long long part_traverse(const DevScene& S, const int4 E, con
         NodePair P;
         ldcb64(nb, link, P.l0, P.l1, P.r0, P.r1);
         const bool right = (path >> d) & 1u;
+        if (CULL) ldcb32(cq.base, link + (right ? 32u : 0u), q0, q1);
         const float4 c0 = right ? P.r0 : P.l0, c1 = right ? P.r1 : P.l1;
         m &= slab_mask<SLAB>(c0, c1, r);
         if (CULL) {
-            float4 q0, q1;
-            ldcb32(cq.base, link + (right ? 32u : 0u), q0, q1);
             float n;
             if (__float_as_uint(q1.w)) m &= cull_pass<ANY>(q0, q1, r, cq, sc_t, n);
         }
