@@ -1073,6 +1073,17 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
     } else if (PHASE == 1) {
         // one frontier part; sc0 = the scratch t the reference enters the meshes with
         const int4 E = ldc(S.parts, part);
+        if (RTX_P1_SHARED_T && valid) {
+            // the parts that finished before this one already merged their keys: a lane's final t
+            // is at most their minimum T, so the walk needs only hits with t <= T (initial scratch t
+            // = the next float above T; equal t still compete on the triangle index).  Read at the
+            // coherence point (the keys' atomics come from every XCD); a stale key is larger, still
+            // a bound.
+            const unsigned long long k0 = __hip_atomic_load(&F.hit_key[slot], __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+            const float tb = __uint_as_float(static_cast<uint32_t>(k0 >> 32) + 1u);
+            if (k0 != ~0ull && tb < sc_t) sc_t = tb;
+        }
         const float sc0 = sc_t;
         uint32_t sc_tri = 0;
         unsigned long long unused = 0;

@@ -14,8 +14,8 @@
 // switch; their records stay under profiles/ (profiles/r01/ablate_history.md, profiles/r03/
 // ab_*.txt): the plane-skip of primary rays, the touch prefetch of child records, XCD bands
 // and XCD runs, the early sphere-loop exit, the unfused triangle test, the non-asm child select;
-// round 4: the 128-ray pair kernel, the culled walks' prefetch touches and the split parts' shared
-// best key (profiles/r04/).
+// round 4: the 128-ray pair kernel and the culled walks' prefetch touches (profiles/r04/); round 5:
+// the split grid with the part fastest and a per-group rotation of the XCD dealing (profiles/r05/).
 #ifndef RTX_VARIANTS_H
 #define RTX_VARIANTS_H
 
@@ -44,6 +44,15 @@
 // than 1 on Synthetic100k and its shares, W4_Optional and Bunny + 8 lights at s = 8; 0 is slower.
 #ifndef RTX_OCC_POLL
 #define RTX_OCC_POLL 2
+#endif
+
+// split closest hit (PHASE 1): a part walk starts from the minimum key the pixel's other parts
+// have merged so far (1, product: read at the coherence point, the next float above its t) or from
+// the sphere/plane scratch t (0).  profiles/r05/ab_p1_shared_key.txt: 1 is ~1 % faster on
+// Synthetic100k (0.857 -> 0.847 ms), neutral elsewhere; round 4's version (a plain load) measured
+// nothing.
+#ifndef RTX_P1_SHARED_T
+#define RTX_P1_SHARED_T 1
 #endif
 
 // ---- diagnostics (never a product build) -------------------------------------------------

@@ -445,7 +445,17 @@ def test_cull_adversarial_lights(cull_ctx, plain_ctx, light_case):
     assert ok.value == 1
 
 
-def test_cull_ordered_walk_tie_break_is_observable(cull_ctx, plain_ctx, tmp_path):
+@pytest.fixture(scope="module")
+def split_cull_ctx():
+    """The cull with every tile split (RTX_SPLIT=force) into few parts: the closest hit is the
+    minimum of the parts' (t, triangle) keys (PHASE 1)."""
+    ctx = _ctx_env(RTX_CULL_MIN_SA="0", RTX_CULL_RATIO="0", RTX_SPLIT="force", RTX_SPLIT_PARTS="8")
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_cull_ordered_walk_tie_break_is_observable(cull_ctx, split_cull_ctx, plain_ctx, tmp_path, split):
     """The tie test above cannot see a wrong tie-break: duplicate faces shade identically.  Here
     each duplicate pair gets DIFFERENT normals (the stored per-triangle normals are a separate
     input; the copy's is tilted, same side as the original's so back-face culling is unchanged
@@ -509,7 +519,9 @@ def test_cull_ordered_walk_tie_break_is_observable(cull_ctx, plain_ctx, tmp_path
         swapped[[lo, hi]] = swapped[[hi, lo]]
     sB = with_normals(swapped)
     p = abi.make_params(256, 192, 0, 1)   # ObservedArea: the normal shows directly
-    _check(cull_ctx, plain_ctx, sA, cam, p, "tilted duplicates", True)
+    _check(split_cull_ctx if split else cull_ctx, plain_ctx, sA, cam, p, "tilted duplicates", True)
+    if split:
+        assert split_cull_ctx.split_info()[0] > 0, "the split frames must have run"
     ra = oracle_bind.render(sA, cam, p)[0]
     rb = oracle_bind.render(sB, cam, p)[0]
     assert (ra != rb).sum() > 1000, "the swapped tie-break must be visible"
