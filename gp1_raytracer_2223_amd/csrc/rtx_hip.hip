@@ -3106,14 +3106,16 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         if (timed) HIP_TRY(c, hipEventRecord(c->ev_tune[0], c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
-        launch_phase<1>(v, dim3(nh, np, 1), s2, c->dev, F);
-        HIP_TRY(c, hipGetLastError());
-        if (F.shadows && c->dev.n_lights) {
-            launch_phase<2>(v, dim3(nh, np, c->dev.n_lights), s2, c->dev, F);
+        if (!RTX_ABL_CHAIN) {
+            launch_phase<1>(v, dim3(nh, np, 1), s2, c->dev, F);
+            HIP_TRY(c, hipGetLastError());
+            if (F.shadows && c->dev.n_lights) {
+                launch_phase<2>(v, dim3(nh, np, c->dev.n_lights), s2, c->dev, F);
+                HIP_TRY(c, hipGetLastError());
+            }
+            launch_phase<3>(v, dim3(nh, 1, 1), s2, c->dev, F);
             HIP_TRY(c, hipGetLastError());
         }
-        launch_phase<3>(v, dim3(nh, 1, 1), s2, c->dev, F);
-        HIP_TRY(c, hipGetLastError());
         if (timed) {   // (before ev_join: the frame's completion then implies this event's)
             HIP_TRY(c, hipEventRecord(c->ev_tune[2], s2));
             c->tune_rec = true;
@@ -3125,7 +3127,7 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, true, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
     else if (c->deep_stack)
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
-    else
+    else if (!(RTX_ABL_MAIN && F.heavy_flag && !F.cost))
         launch_phase<0>(v, grid, c->stream, c->dev, F);
     HIP_TRY(c, hipGetLastError());
     if (F.heavy_flag && c->tune_rec && F.cost) HIP_TRY(c, hipEventRecord(c->ev_tune[1], c->stream));

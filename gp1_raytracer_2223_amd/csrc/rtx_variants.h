@@ -15,7 +15,8 @@
 // ab_*.txt): the plane-skip of primary rays, the touch prefetch of child records, XCD bands
 // and XCD runs, the early sphere-loop exit, the unfused triangle test, the non-asm child select;
 // round 4: the 128-ray pair kernel and the culled walks' prefetch touches (profiles/r04/); round 5:
-// the split grid with the part fastest and a per-group rotation of the XCD dealing (profiles/r05/).
+// the split grid with the part fastest, a per-group rotation of the XCD dealing and wave priority
+// for the heaviest unsplit tiles (profiles/r05/).
 #ifndef RTX_VARIANTS_H
 #define RTX_VARIANTS_H
 
@@ -85,6 +86,14 @@
 #endif
 #ifndef RTX_ABL_LIGHTS
 #define RTX_ABL_LIGHTS 0
+#endif
+// split frames: the main launch alone (the heavy tiles' chain not launched) / the chain alone (the
+// main launch skipped on the frames that do not measure tile costs)
+#ifndef RTX_ABL_CHAIN
+#define RTX_ABL_CHAIN 0
+#endif
+#ifndef RTX_ABL_MAIN
+#define RTX_ABL_MAIN 0
 #endif
 
 // ---- device Update build (rtx_anim.hip; opt-in, RTX_ANIM_DEVICE / --device-update) --------
