@@ -1977,6 +1977,10 @@ struct rtx_ctx {
     bool cull_animated = true;
     uint32_t renders_since_upload = 0;
     uint32_t short_uploads = 0;
+    // An upload in that pattern (the previous upload was rendered at most once too) moves the
+    // geometry under a fixed tile schedule as a moving camera does: the next frame starts motion
+    // mode (prepare; RTX_MOTION=0 turns both off).
+    bool upload_motion = false;
     CullBox* d_cull_btree = nullptr;      // 2n entries
     CullMD* d_cull_mtree = nullptr;       // 2n entries per anchor of one launch
     CullBox* d_cull_nbox = nullptr;       // per node slot of the current image
@@ -2360,6 +2364,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
     if (c) {   // the upload pattern the cull decision reads (see rtx_ctx::cull_animated)
         c->short_uploads = (c->has_scene && c->renders_since_upload <= 1) ? c->short_uploads + 1 : 0;
         c->renders_since_upload = 0;
+        c->upload_motion = c->short_uploads >= 1;
     }
     return upload_scene(c, s, nullptr);
 }
@@ -2932,6 +2937,8 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     }
     std::memcpy(c->prev_cam, F.cam, sizeof(ViewCam) * static_cast<size_t>(n_views));
     c->prev_views = n_views;
+    moved = moved || c->upload_motion;   // animated geometry (rtx_ctx::upload_motion)
+    c->upload_motion = false;
     if (key != c->sched_key) {   // new shape or scene: identity order, fresh costs, no split
         if (c->heavy_pending) HIP_TRY(c, hipEventSynchronize(c->ev_heavy));
         c->heavy_pending = false;
