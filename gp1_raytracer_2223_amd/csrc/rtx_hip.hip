@@ -1981,6 +1981,13 @@ struct rtx_ctx {
     // geometry under a fixed tile schedule as a moving camera does: the next frame starts motion
     // mode (prepare; RTX_MOTION=0 turns both off).
     bool upload_motion = false;
+    // The cull's worth estimate (upload_scene: the surface areas of every node's reference box and
+    // tight box, tens of us of host time per upload) is reused by the uploads of such a loop for
+    // kCullWorthReuse uploads while the scene's counts stay the same: the decision only picks the
+    // faster of two exact walks.
+    int cull_worth = -1;
+    uint32_t cull_worth_age = 0;
+    std::string cull_worth_sig;
     CullBox* d_cull_btree = nullptr;      // 2n entries
     CullMD* d_cull_mtree = nullptr;       // 2n entries per anchor of one launch
     CullBox* d_cull_nbox = nullptr;       // per node slot of the current image
@@ -2044,39 +2051,47 @@ int bvh_depth_check(const rtx_mesh& m, std::string& why, int& depth) {
     return RTX_OK;
 }
 
+// Per device node slot of one mesh's re-laid-out tree, slots [r0, r1): the range of device
+// triangles under it (children's slots follow their parent's, so one backward sweep).  `contig`:
+// every subtree's leaves hold consecutive triangles in left-then-right order (build_parts'
+// condition); `ordered`: every left child's range ends at or before its sibling's starts (the
+// ordered walk's, DevScene::cull).  One sweep serves both (an animated loop uploads every frame).
+void slot_ranges(const std::vector<float4>& nodes, uint32_t r0, uint32_t r1, std::vector<uint2>& rng, bool& contig,
+                 bool& ordered) {
+    if (rng.size() < r1) rng.resize(r1, make_uint2(0u, 0u));
+    contig = ordered = true;
+    for (uint32_t sl = r1; sl-- > r0;) {
+        uint32_t link, cnt;
+        std::memcpy(&link, &nodes[2 * sl + 1].z, 4);
+        std::memcpy(&cnt, &nodes[2 * sl + 1].w, 4);
+        if (cnt) {
+            rng[sl] = make_uint2(link, link + cnt);
+        } else {
+            const uint2 l = rng[link], r = rng[link + 1];
+            contig = contig && l.y == r.x;
+            ordered = ordered && l.y <= r.x;
+            rng[sl] = make_uint2(std::min(l.x, r.x), std::max(l.y, r.y));
+        }
+    }
+}
+
 // Frontier of one re-laid-out mesh BVH for split rendering: start from the root and split
 // the part with the most triangles until kPartsPerMesh parts (or only leaves) remain.
 // Returns false when the tree's left-then-right DFS does not visit the triangles in
-// increasing index order — the property that makes the min-key merge of the parts equal
-// to the reference's first-found closest hit — so the scene is rendered unsplit.
+// increasing index order (`contig`, slot_ranges) — the property that makes the min-key merge of
+// the parts equal to the reference's first-found closest hit — so the scene is rendered unsplit.
 bool build_parts(const std::vector<float4>& nodes, uint32_t root, uint32_t mesh, uint32_t target,
-                 std::vector<int4>& parts) {
+                 const std::vector<uint2>& rng, bool contig, std::vector<int4>& parts) {
+    if (!contig) return false;
     auto link = [&](uint32_t n) { uint32_t u; std::memcpy(&u, &nodes[2 * n + 1].z, 4); return u; };
     auto ntri = [&](uint32_t n) { uint32_t u; std::memcpy(&u, &nodes[2 * n + 1].w, 4); return u; };
-    // DFS leaf order and subtree triangle counts
-    std::vector<uint32_t> st{root}, post;
-    uint32_t next_tri = ~0u;
-    while (!st.empty()) {
-        const uint32_t n = st.back();
-        st.pop_back();
-        post.push_back(n);
-        if (ntri(n)) {
-            if (next_tri != ~0u && link(n) != next_tri) return false;
-            next_tri = link(n) + ntri(n);
-        } else {
-            st.push_back(link(n) + 1);
-            st.push_back(link(n));
-        }
-    }
-    std::vector<uint32_t> sub(nodes.size() / 2, 0);
-    for (auto it = post.rbegin(); it != post.rend(); ++it)
-        sub[*it] = ntri(*it) ? ntri(*it) : sub[link(*it)] + sub[link(*it) + 1];
+    auto sub = [&](uint32_t n) { return rng[n].y - rng[n].x; };   // triangles under slot n
     struct P { uint32_t node, path, depth; };
     std::vector<P> fr{{root, 0u, 0u}};
     while (fr.size() < target) {
         int best = -1;
         for (size_t k = 0; k < fr.size(); ++k)
-            if (!ntri(fr[k].node) && fr[k].depth < 31 && (best < 0 || sub[fr[k].node] > sub[fr[best].node]))
+            if (!ntri(fr[k].node) && fr[k].depth < 31 && (best < 0 || sub(fr[k].node) > sub(fr[best].node)))
                 best = static_cast<int>(k);
         if (best < 0) break;
         const P e = fr[best];
@@ -2393,7 +2408,21 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
                    (c->short_uploads < 2 || c->cull_animated);
     double bmin[3] = {INFINITY, INFINITY, INFINITY}, bmax[3] = {-INFINITY, -INFINITY, -INFINITY};   // mesh vertices
     std::vector<std::pair<uint32_t, uint32_t>> mesh_slots;   // node slots [first, end) of each mesh's tree
+    std::vector<uint2> slot_rng;   // per device node slot: its triangles (slot_ranges)
+    bool ordered_all = true;
     std::vector<float> tbox;   // per triangle (lo, hi) per axis: the cull's worth estimate below
+    std::string worth_sig;
+    bool reuse_worth = false;
+    if (cull_on) {
+        // (not the node count: an animated loop's host rebuilds its trees, whose sizes vary)
+        size_t nt = 0;
+        for (uint32_t mi = 0; mi < s->n_meshes; ++mi) nt += s->meshes[mi].n_indices / 3;
+        worth_sig = std::to_string(s->n_spheres) + "/" + std::to_string(s->n_planes) + "/" + std::to_string(s->n_meshes) +
+                    "/" + std::to_string(nt) + "/" + std::to_string(s->n_lights);
+        reuse_worth = c->short_uploads >= 1 && c->cull_worth >= 0 && c->cull_worth_age + 1 < kCullWorthReuse &&
+                      c->cull_worth_sig == worth_sig;
+        if (!reuse_worth) tbox.reserve(6 * nt);
+    }
     double max_ee = 0.0;   // max |e1| * |e2| over the triangles (DevScene::tri_fast)
     int max_depth = 0;     // deepest BVH node over the meshes (stack variant)
     for (uint32_t i = 0; i < s->n_spheres; ++i) {
@@ -2439,10 +2468,11 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
                 const float lo = std::fmin(v0[a], std::fmin(v1[a], v2[a])), hi = std::fmax(v0[a], std::fmax(v1[a], v2[a]));
                 bmin[a] = std::fmin(bmin[a], lo);
                 bmax[a] = std::fmax(bmax[a], hi);
-                if (cull_on) { tbox.push_back(lo); tbox.push_back(hi); }
+                if (cull_on && !reuse_worth) { tbox.push_back(lo); tbox.push_back(hi); }
             }
         }
         uint32_t root = 0;
+        bool contig_m = true, ordered_m = true;
         if (m.n_nodes) {
             if (!m.nodes) return fail(c, RTX_E_INVALID, "mesh nodes missing");
             std::string why;
@@ -2480,6 +2510,8 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
                 nodes[2 * dst + 1] = f4(nd.min[2], nd.max[2], bits(link), bits(cnt));
             }
             mesh_slots.push_back({root, static_cast<uint32_t>(nodes.size() / 2)});
+            slot_ranges(nodes, root, static_cast<uint32_t>(nodes.size() / 2), slot_rng, contig_m, ordered_m);
+            ordered_all = ordered_all && ordered_m;
             if (lay && lay->reserve[mi]) {   // slots root .. root + 2T - 1 belong to this mesh
                 const size_t want = 2 * (static_cast<size_t>(root) + 2 * static_cast<size_t>(ntri));
                 if (nodes.size() < want) nodes.resize(want + (want / 2) % 2 * 2, f4(0, 0, 0, 0));
@@ -2493,7 +2525,7 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         // ~48 triangles per part at least: finer parts of a small mesh cost more than they spread
         const uint32_t target = std::max(2u, std::min(c->split_parts, ntri / 48u));
         const size_t p0 = parts.size();
-        if (m.n_nodes && !build_parts(nodes, root, mi, target, parts)) split_ok = false;
+        if (m.n_nodes && !build_parts(nodes, root, mi, target, slot_rng, contig_m, parts)) split_ok = false;
         if (lay && lay->reserve[mi]) {   // exactly `target` entries, the unused ones {-1, ...}
             parts.resize(p0 + target, make_int4(-1, 0, 0, 0));
             lay->part0[mi] = static_cast<uint32_t>(p0);
@@ -2517,41 +2549,46 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         // summed over the nodes (the SAH estimate of how many more slab tests the reference's
         // boxes pass): below c->cull_min_sa the records cost more than they save (measured: W4_Bunny
         // 1.19, -11 %; W4_Optional 2.40, +48 %; Synthetic100k 9.26, +182 %; profiles/r04).
-        cull_rng.assign(nodes.size() / 2, make_uint2(0u, 0u));
-        std::vector<float> nb(6 * (nodes.size() / 2));
-        double sa_ref = 0.0, sa_tight = 0.0;
-        bool increasing = true;
-        auto sa = [](double x, double y, double z) { return 2.0 * (x * y + y * z + z * x); };
-        for (const auto& [r0, r1] : mesh_slots)
-            for (uint32_t sl = r1; sl-- > r0;) {
-                uint32_t link, cnt;
-                std::memcpy(&link, &nodes[2 * sl + 1].z, 4);
-                std::memcpy(&cnt, &nodes[2 * sl + 1].w, 4);
-                float* b = &nb[6 * sl];
-                if (cnt) {
-                    cull_rng[sl] = make_uint2(link, link + cnt);
-                    for (int a = 0; a < 3; ++a) { b[2 * a] = INFINITY; b[2 * a + 1] = -INFINITY; }
-                    for (uint32_t t = link; t < link + cnt && t < tbox.size() / 6; ++t)
+        cull_rng = slot_rng;
+        cull_rng.resize(nodes.size() / 2, make_uint2(0u, 0u));
+        const bool increasing = ordered_all;   // the ordered walk needs left-then-right = increasing index
+        if (reuse_worth) {
+            ++c->cull_worth_age;
+            cull_on = increasing && c->cull_worth == 1;
+        } else {
+            std::vector<float> nb(6 * (nodes.size() / 2));
+            double sa_ref = 0.0, sa_tight = 0.0;
+            auto sa = [](double x, double y, double z) { return 2.0 * (x * y + y * z + z * x); };
+            for (const auto& [r0, r1] : mesh_slots)
+                for (uint32_t sl = r1; sl-- > r0;) {
+                    uint32_t link, cnt;
+                    std::memcpy(&link, &nodes[2 * sl + 1].z, 4);
+                    std::memcpy(&cnt, &nodes[2 * sl + 1].w, 4);
+                    float* b = &nb[6 * sl];
+                    if (cnt) {
+                        for (int a = 0; a < 3; ++a) { b[2 * a] = INFINITY; b[2 * a + 1] = -INFINITY; }
+                        for (uint32_t t = link; t < link + cnt && t < tbox.size() / 6; ++t)
+                            for (int a = 0; a < 3; ++a) {
+                                b[2 * a] = std::fmin(b[2 * a], tbox[6 * t + 2 * a]);
+                                b[2 * a + 1] = std::fmax(b[2 * a + 1], tbox[6 * t + 2 * a + 1]);
+                            }
+                    } else {
                         for (int a = 0; a < 3; ++a) {
-                            b[2 * a] = std::fmin(b[2 * a], tbox[6 * t + 2 * a]);
-                            b[2 * a + 1] = std::fmax(b[2 * a + 1], tbox[6 * t + 2 * a + 1]);
+                            b[2 * a] = std::fmin(nb[6 * link + 2 * a], nb[6 * (link + 1) + 2 * a]);
+                            b[2 * a + 1] = std::fmax(nb[6 * link + 2 * a + 1], nb[6 * (link + 1) + 2 * a + 1]);
                         }
-                } else {
-                    // the ordered walk needs left-then-right DFS order = increasing triangle index
-                    increasing = increasing && cull_rng[link].y <= cull_rng[link + 1].x;
-                    cull_rng[sl] = make_uint2(std::min(cull_rng[link].x, cull_rng[link + 1].x),
-                                              std::max(cull_rng[link].y, cull_rng[link + 1].y));
-                    for (int a = 0; a < 3; ++a) {
-                        b[2 * a] = std::fmin(nb[6 * link + 2 * a], nb[6 * (link + 1) + 2 * a]);
-                        b[2 * a + 1] = std::fmax(nb[6 * link + 2 * a + 1], nb[6 * (link + 1) + 2 * a + 1]);
                     }
+                    const float4 r0v = nodes[2 * sl], r1v = nodes[2 * sl + 1];
+                    sa_ref += sa(double(r0v.y) - r0v.x, double(r0v.w) - r0v.z, double(r1v.y) - r1v.x);
+                    sa_tight += sa(std::fmax(double(b[1]) - b[0], 0.0), std::fmax(double(b[3]) - b[2], 0.0),
+                                   std::fmax(double(b[5]) - b[4], 0.0));
                 }
-                const float4 r0v = nodes[2 * sl], r1v = nodes[2 * sl + 1];
-                sa_ref += sa(double(r0v.y) - r0v.x, double(r0v.w) - r0v.z, double(r1v.y) - r1v.x);
-                sa_tight += sa(std::fmax(double(b[1]) - b[0], 0.0), std::fmax(double(b[3]) - b[2], 0.0),
-                               std::fmax(double(b[5]) - b[4], 0.0));
-            }
-        cull_on = increasing && sa_ref >= c->cull_min_sa * sa_tight;   // false for NaN
+            const bool worth = sa_ref >= c->cull_min_sa * sa_tight;   // false for NaN
+            c->cull_worth = worth ? 1 : 0;
+            c->cull_worth_age = 0;
+            c->cull_worth_sig = worth_sig;
+            cull_on = increasing && worth;
+        }
         for (uint32_t i = 0; i < s->n_lights; ++i) {
             double R = 0.0;
             for (int k = 0; k < 8; ++k) {

@@ -26,6 +26,7 @@ constexpr int kSchedPeriod = 64;      // frames between tile-cost measurements
 // A frame whose camera differs from the previous frame's starts (or extends) motion mode for this
 // many frames: every frame is measured whose previous measurement has completed (no host wait).
 constexpr int kMotionFrames = 64;
+constexpr uint32_t kCullWorthReuse = 16;  // animated uploads per cull worth estimate (rtx_ctx::cull_worth)
 
 // Split rendering of heavy tiles: a wave tile whose measured cost exceeds
 // kSplitPermille/1000 x (frame cost / concurrent wave slots) is rendered by three extra
