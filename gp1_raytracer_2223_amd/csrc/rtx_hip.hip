@@ -2028,29 +2028,6 @@ inline float bitsi(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
 inline int32_t bitsi_f(float f) { int32_t i; std::memcpy(&i, &f, 4); return i; }
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Deepest DFS stack a wave can need for this BVH (pending right siblings on a path): at
-// most the depth of the deepest node, returned in `depth`.  RTX_E_INVALID for a malformed
-// tree.
-int bvh_depth_check(const rtx_mesh& m, std::string& why, int& depth) {
-    std::vector<std::pair<uint32_t, int>> st{{0u, 0}};
-    int maxd = 0;
-    size_t visited = 0;
-    while (!st.empty()) {
-        auto [n, d] = st.back();
-        st.pop_back();
-        if (++visited > 4ull * m.n_nodes + 4) { why = "BVH has a cycle"; return RTX_E_INVALID; }
-        maxd = d > maxd ? d : maxd;
-        const rtx_bvh_node& nd = m.nodes[n];
-        if (nd.idx_count == 0) {
-            if (nd.left_node + 1 >= m.n_nodes || nd.left_node == 0) { why = "BVH child index out of range"; return RTX_E_INVALID; }
-            st.push_back({nd.left_node + 1, d + 1});
-            st.push_back({nd.left_node, d + 1});
-        }
-    }
-    depth = maxd;
-    return RTX_OK;
-}
-
 // Per device node slot of one mesh's re-laid-out tree, slots [r0, r1): the range of device
 // triangles under it (children's slots follow their parent's, so one backward sweep).  `contig`:
 // every subtree's leaves hold consecutive triangles in left-then-right order (build_parts'
@@ -2424,6 +2401,7 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         if (!reuse_worth) tbox.reserve(6 * nt);
     }
     double max_ee = 0.0;   // max |e1| * |e2| over the triangles (DevScene::tri_fast)
+    double max_ee2_lo = 0.0;
     int max_depth = 0;     // deepest BVH node over the meshes (stack variant)
     for (uint32_t i = 0; i < s->n_spheres; ++i) {
         const rtx_sphere& p = s->spheres[i];
@@ -2460,9 +2438,16 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
             tri.push_back(f4(v0[0], v0[1], v0[2], n[0]));
             tri.push_back(e1);
             tri.push_back(e2);
-            const double ee = std::sqrt(double(e1.x) * e1.x + double(e1.y) * e1.y + double(e1.z) * e1.z) *
-                              std::sqrt(double(e2.x) * e2.x + double(e2.y) * e2.y + double(e2.z) * e2.z);
-            max_ee = (ee > max_ee || ee != ee) ? ee : max_ee;   // NaN sticks
+            // |e1| |e2| (two square roots) only for a triangle that can raise the maximum: below
+            // max_ee^2 (1 - 2^-40) the product of the roots cannot reach max_ee (their rounding is
+            // ~2^-51); NaN always takes the exact path
+            const double a2 = double(e1.x) * e1.x + double(e1.y) * e1.y + double(e1.z) * e1.z;
+            const double b2 = double(e2.x) * e2.x + double(e2.y) * e2.y + double(e2.z) * e2.z;
+            if (!(a2 * b2 < max_ee2_lo)) {
+                const double ee = std::sqrt(a2) * std::sqrt(b2);
+                max_ee = (ee > max_ee || ee != ee) ? ee : max_ee;   // NaN sticks
+                max_ee2_lo = max_ee * max_ee * (1.0 - 0x1p-40);
+            }
             tri.push_back(f4(bits(m.material), 0.f, 0.f, 0.f));
             for (int a = 0; a < 3; ++a) {
                 const float lo = std::fmin(v0[a], std::fmin(v1[a], v2[a])), hi = std::fmax(v0[a], std::fmax(v1[a], v2[a]));
@@ -2475,24 +2460,30 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
         bool contig_m = true, ordered_m = true;
         if (m.n_nodes) {
             if (!m.nodes) return fail(c, RTX_E_INVALID, "mesh nodes missing");
-            std::string why;
-            int depth = 0;
-            const int drc = bvh_depth_check(m, why, depth);
-            if (drc != RTX_OK) return fail(c, drc, why);
-            max_depth = std::max(max_depth, depth);
-            if (lay) lay->depth[mi] = depth;
             // Re-lay the tree out for the device: the root at an odd slot, every child pair
             // (left, left + 1) at an even slot so one 64-B scalar load fetches both boxes.
-            // Only the numbering changes; the tree and the left-then-right order do not.
+            // Only the numbering changes; the tree and the left-then-right order do not.  The same
+            // walk validates the tree (child indices, cycles) and finds its depth: the deepest DFS
+            // stack a wave can need (pending right siblings on a path).
             if ((nodes.size() / 2) % 2 == 0) { nodes.push_back(f4(0, 0, 0, 0)); nodes.push_back(f4(0, 0, 0, 0)); }
             root = static_cast<uint32_t>(nodes.size() / 2);
-            std::vector<std::pair<uint32_t, uint32_t>> work{{0u, root}};   // (mesh-local node, device slot)
+            struct Work { uint32_t src, dst; int depth; };   // (mesh-local node, device slot, depth)
+            std::vector<Work> work;
+            work.reserve(64);
+            work.push_back({0u, root, 0});
             nodes.resize(nodes.size() + 2);
+            int depth = 0;
+            size_t visited = 0;
             while (!work.empty()) {
-                const auto [src, dst] = work.back();
+                const Work w = work.back();
                 work.pop_back();
+                const uint32_t src = w.src, dst = w.dst;
+                if (++visited > 4ull * m.n_nodes + 4) return fail(c, RTX_E_INVALID, "BVH has a cycle");
+                depth = w.depth > depth ? w.depth : depth;
                 const rtx_bvh_node& nd = m.nodes[src];
                 uint32_t link, cnt;
+                if (nd.idx_count == 0 && (nd.left_node + 1 >= m.n_nodes || nd.left_node == 0))
+                    return fail(c, RTX_E_INVALID, "BVH child index out of range");
                 if (nd.idx_count > 0) {
                     if (nd.first_idx % 3 || nd.idx_count % 3 || nd.first_idx + nd.idx_count > m.n_indices)
                         return fail(c, RTX_E_INVALID, "BVH leaf range invalid");
@@ -2502,13 +2493,15 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
                     link = static_cast<uint32_t>(nodes.size() / 2);   // even: sizes stay even after the root
                     cnt = 0;
                     nodes.resize(nodes.size() + 4);
-                    work.push_back({nd.left_node + 1, link + 1});
-                    work.push_back({nd.left_node, link});
+                    work.push_back({nd.left_node + 1, link + 1, w.depth + 1});
+                    work.push_back({nd.left_node, link, w.depth + 1});
                 }
                 // device layout: {min.x, max.x, min.y, max.y}, {min.z, max.z, link, ntri} (slab_mask)
                 nodes[2 * dst] = f4(nd.min[0], nd.max[0], nd.min[1], nd.max[1]);
                 nodes[2 * dst + 1] = f4(nd.min[2], nd.max[2], bits(link), bits(cnt));
             }
+            max_depth = std::max(max_depth, depth);
+            if (lay) lay->depth[mi] = depth;
             mesh_slots.push_back({root, static_cast<uint32_t>(nodes.size() / 2)});
             slot_ranges(nodes, root, static_cast<uint32_t>(nodes.size() / 2), slot_rng, contig_m, ordered_m);
             ordered_all = ordered_all && ordered_m;
