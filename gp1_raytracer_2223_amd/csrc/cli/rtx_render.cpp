@@ -15,11 +15,15 @@
 #include <algorithm>
 #include <cfloat>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <memory>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -65,6 +69,59 @@ struct Benchmark {
     }
 };
 
+// One Update at a time on a worker thread (the pipelined host side of run_benchmark): start() hands
+// it a host scene and a time, wait() returns when that Update is done.
+class Updater {
+public:
+    Updater() : th_([this] { Loop(); }) {}
+    ~Updater() {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    void start(rtx_host_scene* s, float t) {
+        std::lock_guard<std::mutex> l(m_);
+        s_ = s;
+        t_ = t;
+        has_ = true;
+        done_ = false;
+        cv_.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [this] { return done_; });
+    }
+
+private:
+    void Loop() {
+        std::unique_lock<std::mutex> l(m_);
+        for (;;) {
+            cv_.wait(l, [this] { return has_ || quit_; });
+            if (has_) {   // (a pending Update runs even when quitting: wait() may be waiting for it)
+                has_ = false;
+                rtx_host_scene* s = s_;
+                const float t = t_;
+                l.unlock();
+                rtx_host_scene_update(s, t);
+                l.lock();
+                done_ = true;
+                cv_.notify_all();
+            } else if (quit_) {
+                return;
+            }
+        }
+    }
+    std::mutex m_;
+    std::condition_variable cv_;
+    rtx_host_scene* s_ = nullptr;
+    float t_ = 0.f;
+    bool has_ = false, done_ = true, quit_ = false;
+    std::thread th_;
+};
+
 // The reference's frame loop is serial: Update, Render (into the window surface), present.
 // Here `inflight` frames overlap: frame k is updated, uploaded and queued (render + D2H into
 // its own page-locked host frame) on context k % inflight while frame k - 1 still runs on
@@ -72,13 +129,27 @@ struct Benchmark {
 // behind the current frame's GPU work.  Every frame is still fully rendered and in host
 // memory before it counts: the benchmark ticks when frame k's context has finished.
 // inflight = 1 is the reference's serial loop.
+// With frames in flight and more host scenes of the same catalogue scene (`extra`, D of them) the
+// host side is pipelined too: frames k + 1 .. k + D are updated on D worker threads, each into its
+// own host scene, while the main thread uploads and queues frame k (an upload copies the host
+// arrays into page-locked staging before it returns, so the scene it read is free for frame
+// k + D + 1's Update).  A frame's time is taken when its Update starts.
 // --device-update: the animated meshes' Update (transform + BVH rebuild + scene image) runs on
 // the device (rtx_anim_*); the host only computes the frame's transforms.
 // With `seq` (--sequence t1,t2,...): no timer; frame k is Update(seq[k]) and is written to
 // `<stem>_<k>.bmp` when it completes (the pipelined loop's frames, checked by the tests).
 int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int inflight, bool device_update,
-                  const std::vector<float>* seq = nullptr, const std::string& stem = "") {
+                  const std::vector<float>* seq = nullptr, const std::string& stem = "",
+                  const std::vector<rtx_host_scene*>& extra = {}) {
     const bool animated = rtx_host_scene_animated(hs) == 1;
+    // (pipelined host side) D = the host scenes besides the one being uploaded: frames k + 1 ..
+    // k + D are being updated, frame k + i on worker (k + i) % D into host scene (k + i) % (D + 1)
+    const int D = (animated && !device_update && inflight >= 2) ? static_cast<int>(extra.size()) : 0;
+    std::vector<rtx_host_scene*> hsv{hs};
+    hsv.insert(hsv.end(), extra.begin(), extra.end());
+    std::vector<std::unique_ptr<Updater>> upd;
+    for (int i = 0; i < D; ++i) upd.emplace_back(new Updater());
+    const bool pipe = D > 0;
     const size_t npx = static_cast<size_t>(r.Width()) * r.Height();
     std::vector<rtx_ctx*> ctx{r.Context()};
     for (int f = 1; f < inflight; ++f) {
@@ -170,10 +241,25 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
         }
         const Clock::time_point f0 = Clock::now();
         const float tnow = seq ? (*seq)[queued] : static_cast<float>(secs(start, f0));
-        if (anim) rtx_host_scene_transforms(hs, tnow, mats.data(), static_cast<uint32_t>(n_anim));   // Update(t)'s turn
-        else if (animated) rtx_host_scene_update(hs, tnow);                // Scene::Update
+        rtx_host_scene* cur = hs;
+        if (pipe) {
+            const long H = D + 1;
+            cur = hsv[queued % H];
+            auto launch = [&](long k) {   // frame k's Update, on its worker, into its host scene
+                if (!seq || k < static_cast<long>(seq->size()))
+                    upd[k % D]->start(hsv[k % H], seq ? (*seq)[k] : static_cast<float>(secs(start, Clock::now())));
+            };
+            if (queued == 0)
+                for (long k = 0; k < D; ++k) launch(k);
+            upd[queued % D]->wait();   // this frame's Update (started D frames ago)
+            launch(queued + D);
+        } else if (anim) {
+            rtx_host_scene_transforms(hs, tnow, mats.data(), static_cast<uint32_t>(n_anim));   // Update(t)'s turn
+        } else if (animated) {
+            rtx_host_scene_update(hs, tnow);                // Scene::Update
+        }
         const Clock::time_point f1 = Clock::now();
-        if (!ok(rtx_host_scene_view(hs, &s, &cam), "rtx_host_scene_view", nullptr)) break;
+        if (!ok(rtx_host_scene_view(cur, &s, &cam), "rtx_host_scene_view", nullptr)) break;
         if (anim) {
             if (rtx_anim_update(anim, ctx[f], mats.data()) != RTX_OK) {
                 std::fprintf(stderr, "rtx_anim_update: %s\n", rtx_anim_last_error(anim));
@@ -197,6 +283,7 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
         ++queued;
     }
     for (int f = 0; f < inflight; ++f) rtx_synchronize(ctx[f]);
+    for (auto& u : upd) u->wait();   // (Updates started for frames the loop did not queue)
     if (anim) {
         if (!anim_ok()) rc = 1;
         rtx_anim_destroy(anim);
@@ -269,6 +356,21 @@ int main(int argc, char** argv) {
         return 1;
     }
     if (t >= 0.f) rtx_host_scene_update(hs, t);
+    // the pipelined loop's second host scene (run_benchmark): animated scenes, frames in flight,
+    // host Update
+    // (up to two more: two Updates in flight with three or more frames in flight)
+    auto more_scenes = [&]() {
+        std::vector<rtx_host_scene*> v;
+        if (inflight < 2 || device_update || rtx_host_scene_animated(hs) != 1) return v;
+        for (int i = 0; i < std::min(inflight, 3) - 1; ++i) {
+            rtx_host_scene* h = nullptr;
+            char e2[512] = {0};
+            if (rtx_host_scene_create(scene.c_str(), assets.empty() ? nullptr : assets.c_str(), &h, e2, sizeof e2) != RTX_OK)
+                break;   // (fewer Updates in flight, or the loop unpipelined)
+            v.push_back(h);
+        }
+        return v;
+    };
     int rc = 0;
     try {
         rtx::Renderer r(W, H);
@@ -278,12 +380,16 @@ int main(int argc, char** argv) {
             // --sequence t1,...: the pipelined frame loop over fixed Update times, frame k
             // written to <out stem>_<k>.bmp
             const std::string stem = out.size() > 4 && out.substr(out.size() - 4) == ".bmp" ? out.substr(0, out.size() - 4) : out;
-            rc = run_benchmark(r, hs, 0, inflight, device_update, &seq, stem);
+            const std::vector<rtx_host_scene*> more = more_scenes();
+            rc = run_benchmark(r, hs, 0, inflight, device_update, &seq, stem, more);
+            for (rtx_host_scene* h : more) rtx_host_scene_destroy(h);
             rtx_host_scene_destroy(hs);
             return rc;
         }
         if (bench) {
-            rc = run_benchmark(r, hs, bench, inflight, device_update);
+            const std::vector<rtx_host_scene*> more = more_scenes();
+            rc = run_benchmark(r, hs, bench, inflight, device_update, nullptr, "", more);
+            for (rtx_host_scene* h : more) rtx_host_scene_destroy(h);
         } else {
             r.Render(hs, true);
             auto t0 = Clock::now();
