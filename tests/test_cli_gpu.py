@@ -55,14 +55,17 @@ def _channels(px: np.ndarray) -> np.ndarray:
 
 @pytest.mark.parametrize("scene,inflight,exact,device", [("W4_Bunny", 2, True, False), ("W4_Optional", 2, False, False),
                                                          ("W4_Optional", 3, False, False),
+                                                         ("W4_Optional", 4, False, False),
                                                          ("W4_Reference", 1, False, False),
                                                          ("W4_Bunny", 2, True, True), ("W4_Optional", 3, False, True),
                                                          ("W4_Reference", 2, False, True)])
 def test_pipelined_frame_loop_matches_oracle(tmp_path, scene, inflight, exact, device):
     """The overlapped frame loop (frame k+1's Update and BVH rebuild on the host while frame
     k renders on another context) renders every frame of an animated sequence exactly as
-    the reference's serial loop: Update(t_k) on one persistent scene, then Render.  With
-    --device-update the Update itself runs on the device (rtx_anim_*)."""
+    the reference's serial loop: Update(t_k) on one persistent scene, then Render.  With 2+
+    frames in flight the host Updates themselves run ahead on worker threads, each into its
+    own copy of the scene (1 or 2 of them: inflight 2 / 3-4).  With --device-update the Update
+    itself runs on the device (rtx_anim_*)."""
     if not EXE.exists():
         pytest.skip("rtx_render not built")
     W, H = 160, 120
