@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <type_traits>
@@ -1918,6 +1919,14 @@ struct rtx_ctx {
     hipEvent_t ev_heavy = nullptr;
     hipStream_t split_stream = nullptr;   // split launches run beside the main kernel
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // Throughput mode (prepare): another context of this process on the same device still had a frame
+    // in flight when this one was queued (ev_frame, the end of each queued frame; g_frames).  The
+    // GPU then interleaves the contexts' frames and a tile's critical path is hidden by the other
+    // frames, so the split launches only add work: the measured frames select heavy tiles with at
+    // least kThroughputPermille and the tuner (whose timings the other frames distort) waits.
+    hipEvent_t ev_frame = nullptr;
+    bool concurrent = false;
+    bool throughput_off = false;                // RTX_THROUGHPUT=0
     int heavy_cur = 0;
     uint32_t heavy_n = 0;
     bool heavy_pending = false;
@@ -2088,6 +2097,32 @@ extern "C" int rtx_abi_version(void) { return RTX_ABI_VERSION; }
 namespace {
 // Reason for the last failed rtx_create on this thread (rtx_last_error(NULL)).
 thread_local std::string g_create_err;
+
+// The process's contexts that have queued a frame (rtx_ctx::ev_frame), for throughput mode.
+std::mutex g_frames_m;
+std::vector<rtx_ctx*> g_frames;
+
+// Another context on c's device with a frame still in flight (its ev_frame not reached).
+bool frames_concurrent(rtx_ctx* c) {
+    std::lock_guard<std::mutex> l(g_frames_m);
+    for (rtx_ctx* o : g_frames) {
+        if (o == c || o->device != c->device) continue;
+        const hipError_t q = hipEventQuery(o->ev_frame);
+        if (q == hipErrorNotReady) {
+            (void)hipGetLastError();   // (not-ready is no error for the caller's checks)
+            return true;
+        }
+    }
+    return false;
+}
+void frames_note(rtx_ctx* c) {
+    std::lock_guard<std::mutex> l(g_frames_m);
+    if (std::find(g_frames.begin(), g_frames.end(), c) == g_frames.end()) g_frames.push_back(c);
+}
+void frames_forget(rtx_ctx* c) {
+    std::lock_guard<std::mutex> l(g_frames_m);
+    g_frames.erase(std::remove(g_frames.begin(), g_frames.end(), c), g_frames.end());
+}
 }  // namespace
 
 extern "C" int rtx_create(rtx_ctx** out, int device_id) {
@@ -2112,6 +2147,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     // RTX_TILE_ORDER=0 disables cost-ordered tile dispatch (identity order every frame)
     if (const char* e = std::getenv("RTX_TILE_ORDER")) c->sched_enabled = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_MOTION")) c->motion_off = std::strcmp(e, "0") == 0;
+    if (const char* e = std::getenv("RTX_THROUGHPUT")) c->throughput_off = std::strcmp(e, "0") == 0;
     if (const char* e = std::getenv("RTX_SCHED_PERIOD"))
         c->sched_period = std::max<uint32_t>(1u, static_cast<uint32_t>(std::strtoul(e, nullptr, 10)));
     // RTX_SPLIT=0 renders heavy tiles in one piece; RTX_SPLIT=force splits every tile
@@ -2159,6 +2195,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     RTX_CREATE_TRY(hipEventCreateWithFlags(&c->sb[1].done, hipEventDisableTiming));
     RTX_CREATE_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     RTX_CREATE_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    RTX_CREATE_TRY(hipEventCreateWithFlags(&c->ev_frame, hipEventDisableTiming));
     for (auto& e : c->ev_tune) RTX_CREATE_TRY(hipEventCreate(&e));
     RTX_CREATE_TRY(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
     RTX_CREATE_TRY(hipStreamCreateWithPriority(&c->split_stream, hipStreamNonBlocking, hi_prio));
@@ -2185,6 +2222,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
 
 extern "C" void rtx_destroy(rtx_ctx* c) {
     if (!c) return;
+    frames_forget(c);
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& B : c->sb) {
@@ -2216,6 +2254,7 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     if (c->ev_heavy) (void)hipEventDestroy(c->ev_heavy);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->ev_frame) (void)hipEventDestroy(c->ev_frame);
     for (auto& e : c->ev_tune)
         if (e) (void)hipEventDestroy(e);
     if (c->split_stream) {
@@ -3011,7 +3050,8 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
             c->heavy_cur ^= 1;
             // nothing to balance while no tile is heavy at the default factor (the tuner only
             // raises the factor from there when the split chain is the longer)
-            if (c->heavy_n == 0 && c->split_permille == kSplitPermille) c->tune_done = true;
+            if (c->heavy_n == 0 && c->split_permille == kSplitPermille && c->set_permille[c->heavy_cur] == kSplitPermille)
+                c->tune_done = true;
             if (c->tune_rec) {   // the measured frame's timings: complete (they precede ev_heavy)
                 c->tune_rec = false;
                 float mm = 0.f, ch = 0.f;
@@ -3032,7 +3072,9 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     // Measure tile costs on the first frame of a shape and then every kSchedPeriod frames;
     // the frames in between reuse the last order and pay nothing for scheduling.
     // while the split threshold is being tuned (a scene with split tiles), every other frame is measured
-    const bool tuning = c->tune_on && !c->tune_done && c->heavy_n > 0 && c->split_mode == 1 && c->split_ok && !motion;
+    c->concurrent = !c->throughput_off && c->tune_on && frames_concurrent(c);   // (rtx_ctx::ev_frame)
+    const bool tuning = c->tune_on && !c->tune_done && c->heavy_n > 0 && c->split_mode == 1 && c->split_ok && !motion &&
+                        !c->concurrent;
     const bool measure = c->sched_enabled && !c->heavy_pending &&
                          (!c->sched_ready || motion || c->sched_frame % (tuning ? 2u : c->sched_period) == 0);
     ++c->sched_frame;
@@ -3139,7 +3181,7 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         const uint32_t nh = (c->heavy_n + kWavesPerBlock - 1) / kWavesPerBlock, np = c->dev.n_parts;   // heavy wave tiles per workgroup
         hipStream_t s2 = c->split_stream;
         // split_tune: static cameras only (a moving one changes the frame under the measurement)
-        const bool timed = F.cost && c->tune_on && !c->tune_done && c->split_mode == 1 && !c->frame_motion;
+        const bool timed = F.cost && c->tune_on && !c->tune_done && c->split_mode == 1 && !c->frame_motion && !c->concurrent;
         if (timed) HIP_TRY(c, hipEventRecord(c->ev_tune[0], c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
@@ -3173,14 +3215,17 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         const uint32_t slots = (c->split_mode == 0 || !c->split_ok) ? 0u
                                : (c->split_mode == 2 ? 0xffffffffu : c->split_slots);
         const int stage = c->heavy_cur ^ 1;
-        c->set_permille[stage] = c->split_permille;
+        // (throughput mode: at least kThroughputPermille, see rtx_ctx::ev_frame)
+        const uint32_t permille = c->concurrent ? std::max<uint32_t>(c->split_permille, kThroughputPermille)
+                                                : c->split_permille;
+        c->set_permille[stage] = permille;
         const uint32_t nch = (F.n_tiles + kSchedChunk - 1) / kSchedChunk;
         hipLaunchKernelGGL(rtx_sched_count, dim3(nch), dim3(kReorderThreads), 0, c->stream, F.cost, F.n_tiles,
                            F.heavy_flag, c->d_saved_cost, c->d_hist, c->d_csum, nch, F.part_cost);
         HIP_TRY(c, hipGetLastError());
         hipLaunchKernelGGL(rtx_sched_scan, dim3(1), dim3(kScanThreads), 0, c->stream, c->d_hist, nch,
                            c->d_csum,
-                           F.n_tiles, slots, c->split_permille, c->d_thr, c->d_heavy_n);
+                           F.n_tiles, slots, permille, c->d_thr, c->d_heavy_n);
         HIP_TRY(c, hipGetLastError());
         hipLaunchKernelGGL(rtx_sched_scatter, dim3(nch), dim3(kReorderThreads), 0, c->stream, F.cost, c->d_order,
                            F.n_tiles, c->d_hist, nch, c->d_thr, slots == 0xffffffffu ? 1u : 0u,
@@ -3191,6 +3236,8 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         c->heavy_pending = true;
         c->sched_ready = true;
     }
+    HIP_TRY(c, hipEventRecord(c->ev_frame, c->stream));   // the frame's end, for other contexts' prepare
+    frames_note(c);
     return RTX_OK;
 }
 

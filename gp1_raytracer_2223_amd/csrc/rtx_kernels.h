@@ -35,6 +35,8 @@ constexpr int kPartsPerMesh = 64;      // target frontier size per mesh BVH (wit
                                        // 1080p: 64 parts 1.00 ms, 128 1.12, 256 1.46; before it 128 beat 64 by 6 %)
 constexpr int kMaxParts = 1024;        // all meshes together
 constexpr int kMaxHeavyTiles = 8192;   // heavy wave tiles per frame (hit-key buffer: 64 px each)
+// split factor floor while other contexts' frames are in flight (rtx_ctx::ev_frame)
+constexpr uint32_t kThroughputPermille = 2600;
 // 1.5 (v14 sweep, tools/split_sweep.sh): Synthetic100k 4.38 -> 3.51 ms, W4_Optional within
 // noise of 2.0; below 1.25 the split overhead outgrows the tail it removes
 constexpr int kSplitPermille = 1500;
