@@ -88,7 +88,6 @@ COST = [41, 19, 14, 12, 63, 9, 15, 1, 26, 6, 31, 103]   # SURVEY §8(d) FLOP per
 # 6, n / f 6 add + 4 min/max, n - dt 1 — counted only in the executed-work model (frac_executed)
 COST_CULL_TEST = 23
 K_KERNEL_LAUNCHES = 1000   # launches averaged for the headline's roofline.kernel_ms
-KERNEL_CLOCK_LAUNCHES = 200   # untimed launches before kernel_ms (the GPU clock's ramp)
 
 # BASELINE.json's multi-GPU workloads: one image per step, tiled over the ranks (steps per run)
 # (+ W4_Optional: with Synthetic100k the scene the exact cull runs on, so its line carries the
@@ -454,15 +453,11 @@ class Workload:
         return self.d.max(time.perf_counter() - t0)
 
     def kernel_ms(self, launches: int) -> float:
-        """Mean launch time of ONE context's serialized launches (HIP events on its stream), after
-        KERNEL_CLOCK_LAUNCHES untimed ones: a fresh process starts the GPU at its idle clock
-        ("Short runs and the GPU clock"), which the rocprofv3 mean of the same
-        command does not see either."""
+        """Mean launch time of ONE context's serialized launches (HIP events on its stream)."""
         ms = C.c_float()
         ctx = self.ctxs[0]
-        for n in (min(KERNEL_CLOCK_LAUNCHES, launches), launches):
-            abi.check(self.lib.rtx_time_views(ctx.h, self.views, self.nviews, C.byref(self.params), n,
-                                              C.byref(ms)), "rtx_time_views", ctx.h)
+        abi.check(self.lib.rtx_time_views(ctx.h, self.views, self.nviews, C.byref(self.params), launches,
+                                          C.byref(ms)), "rtx_time_views", ctx.h)
         return ms.value
 
     def flop(self) -> tuple[int, int, int, int]:
@@ -494,11 +489,14 @@ class Workload:
 
     def run(self, steps: int, warmup: int, launches: int, gather: bool, tag: str) -> dict:
         d, W, H = self.d, self.W, self.H
-        kernel_ms = self.kernel_ms(launches)
+        self.kernel_ms(launches)   # (untimed here: the serialized launches also bring the GPU clock up)
         for i in range(warmup):
             self.step(i)
         self.sync_all()
         elapsed = self.timed(self.step, steps)          # device-resident frames (`value`)
+        # timed after the steps: a fresh process starts the GPU at its idle clock, whose ramp a mean
+        # taken first would include ("Short runs and the GPU clock")
+        kernel_ms = self.kernel_ms(launches)
 
         # the same frames gathered into host frames shared by the ranks
         nbytes = self.nviews * W * H * 16   # uint32 pixels + float RGB plane per view (parity)
@@ -759,7 +757,7 @@ def main() -> int:
                  "note": "FP32 VALU-bound path (no dense contraction, 4 B/pixel of HBM output); "
                          "FLOP = SURVEY §8(d) algorithmic model counted by the instrumented kernel; "
                          "kernel_ms/achieved are rank 0's launches (mean of kernel_launches serialized launches, "
-                         "after 200 untimed launches, before the warm-up)"})
+                         "timed after the timed steps, the clock up)"})
     strong = args.mode == "frame"
     out = {
         "metric": "Mpixels/s (primary+shadow rays) at 1920x1080; per-channel max-abs vs CPU ref",
