@@ -1988,7 +1988,7 @@ struct rtx_ctx {
     uint32_t short_uploads = 0;
     // An upload in that pattern (the previous upload was rendered at most once too) moves the
     // geometry under a fixed tile schedule as a moving camera does: the next frame starts motion
-    // mode (prepare; RTX_MOTION=0 turns both off).
+    // mode when the scene has split tiles (prepare; RTX_MOTION=0 turns both off).
     bool upload_motion = false;
     // The cull's worth estimate (upload_scene: the surface areas of every node's reference box and
     // tight box, tens of us of host time per upload) is reused by the uploads of such a loop for
@@ -3006,7 +3006,10 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     }
     std::memcpy(c->prev_cam, F.cam, sizeof(ViewCam) * static_cast<size_t>(n_views));
     c->prev_views = n_views;
-    moved = moved || c->upload_motion;   // animated geometry (rtx_ctx::upload_motion)
+    // animated geometry (rtx_ctx::upload_motion), where a stale schedule costs: a scene with split
+    // tiles (W4_Optional's F6 loop: GPU wait 0.51 -> 0.43 ms).  Without them the per-frame
+    // measurement is the larger cost (W4_Bunny's loop 7-10 % slower, W4_Reference's serial 11 %).
+    moved = moved || (c->upload_motion && c->heavy_n > 0);
     c->upload_motion = false;
     if (key != c->sched_key) {   // new shape or scene: identity order, fresh costs, no split
         if (c->heavy_pending) HIP_TRY(c, hipEventSynchronize(c->ev_heavy));
