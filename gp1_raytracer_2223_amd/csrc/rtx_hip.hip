@@ -3075,7 +3075,10 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     // Measure tile costs on the first frame of a shape and then every kSchedPeriod frames;
     // the frames in between reuse the last order and pay nothing for scheduling.
     // while the split threshold is being tuned (a scene with split tiles), every other frame is measured
-    c->concurrent = !c->throughput_off && c->tune_on && frames_concurrent(c);   // (rtx_ctx::ev_frame)
+    // (rtx_ctx::ev_frame; asked only where a tile can be split: the other contexts' event queries
+    // are not free in a GPU-bound loop)
+    c->concurrent = !c->throughput_off && c->tune_on && c->split_ok && (c->heavy_n > 0 || !c->tune_done) &&
+                    frames_concurrent(c);
     const bool tuning = c->tune_on && !c->tune_done && c->heavy_n > 0 && c->split_mode == 1 && c->split_ok && !motion &&
                         !c->concurrent;
     const bool measure = c->sched_enabled && !c->heavy_pending &&
