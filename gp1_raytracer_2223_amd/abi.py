@@ -122,6 +122,8 @@ def load_host() -> C.CDLL:
         lib.rtx_host_scene_destroy.restype = None
         lib.rtx_host_scene_update.argtypes = [VP, C.c_float]
         lib.rtx_host_scene_update.restype = C.c_int
+        lib.rtx_host_scene_copy_state.argtypes = [VP, VP]
+        lib.rtx_host_scene_copy_state.restype = C.c_int
         lib.rtx_host_scene_view.argtypes = [VP, C.POINTER(Scene), C.POINTER(Camera)]
         lib.rtx_host_scene_view.restype = C.c_int
         lib.rtx_host_scene_animated.argtypes = [VP]

@@ -45,8 +45,9 @@ def _stale(out: Path, deps: list[Path]) -> bool:
 def build_host(force: bool = False) -> Path:
     LIB.mkdir(exist_ok=True)
     out = LIB / "librtx_host.so"
-    srcs = [CSRC / "host" / "scene.cpp", CSRC / "host" / "host_api.cpp"]
-    deps = srcs + list((CSRC / "host").glob("*.h")) + [INC / "rtx.h", INC / "rtx_host.h", Path(__file__)]
+    srcs = [CSRC / "host" / "scene.cpp", CSRC / "host" / "host_api.cpp", CSRC / "host" / "view.cpp"]
+    deps = srcs + list((CSRC / "host").glob("*.h")) + [INC / "rtx.h", INC / "rtx_host.h", INC / "rtx_view.h",
+                                                         Path(__file__)]
     if force or _stale(out, deps):
         _run(["g++", "-std=c++17", "-O3", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared", "-pthread",
               "-Wall", "-Wextra", f"-I{INC}", *srcs, "-o", out, "-ldl"])

@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <iostream>
 #include <memory>
 #include <numeric>
@@ -69,12 +70,20 @@ struct Benchmark {
     }
 };
 
-// One Update at a time on a worker thread (the pipelined host side of run_benchmark): start() hands
-// it a host scene and a time, wait() returns when that Update is done.
-class Updater {
+// The pipelined host side of run_benchmark.  The reference's BuildBVH permutes the triangles in
+// place (DataTypes.h:335-363), so the state Update k leaves depends on every earlier Update: ONE
+// chain scene is updated serially, on a worker thread, and after Update k its state is copied into
+// snapshot k % D (rtx_host_scene_copy_state), which the main thread uploads.  The worker runs up to D
+// frames ahead of the uploads: Update k + 1 overlaps frame k's upload and the GPU's frames, and only
+// the snapshot copy waits for its slot.  time_of(k) gives frame k's Update time (taken when that
+// Update starts); `limit` (>= 0) stops the worker after that many frames.
+class ChainUpdater {
 public:
-    Updater() : th_([this] { Loop(); }) {}
-    ~Updater() {
+    ChainUpdater(rtx_host_scene* chain, std::vector<rtx_host_scene*> snaps, std::function<float(long)> time_of,
+                 long limit)
+        : chain_(chain), snaps_(std::move(snaps)), time_of_(std::move(time_of)), limit_(limit),
+          th_([this] { Loop(); }) {}
+    ~ChainUpdater() {
         {
             std::lock_guard<std::mutex> l(m_);
             quit_ = true;
@@ -82,44 +91,49 @@ public:
         cv_.notify_all();
         th_.join();
     }
-    void start(rtx_host_scene* s, float t) {
-        std::lock_guard<std::mutex> l(m_);
-        s_ = s;
-        t_ = t;
-        has_ = true;
-        done_ = false;
-        cv_.notify_all();
-    }
-    void wait() {
+    // frame k's snapshot, once Update k has been copied into it (nullptr if the worker failed)
+    rtx_host_scene* wait(long k) {
         std::unique_lock<std::mutex> l(m_);
-        cv_.wait(l, [this] { return done_; });
+        cv_.wait(l, [&] { return ready_ > k || failed_; });
+        return failed_ ? nullptr : snaps_[k % snaps_.size()];
+    }
+    // frame k's upload has returned (the upload copied the arrays): its snapshot may be overwritten
+    void release(long k) {
+        std::lock_guard<std::mutex> l(m_);
+        released_ = std::max(released_, k + 1);
+        cv_.notify_all();
     }
 
 private:
     void Loop() {
-        std::unique_lock<std::mutex> l(m_);
-        for (;;) {
-            cv_.wait(l, [this] { return has_ || quit_; });
-            if (has_) {   // (a pending Update runs even when quitting: wait() may be waiting for it)
-                has_ = false;
-                rtx_host_scene* s = s_;
-                const float t = t_;
-                l.unlock();
-                rtx_host_scene_update(s, t);
-                l.lock();
-                done_ = true;
-                cv_.notify_all();
-            } else if (quit_) {
-                return;
+        const long D = static_cast<long>(snaps_.size());
+        for (long k = 0;; ++k) {
+            {
+                std::lock_guard<std::mutex> l(m_);
+                if (quit_ || (limit_ >= 0 && k >= limit_)) return;
             }
+            rtx_host_scene_update(chain_, time_of_(k));   // Scene::Update, in the reference's order
+            std::unique_lock<std::mutex> l(m_);
+            cv_.wait(l, [&] { return quit_ || k < released_ + D; });
+            if (quit_) return;
+            l.unlock();
+            const int rc = rtx_host_scene_copy_state(snaps_[k % D], chain_);
+            l.lock();
+            if (rc != RTX_OK) failed_ = true;
+            ready_ = k + 1;
+            cv_.notify_all();
+            if (failed_) return;
         }
     }
+    rtx_host_scene* chain_;
+    std::vector<rtx_host_scene*> snaps_;
+    std::function<float(long)> time_of_;
+    long limit_;
     std::mutex m_;
     std::condition_variable cv_;
-    rtx_host_scene* s_ = nullptr;
-    float t_ = 0.f;
-    bool has_ = false, done_ = true, quit_ = false;
-    std::thread th_;
+    long ready_ = 0, released_ = 0;
+    bool quit_ = false, failed_ = false;
+    std::thread th_;   // (last: started after the members above)
 };
 
 // The reference's frame loop is serial: Update, Render (into the window surface), present.
@@ -130,10 +144,11 @@ private:
 // memory before it counts: the benchmark ticks when frame k's context has finished.
 // inflight = 1 is the reference's serial loop.
 // With frames in flight and more host scenes of the same catalogue scene (`extra`, D of them) the
-// host side is pipelined too: frames k + 1 .. k + D are updated on D worker threads, each into its
-// own host scene, while the main thread uploads and queues frame k (an upload copies the host
-// arrays into page-locked staging before it returns, so the scene it read is free for frame
-// k + D + 1's Update).  A frame's time is taken when its Update starts.
+// host side is pipelined too (ChainUpdater): `hs` is updated serially on a worker thread, one
+// Update history as in the reference's loop, and each frame's state is uploaded from a snapshot
+// (one of the D extra scenes) while the worker goes on with the next Updates (an upload copies the
+// host arrays into page-locked staging before it returns, so the snapshot is free again after it).
+// A frame's time is taken when its Update starts.
 // --device-update: the animated meshes' Update (transform + BVH rebuild + scene image) runs on
 // the device (rtx_anim_*); the host only computes the frame's transforms.
 // With `seq` (--sequence t1,t2,...): no timer; frame k is Update(seq[k]) and is written to
@@ -142,13 +157,9 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
                   const std::vector<float>* seq = nullptr, const std::string& stem = "",
                   const std::vector<rtx_host_scene*>& extra = {}) {
     const bool animated = rtx_host_scene_animated(hs) == 1;
-    // (pipelined host side) D = the host scenes besides the one being uploaded: frames k + 1 ..
-    // k + D are being updated, frame k + i on worker (k + i) % D into host scene (k + i) % (D + 1)
+    // (pipelined host side) D = the snapshot scenes: `hs` is the chain the worker updates, frame k is
+    // uploaded from snapshot extra[k % D]
     const int D = (animated && !device_update && inflight >= 2) ? static_cast<int>(extra.size()) : 0;
-    std::vector<rtx_host_scene*> hsv{hs};
-    hsv.insert(hsv.end(), extra.begin(), extra.end());
-    std::vector<std::unique_ptr<Updater>> upd;
-    for (int i = 0; i < D; ++i) upd.emplace_back(new Updater());
     const bool pipe = D > 0;
     const size_t npx = static_cast<size_t>(r.Width()) * r.Height();
     std::vector<rtx_ctx*> ctx{r.Context()};
@@ -173,6 +184,11 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
     const Clock::time_point start = Clock::now();
     const double cpu0 = cpu_secs();
     Clock::time_point prev = start;
+    std::unique_ptr<ChainUpdater> chain;
+    if (pipe)
+        chain.reset(new ChainUpdater(
+            hs, extra, [&](long k) { return seq ? (*seq)[k] : static_cast<float>(secs(start, Clock::now())); },
+            seq ? static_cast<long>(seq->size()) : -1));
     rtx_scene s;
     rtx_camera cam;
     auto ok = [&](int code, const char* what, rtx_ctx* c) {
@@ -243,16 +259,12 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
         const float tnow = seq ? (*seq)[queued] : static_cast<float>(secs(start, f0));
         rtx_host_scene* cur = hs;
         if (pipe) {
-            const long H = D + 1;
-            cur = hsv[queued % H];
-            auto launch = [&](long k) {   // frame k's Update, on its worker, into its host scene
-                if (!seq || k < static_cast<long>(seq->size()))
-                    upd[k % D]->start(hsv[k % H], seq ? (*seq)[k] : static_cast<float>(secs(start, Clock::now())));
-            };
-            if (queued == 0)
-                for (long k = 0; k < D; ++k) launch(k);
-            upd[queued % D]->wait();   // this frame's Update (started D frames ago)
-            launch(queued + D);
+            cur = chain->wait(queued);   // frame `queued`'s Update (the worker's chain), in its snapshot
+            if (!cur) {
+                std::fprintf(stderr, "rtx_host_scene_copy_state failed\n");
+                rc = 1;
+                break;
+            }
         } else if (anim) {
             rtx_host_scene_transforms(hs, tnow, mats.data(), static_cast<uint32_t>(n_anim));   // Update(t)'s turn
         } else if (animated) {
@@ -273,6 +285,7 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
         } else if ((animated || queued < inflight) && !ok(rtx_upload_scene(ctx[f], &s), "rtx_upload_scene", ctx[f])) {
             break;
         }
+        if (pipe) chain->release(queued);   // the upload copied the snapshot's arrays
         const Clock::time_point f2 = Clock::now();
         if (!ok(rtx_render_async(ctx[f], &cam, &p, 0), "rtx_render_async", ctx[f])) break;  // Renderer::Render
         if (!ok(rtx_gather_async(ctx[f], buf[f].data(), nullptr), "rtx_gather_async", ctx[f])) break;
@@ -283,7 +296,7 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
         ++queued;
     }
     for (int f = 0; f < inflight; ++f) rtx_synchronize(ctx[f]);
-    for (auto& u : upd) u->wait();   // (Updates started for frames the loop did not queue)
+    chain.reset();   // (stops the worker after its current Update)
     if (anim) {
         if (!anim_ok()) rc = 1;
         rtx_anim_destroy(anim);

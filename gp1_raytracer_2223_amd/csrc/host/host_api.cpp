@@ -59,6 +59,11 @@ extern "C" int rtx_host_scene_update(rtx_host_scene* s, float total_time) {
     return RTX_OK;
 }
 
+extern "C" int rtx_host_scene_copy_state(rtx_host_scene* dst, const rtx_host_scene* src) {
+    if (!dst || !src) return RTX_E_INVALID;
+    return dst->scene->CopyStateFrom(*src->scene) ? RTX_OK : RTX_E_INVALID;
+}
+
 extern "C" int rtx_host_scene_view(rtx_host_scene* s, rtx_scene* out_scene, rtx_camera* out_camera) {
     if (!s) return RTX_E_INVALID;
     rtx::Camera& cam = s->scene->GetCamera();

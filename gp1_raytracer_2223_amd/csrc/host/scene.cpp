@@ -787,6 +787,28 @@ rtx_scene Scene::View() {
     return s;
 }
 
+bool Scene::CopyStateFrom(const Scene& o) {
+    if (o.m_Meshes.size() != m_Meshes.size() || o.sceneName != sceneName) return false;
+    for (size_t i = 0; i < m_Meshes.size(); ++i) {
+        const TriangleMesh& a = *o.m_Meshes[i];
+        TriangleMesh& b = *m_Meshes[i];
+        if (a.positions.size() != b.positions.size() || a.indices.size() != b.indices.size()) return false;
+        b.normals = a.normals;
+        b.indices = a.indices;
+        b.rotationTransform = a.rotationTransform;
+        b.translationTransform = a.translationTransform;
+        b.scaleTransform = a.scaleTransform;
+        b.minAABB = a.minAABB;
+        b.maxAABB = a.maxAABB;
+        b.nodes = a.nodes;
+        b.nodesUsed = a.nodesUsed;
+        b.transformedPositions = a.transformedPositions;
+        b.transformedNormals = a.transformedNormals;
+    }
+    m_Camera = o.m_Camera;
+    return true;
+}
+
 float Scene::SpinYaw(float t) { return (cosf(t) + 1.f) / 2.f * kPi2; }   // Scene.cpp:394
 
 // ---------------------------------------------------------------- catalogue

@@ -143,6 +143,10 @@ public:
 
     // Flat C-ABI view pointing into this object's storage (valid until next Update).
     rtx_scene View();
+    // Copy the state an Update leaves (every mesh's transforms, world arrays, the BVH-permuted
+    // indices and normals, the node array) from `o`, a scene of the same kind: a snapshot of one
+    // Update history for a pipelined frame loop.  False when the meshes do not match.
+    bool CopyStateFrom(const Scene& o);
 
     std::vector<rtx_sphere> m_Spheres;
     std::vector<rtx_plane> m_Planes;

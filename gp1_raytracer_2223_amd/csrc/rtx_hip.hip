@@ -1723,8 +1723,8 @@ __device__ __forceinline__ uint32_t cost_class(uint32_t cst) {   // heavier -> s
 
 // A tile rendered split this frame has no fresh one-piece cost: it keeps the one it had
 // when it was last rendered whole (kept in `saved`) — or, with `parts` (motion mode: the camera
-// moves, so that cost goes stale), the sum of its split waves' durations, which lets a tile that
-// stopped being heavy leave the split set.
+// moves, so that cost goes stale), the sum of its split waves' durations for this frame's sort,
+// which lets a tile that stopped being heavy leave the split set (`saved` is left as it was).
 __global__ void __launch_bounds__(kReorderThreads) rtx_sched_count(uint32_t* __restrict__ cost, uint32_t n,
                                                                    const uint32_t* __restrict__ was_heavy,
                                                                    uint32_t* __restrict__ saved,
@@ -1742,9 +1742,15 @@ __global__ void __launch_bounds__(kReorderThreads) rtx_sched_count(uint32_t* __r
         const uint32_t t = base + k * kReorderThreads + tid;   // coalesced; counting ignores order
         if (t >= n) break;
         uint32_t c = cost[t];
-        if (was_heavy && was_heavy[t] && !parts) {
-            c = saved[t];
-            cost[t] = c;
+        if (was_heavy && was_heavy[t]) {
+            // split this frame: static frames sort it by the one-piece cost it had when last
+            // rendered whole; motion mode by its part waves' sum (cost[t]), which stands in for this
+            // frame only — the saved one-piece cost stays (a part sum leaves out each part wave's
+            // fixed work, so it would cost the tile low once motion ends)
+            if (!parts) {
+                c = saved[t];
+                cost[t] = c;
+            }
         } else {
             saved[t] = c;
         }
@@ -1925,6 +1931,7 @@ struct rtx_ctx {
     // frames, so the split launches only add work: the measured frames select heavy tiles with at
     // least kThroughputPermille and the tuner (whose timings the other frames distort) waits.
     hipEvent_t ev_frame = nullptr;
+    bool in_registry = false;                   // listed in g_frames (its ev_frame is recorded per frame)
     bool concurrent = false;
     bool throughput_off = false;                // RTX_THROUGHPUT=0
     int heavy_cur = 0;
@@ -1999,6 +2006,9 @@ struct rtx_ctx {
     std::string cull_worth_sig;
     CullBox* d_cull_btree = nullptr;      // 2n entries
     CullMD* d_cull_mtree = nullptr;       // 2n entries per anchor of one launch
+    size_t cull_mtree_cap = 0;            // entries d_cull_mtree holds
+    uint32_t cull_failures = 0;           // record builds that failed (the image then renders unculled)
+    uint32_t cull_fail_at = 0, cull_launches = 0;   // RTX_CULL_FAIL=k: the k-th record build fails (tests)
     CullBox* d_cull_nbox = nullptr;       // per node slot of the current image
     uint32_t* d_cull_arrive = nullptr;    // per tree (kCullMaxAnchors margin trees, then the box tree)
     size_t cull_tree_cap = 0, cull_nbox_cap = 0;   // leaves n the trees hold, slots nbox holds
@@ -2159,6 +2169,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     }
     if (const char* e = std::getenv("RTX_CULL_LEAVES")) c->cull_leaves = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_CULL_ANIMATED")) c->cull_animated = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RTX_CULL_FAIL")) c->cull_fail_at = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RTX_CULL_TOP_LDS"))
         c->cull_top_lds = std::min<uint32_t>(kCullTopLds, static_cast<uint32_t>(std::strtoul(e, nullptr, 10)));
     if (const char* e = std::getenv("RTX_CULL_MIN_SA")) {
@@ -2299,17 +2310,27 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay);
 int cull_launch(rtx_ctx* c, const CullAnchors& A, bool boxes) {
     const uint32_t nt = c->cull_ntris;
     const uint32_t n = c->cull_n;
-    if (n > c->cull_tree_cap || c->cull_nslots > c->cull_nbox_cap || !c->d_cull_arrive) {
+    if (c->cull_fail_at && ++c->cull_launches == c->cull_fail_at)   // RTX_CULL_FAIL (tests of the error path)
+        return fail(c, RTX_E_NOMEM, "cull records: injected failure (RTX_CULL_FAIL)");
+    // the anchors' margin trees: 2n entries per anchor of THIS launch (an upload's first launch has the
+    // lights and the views, later ones the views that moved), grown on demand
+    const size_t mtree_need = 2 * static_cast<size_t>(n) * std::max<uint32_t>(A.n, 1u);
+    if (n > c->cull_tree_cap || mtree_need > c->cull_mtree_cap || c->cull_nslots > c->cull_nbox_cap ||
+        !c->d_cull_arrive) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         if (n > c->cull_tree_cap) {
             (void)hipFree(c->d_cull_btree);
-            (void)hipFree(c->d_cull_mtree);
             c->d_cull_btree = nullptr;
-            c->d_cull_mtree = nullptr;
             c->cull_tree_cap = 0;
             HIP_TRY(c, hipMalloc(&c->d_cull_btree, 2 * static_cast<size_t>(n) * sizeof(CullBox)));
-            HIP_TRY(c, hipMalloc(&c->d_cull_mtree, 2 * static_cast<size_t>(n) * kCullMaxAnchors * sizeof(CullMD)));
             c->cull_tree_cap = n;
+        }
+        if (mtree_need > c->cull_mtree_cap) {
+            (void)hipFree(c->d_cull_mtree);
+            c->d_cull_mtree = nullptr;
+            c->cull_mtree_cap = 0;
+            HIP_TRY(c, hipMalloc(&c->d_cull_mtree, mtree_need * sizeof(CullMD)));
+            c->cull_mtree_cap = mtree_need;
         }
         if (c->cull_nslots > c->cull_nbox_cap) {
             (void)hipFree(c->d_cull_nbox);
@@ -2362,6 +2383,9 @@ void cull_records(rtx_ctx* c, const std::vector<float>& T, const rtx_light* ligh
 
 // Before a frame: after an upload the boxes and the lights' records, and the records of every view
 // whose camera origin is not the one its records of the current image were made for (bitwise).
+// The records' state (pending boxes, valid views) is committed only once their launches are queued:
+// when building them fails (an allocation), the image renders without the cull from then on — the
+// unculled walk, the same pixels — instead of a later frame trusting records never written.
 int cull_views(rtx_ctx* c, const FrameArgs& F) {
     CullAnchors A{};
     const bool boxes = c->cull_boxes_pending;
@@ -2373,11 +2397,11 @@ int cull_views(rtx_ctx* c, const FrameArgs& F) {
             ++A.n;
         }
     }
+    uint32_t valid = c->cull_view_valid;
     for (uint32_t v = 0; v < F.n_views && v < static_cast<uint32_t>(kMaxViews); ++v) {
         const float* o = F.cam[v].origin;
-        if ((c->cull_view_valid >> v) & 1u && std::memcmp(c->cull_view[v], o, 12) == 0) continue;
-        std::memcpy(c->cull_view[v], o, 12);
-        c->cull_view_valid |= 1u << v;
+        if ((valid >> v) & 1u && std::memcmp(c->cull_view[v], o, 12) == 0) continue;
+        valid |= 1u << v;
         for (int k = 0; k < 3; ++k) A.p[A.n][k] = o[k];
         A.p[A.n][3] = 0.f;
         A.bt[A.n] = F.cam[v].cull_bt;
@@ -2385,9 +2409,22 @@ int cull_views(rtx_ctx* c, const FrameArgs& F) {
         ++A.n;
     }
     if (A.n == 0 && !boxes) return RTX_OK;
+    if (cull_launch(c, A, boxes) != RTX_OK) {   // (c->err says why)
+        c->dev.cull = nullptr;
+        c->dev.cull_T = nullptr;
+        c->dev.cull_stride = 0;
+        c->cull_boxes_pending = false;
+        c->cull_view_valid = 0;
+        ++c->cull_failures;
+        (void)hipGetLastError();
+        return RTX_OK;
+    }
     if (A.n > (boxes ? c->cull_lights.size() : 0u)) ++c->cull_updates;
+    for (uint32_t j = 0; j < A.n; ++j)
+        if (A.idx[j] < static_cast<uint32_t>(kMaxViews)) std::memcpy(c->cull_view[A.idx[j]], A.p[j], 12);
+    c->cull_view_valid = valid;
     c->cull_boxes_pending = false;
-    return cull_launch(c, A, boxes);
+    return RTX_OK;
 }
 }  // namespace
 
@@ -3242,8 +3279,20 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         c->heavy_pending = true;
         c->sched_ready = true;
     }
-    HIP_TRY(c, hipEventRecord(c->ev_frame, c->stream));   // the frame's end, for other contexts' prepare
-    frames_note(c);
+    // the frame's end, for other contexts' throughput mode (prepare).  Only a context whose tiles can
+    // be split records it: one that has nothing to split (no frontier, or no heavy tile at a converged
+    // factor: W4_Bunny) skips the event and the registry's lock on every frame.
+    const bool tracked = c->split_ok && c->split_mode != 0 && !(c->heavy_n == 0 && c->tune_done);
+    if (tracked) {
+        HIP_TRY(c, hipEventRecord(c->ev_frame, c->stream));
+        if (!c->in_registry) {
+            frames_note(c);
+            c->in_registry = true;
+        }
+    } else if (c->in_registry) {
+        frames_forget(c);
+        c->in_registry = false;
+    }
     return RTX_OK;
 }
 

@@ -49,6 +49,12 @@ class HostScene:
         abi.check(self._lib.rtx_host_scene_update(self._h, float(total_time)), "rtx_host_scene_update")
         self.generation += 1
 
+    def copy_state(self, src: "HostScene") -> None:
+        """The state src's Updates left (rtx_host_scene_copy_state): a snapshot of ONE Update
+        history, as the pipelined frame loop uploads them."""
+        abi.check(self._lib.rtx_host_scene_copy_state(self._h, src._h), "rtx_host_scene_copy_state")
+        self.generation += 1
+
     @property
     def animated(self) -> bool:
         """Update(t) moves geometry (re-upload after it)."""

@@ -29,6 +29,13 @@ void rtx_host_scene_destroy(rtx_host_scene* s);
 /* Scene_W4_*::Update minus the SDL camera input: yaw = (cos t + 1)/2 * 2pi on every
  * animated mesh, transforms + BVH rebuilt (source/Scene.cpp:391-400, 431-437, 468-474). */
 int rtx_host_scene_update(rtx_host_scene* s, float total_time);
+/* Copy the state Update(t) leaves in `src` (meshes' transforms, world positions and normals, the
+ * BVH-permuted indices and normals, the node array; the camera) into `dst`, a host scene created
+ * with the same name.  The reference's BuildBVH permutes the triangles in place
+ * (DataTypes.h:335-363), so a scene's state depends on its whole Update history: a pipelined
+ * frame loop updates ONE scene serially and uploads snapshots of it.  RTX_E_INVALID when the
+ * scenes differ. */
+int rtx_host_scene_copy_state(rtx_host_scene* dst, const rtx_host_scene* src);
 /* Flat view (pointers into the scene; valid until the next update/destroy) and the
  * camera after CalculateCameraToWorld(). */
 int rtx_host_scene_view(rtx_host_scene* s, rtx_scene* out_scene, rtx_camera* out_camera);

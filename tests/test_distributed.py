@@ -159,7 +159,8 @@ def test_bench_one_gpu_contract(tmp_path):
     sample): one JSON line with the contract's fields; `value` = pixels / ms_per_step; the roofline
     object; the CPU baseline and `speedup_vs_cpu` against its best configuration; every extra
     workload with its parity and the one-GPU strong-scaling predictor (efficiency = t_full / (s x the
-    slowest share)); the culled Synthetic100k line marks its FLOP basis as reference-equivalent."""
+    slowest share)); the culled lines' `frac` counts the work the culled walk executes, the
+    reference-equivalent rate beside it."""
     import json
     import subprocess
     import sys
@@ -192,7 +193,9 @@ def test_bench_one_gpu_contract(tmp_path):
             assert abs(x["efficiency"] - sp["t_full_ms"] / (s * max(x["share_ms"]))) < 1e-3
     assert "flop_basis" in scenes["Synthetic100k"]["roofline_rank0"]
     assert "flop_basis" not in scenes["Bunny8Lights"]["roofline_rank0"]
-    for name in ("Synthetic100k", "W4_Optional"):   # the culled scenes: executed-work roofline too
+    for name in ("Synthetic100k", "W4_Optional"):   # the culled scenes: `frac` is executed work
         rr = scenes[name]["roofline_rank0"]
-        assert 0 < rr["frac_executed"] < rr["frac"], (name, rr)
-        assert abs(rr["frac_executed"] - rr["achieved_executed"] / rr["peak"]) < 1e-3
+        assert rr["flop_basis"].startswith("executed"), (name, rr)
+        assert 0 < rr["frac"] < rr["frac_reference_equivalent"], (name, rr)
+        assert abs(rr["frac"] - rr["achieved"] / rr["peak"]) < 1e-3
+        assert abs(rr["frac_reference_equivalent"] - rr["achieved_reference_equivalent"] / rr["peak"]) < 1e-3

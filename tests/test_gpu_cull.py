@@ -538,7 +538,7 @@ def _counts(ctx, s, cam, p, culled):
 
 @pytest.mark.parametrize("name", ["Synthetic100k", "W4_Optional", "W4_Bunny"])
 def test_executed_work_counts(product_ctx, name):
-    """The culled walk's counting variant (bench.py's roofline.frac_executed): every counter
+    """The culled walk's counting variant (bench.py's roofline.frac on the culled lines): every counter
     outside the BVH walk equals the reference traversal's count (same rays, hits, shadows,
     shading), the culled walk tests at most the reference's triangles, and for Synthetic100k it
     executes a small fraction of the reference's slab and triangle tests (the CPU cost model,

@@ -91,3 +91,36 @@ def test_nan_mesh_takes_direct_builder(tmp_path):
                             json.dumps([1, 3])], capture_output=True, text=True, env=env, check=True)
         out[builder] = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["fast"] == out["direct"]
+
+
+@pytest.mark.parametrize("scene", ["W4_Bunny", "W4_Optional"])
+def test_pipelined_loop_keeps_one_update_history(scene):
+    """The CLI's pipelined frame loop (csrc/cli/rtx_render.cpp, ChainUpdater) updates ONE scene
+    serially and uploads snapshots of it (rtx_host_scene_copy_state).  Every snapshot equals a
+    scene updated serially through the same times — indices, normals and nodes included, which the
+    in-place BVH permutation makes depend on the whole history.  Handing the Updates round robin to
+    several scenes (round 5's loop) does not: a scene that skipped an Update keeps another triangle
+    order."""
+    from gp1_raytracer_2223_amd.scene import HostScene
+    times = [0.3, 0.9, 1.7, 2.2]
+    serial, chain = HostScene(scene), HostScene(scene)
+    snaps = [HostScene(scene), HostScene(scene)]
+    for k, t in enumerate(times):
+        serial.update(t)
+        chain.update(t)
+        snap = snaps[k % 2]
+        snap.copy_state(chain)
+        assert [_digest(m) for m in snap.arrays()["meshes"]] == [_digest(m) for m in serial.arrays()["meshes"]], k
+    # round robin over two scenes: the second one never sees Update 0.3
+    skipped = HostScene(scene)
+    for t in times[1::2]:
+        skipped.update(t)
+    a, b = serial.arrays()["meshes"][0], skipped.arrays()["meshes"][0]
+    assert np.array_equal(a["tpositions"], b["tpositions"])
+    assert not np.array_equal(a["indices"], b["indices"])
+
+
+def test_copy_state_refuses_another_scene():
+    from gp1_raytracer_2223_amd.scene import HostScene
+    with pytest.raises(Exception):
+        HostScene("W4_Bunny").copy_state(HostScene("W4_Optional"))
