@@ -58,7 +58,7 @@ def build_hip(force: bool = False) -> Path:
     LIB.mkdir(exist_ok=True)
     out = LIB / "librtx_hip.so"
     srcs = [CSRC / "rtx_hip.hip", CSRC / "rtx_anim.hip", CSRC / "rtx_group.cpp"]
-    deps = srcs + list(CSRC.glob("*.h")) + [INC / "rtx.h", Path(__file__)]   # flags live here
+    deps = srcs + list(CSRC.glob("*.h")) + [INC / "rtx.h", INC / "rtx_diag.h", Path(__file__)]   # flags live here
     if force or _stale(out, deps):
         # -fno-slp-vectorize: the SLP packer turns independent f32 ops into v_pk_* plus
         # v_mov shuffles; measured 8 % slower on the render kernel (profiles/r01/ablate_*.txt).
@@ -77,11 +77,23 @@ def build_cli(force: bool = False) -> Path:
     """Headless C++ host program over both libraries (lib/rtx_render)."""
     out = LIB / "rtx_render"
     src = CSRC / "cli" / "rtx_render.cpp"
-    deps = [src, INC / "rtx_renderer.hpp", INC / "rtx.h", INC / "rtx_host.h", LIB / "librtx_hip.so",
+    deps = [src, CSRC / "cli" / "benchmark.h", INC / "rtx_renderer.hpp", INC / "rtx.h", INC / "rtx_host.h", LIB / "librtx_hip.so",
             LIB / "librtx_host.so"]
     if force or _stale(out, deps):
         _run(["g++", "-std=c++17", "-O2", "-Wall", f"-I{INC}", src, "-o", out, f"-L{LIB}", "-lrtx_hip", "-lrtx_host",
               "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"])
+    return out
+
+
+def build_view(force: bool = False) -> Path:
+    """The SDL viewer (lib/rtx_view): SDL2 is dlopen'ed at run time, nothing links against it."""
+    out = LIB / "rtx_view"
+    src = CSRC / "cli" / "rtx_view.cpp"
+    deps = [src, CSRC / "cli" / "benchmark.h", INC / "rtx.h", INC / "rtx_host.h", INC / "rtx_view.h",
+            LIB / "librtx_hip.so", LIB / "librtx_host.so"]
+    if force or _stale(out, deps):
+        _run(["g++", "-std=c++17", "-O2", "-Wall", f"-I{INC}", src, "-o", out, f"-L{LIB}", "-lrtx_hip", "-lrtx_host",
+              "-ldl", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"])
     return out
 
 
@@ -129,6 +141,7 @@ def build_all(force: bool = False) -> None:
     build_hip(force)
     build_reference(force)   # after librtx_hip.so: oracle/_ref/ref_binding links it
     build_cli(force)
+    build_view(force)
 
 
 if __name__ == "__main__":

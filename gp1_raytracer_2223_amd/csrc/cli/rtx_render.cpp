@@ -31,6 +31,7 @@
 
 #include <sys/resource.h>
 
+#include "benchmark.h"
 #include "rtx_renderer.hpp"
 
 namespace {
@@ -42,33 +43,6 @@ double cpu_secs() {   // the process's CPU time, every thread (user + system)
     getrusage(RUSAGE_SELF, &u);
     return double(u.ru_utime.tv_sec + u.ru_stime.tv_sec) + 1e-6 * double(u.ru_utime.tv_usec + u.ru_stime.tv_usec);
 }
-
-// Timer::StartBenchmark / Update FPS logic (Timer.cpp:44-131), same float arithmetic.
-struct Benchmark {
-    int frames;
-    std::vector<float> dfps;
-    float high = FLT_MIN, low = FLT_MAX, avg = 0.f;   // m_BenchmarkHigh = FLT_MIN as in the reference
-    float fps_timer = 0.f;
-    int fps_count = 0;
-    explicit Benchmark(int n) : frames(n) {}
-    bool Tick(float elapsed) {   // returns true when the last window closed
-        fps_timer += elapsed;
-        ++fps_count;
-        if (fps_timer >= 1.0f) {
-            const float d = fps_count / fps_timer;
-            fps_count = 0;
-            fps_timer = 0.f;
-            dfps.push_back(d);
-            low = std::min(low, d);
-            high = std::max(high, d);
-            if (static_cast<int>(dfps.size()) >= frames) {
-                avg = std::accumulate(dfps.begin(), dfps.end(), 0.f) / float(frames);
-                return true;
-            }
-        }
-        return false;
-    }
-};
 
 // The pipelined host side of run_benchmark.  The reference's BuildBVH permutes the triangles in
 // place (DataTypes.h:335-363), so the state Update k leaves depends on every earlier Update: ONE
@@ -176,7 +150,7 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
     std::vector<char> upd_ok(inflight, 1);   // --sequence: the device Update of the frame in buf[f] succeeded
     for (int f = 0; f < inflight; ++f) rtx_host_register(ctx[f], buf[f].data(), npx * 4);   // async D2H
     const rtx_render_params p = r.Params();
-    Benchmark b(windows);
+    rtx::Benchmark b(windows);
     if (!seq) std::cout << "**BENCHMARK STARTED**\n";
     double t_update = 0, t_upload = 0, t_queue = 0, t_wait = 0;
     long frames = 0, queued = 0;
@@ -305,15 +279,7 @@ int run_benchmark(rtx::Renderer& r, rtx_host_scene* hs, int windows, int infligh
     for (int f = 0; f < inflight; ++f) rtx_host_unregister(ctx[f], buf[f].data());
     for (size_t i = 1; i < ctx.size(); ++i) rtx_destroy(ctx[i]);
     if (rc || seq) return rc;
-    std::cout << "**BENCHMARK FINISHED**\n";
-    std::cout << ">> HIGH = " << b.high << std::endl;
-    std::cout << ">> LOW = " << b.low << std::endl;
-    std::cout << ">> AVG = " << b.avg << std::endl;
-    std::ofstream out("benchmark.txt");
-    out << "FRAMES = " << b.dfps.size() << std::endl;
-    out << "HIGH = " << b.high << std::endl;
-    out << "LOW = " << b.low << std::endl;
-    out << "AVG = " << b.avg << std::endl;
+    rtx::WriteBenchmark(b);
     const double n = static_cast<double>(queued);
     // host CPU use of the loop: process CPU time (the build pool's spinning workers included) over
     // wall time, in cores

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "rtx.h"
+#include "rtx_diag.h"
 #include "rtx_anim.h"
 #include "rtx_cull.h"
 #include "rtx_fastdiv.h"
@@ -858,6 +859,11 @@ __device__ __forceinline__ uint32_t q8(float c) {
 //                                          atomicOr of the light's occlusion bit
 //   PHASE 3  grid (heavy):                 hit record from the key, spheres/planes
 //                                          occlusion + the bits, shading, output
+// A light-major frame (FrameArgs::lm_*, small launches: a stripe share) replaces PHASE 0 by
+//   PHASE 4  grid (tiles):                 PHASE 0 up to the hit record, which it writes
+//   PHASE 5  persistent waves over the (tile, light) items: that light's shadow ray from the
+//                                          record -> the occluded lanes; the tile's last light wave
+//                                          shades every light in order (the occlusion published)
 // Every phase recomputes the primary ray and the sphere/plane hits with the same code, so
 // all of them see bit-identical values.
 // DEEP: the variant for scenes whose BVH is kStackDepth or more levels deep (a DFS stack of
@@ -875,12 +881,18 @@ __device__ __forceinline__ uint32_t q8(float c) {
 // W4_Optional's variant 231 -> 223 us.  The variant with spheres and meshes stays at 7 (8: +4 %).
 // CULLK: the variant with the exact cull (DevScene::cull; launched only for scenes that have the
 // records — the code of the cull paths costs the kernel without them registers and 8 %).
-template <bool COUNT, int PHASE, bool DEEP = false, int SPEC = 0, bool HSTK = false, bool CULLK = false>
-__global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
-                                                  : ((SPEC & (kSpecOneMesh | kSpecNoMesh))
-                                                         ? RTX_SPEC_WAVES
-                                                         : (SPEC ? RTX_SPEC_WAVES_PARTIAL : RTX_MIN_WAVES_PER_EU)))
-    rtx_render_kernel(const DevScene S, const FrameArgs F) {
+#define f_mode (kComb ? RTX_MODE_COMBINED : F.mode)
+#define f_shadows (kComb ? 1 : F.shadows)
+#define n_sph (kNoSph ? 0u : S.n_spheres)
+#define n_pl (kP5 ? 5u : S.n_planes)          // constant trip counts: the plane and mesh loops unroll
+#define n_mesh (kNoMesh ? 0u : (kOneMesh ? 1u : S.n_meshes))
+// One wave tile of one phase (rtx_render_kernel below dispatches the tiles and describes the phases): `widx` = the
+// wave's index in the launch (PHASE 5: its item), `stk` / `sT` its DFS stacks, `pnum` its shadow-ray
+// plane numerators in LDS.
+template <bool COUNT, int PHASE, bool DEEP, int SPEC, bool HSTK, bool CULLK>
+__device__ __forceinline__ void render_tile(const DevScene& S, const FrameArgs& F, uint32_t widx, uint32_t tile,
+                                            uint32_t part, uint32_t light, uint4* stk, unsigned long long* sT,
+                                            float (*pnum)[64], uint32_t lane) {
     constexpr int kKinds = SPEC & kSpecKindAll;
     constexpr bool kPoint = (SPEC & kSpecPoint) != 0;
     constexpr bool kNoSph = (SPEC & kSpecNoSpheres) != 0, kComb = (SPEC & kSpecCombShadows) != 0;
@@ -888,49 +900,11 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
     constexpr bool kNoMesh = (SPEC & kSpecNoMesh) != 0;
     constexpr bool kRoom = (SPEC & kSpecRoomPlanes) != 0 && (SPEC & kSpecFivePlanes) != 0;
     constexpr bool kCullBack = (SPEC & kSpecCullBack) != 0 && !COUNT;
-#define f_mode (kComb ? RTX_MODE_COMBINED : F.mode)
-#define f_shadows (kComb ? 1 : F.shadows)
-#define n_sph (kNoSph ? 0u : S.n_spheres)
-#define n_pl (kP5 ? 5u : S.n_planes)          // constant trip counts: the plane and mesh loops unroll
-#define n_mesh (kNoMesh ? 0u : (kOneMesh ? 1u : S.n_meshes))
-    constexpr int kDepth = HSTK ? 1 : (DEEP ? kStackDepthDeep : kStackDepth);
-    __shared__ uint4 stkE[kBlockThreads / 64][kDepth];
-    __shared__ unsigned long long stkT[(COUNT && !HSTK) ? kBlockThreads / 64 : 1][(COUNT && !HSTK) ? kDepth : 1];
-    // per-lane shadow-ray plane numerators, shared by every light (see the light loop)
-    __shared__ float pnumS[kBlockThreads / 64][kPlaneCache][64];
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
 #if RTX_STAMPS
     // diagnostic build only: per-wave {start, end, hw_id} in the counters buffer
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_prim = t_start, t_shadow = 0;   // primary hit done; shadow mesh walks
 #endif
-    uint4* stk = stkE[wave];
-    unsigned long long* sT = stkT[COUNT ? wave : 0];
-
-    // Work unit = one 8x8 wave tile of one view; the waves of a workgroup (one by default,
-    // RTX_BLOCK_THREADS) are independent (no barrier) and take consecutive entries of the
-    // dispatch order.  The order is a permutation (F.order, null = identity) that
-    // rtx_reorder_kernel derives from the previous frame's measured per-tile cost: heavy
-    // tiles start first and do not form a tail.  One-wave workgroups free their slot the
-    // moment the wave ends (4-wave ones held it until the slowest sibling ended: Bunny
-    // -3 %, Synthetic100k -9 %).  Which wave renders a tile never changes a pixel's value.
-    const uint32_t b = blockIdx.x;
-    uint32_t widx = b * kWavesPerBlock + wave;   // wave index in the launch
-    uint32_t tile, part = 0, light = 0;
-    if (PHASE == 0) {
-        if (widx >= F.n_tiles) return;
-        tile = F.order ? ldc(F.order, widx) : widx;
-        if (F.heavy_flag && ldc(F.heavy_flag, tile)) return;   // rendered by the split launches
-    } else {
-        // grid (heavy tiles / waves per block, parts, lights), tile fastest: every heavy tile's part 0 is
-        // dispatched first, the big top-of-tree parts before the small ones.  (Pinning a
-        // part to one XCD for L2 locality was measured slower: the heavy parts then load a
-        // few XCDs only.)
-        if (widx >= F.heavy_n) return;
-        part = blockIdx.y;
-        light = blockIdx.z;
-        tile = ldc(F.heavy_list, widx);
-    }
     if constexpr (HSTK) {   // this wave's stacks in HBM
         stk = S.hstk + static_cast<size_t>(widx) * S.hstk_depth;
         if (COUNT) sT = S.hstkT + static_cast<size_t>(widx) * S.hstk_depth;
@@ -976,11 +950,11 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
     // FAST: every active lane's inverse direction finite and non-zero (make_ray's domain)
     const bool fast = (active & vslow) == 0 && S.tri_fast;
     // octant of the wave's primary rays (-1: mixed signs, or no octant copies)
-    const int poct = (fast && S.oct_bytes && PHASE == 0) ? batch_octant(vr, active) : -1;
+    const int poct = (fast && S.oct_bytes && (PHASE == 0 || PHASE == 4)) ? batch_octant(vr, active) : -1;
     // exact cull of the view's camera anchor (FAST waves; a direction normalised from a magnitude
     // of at least 2^-30 has |d| = 1 +- 3u, which the bound assumes)
     constexpr bool kCull = CULLK && !RTX_STAMPS_WALK;   // (with COUNT: rtx_count_work_culled)
-    const bool pcull = kCull && S.cull_stride && fast && (PHASE == 0 || PHASE == 1);
+    const bool pcull = kCull && S.cull_stride && fast && (PHASE == 0 || PHASE == 1 || PHASE == 4);
     CullRay pq{};
     if (pcull)
         pq = cull_ray(S.cull + static_cast<size_t>(uni(view)) * (S.cull_stride / 16u), vr, dm >= 0x1p-30f,
@@ -990,7 +964,8 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
     float best_t = FLT_MAX, sc_t = FLT_MAX;
     // kind: 0 none, 1 sphere, 2 plane, 3 triangle; best_idx: the record's BYTE offset
     uint32_t best_kind = 0, best_idx = 0;
-    for (uint32_t i = 0; i < n_sph * 16u; i += 16u) {
+    // (PHASE 5 reads the hit record PHASE 4 wrote: no closest-hit work)
+    for (uint32_t i = 0; i < ((PHASE == 5 || PHASE == 6) ? 0u : n_sph * 16u); i += 16u) {
         const float4 s = ldcb16(S.spheres, opaque(i));
         if (COUNT && valid) cnt.c[kSphere]++;
         const SphereProj q = sphere_perp(s, vr);
@@ -1008,7 +983,8 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
     // numerators come from the host (ViewCam::room_a); in a FAST wave every d is inside div_rn's
     // divisor domain with its RN(1/d) already in the ray, so when the host found the numerators
     // inside theirs too, t = RN(a / d) costs 3 VALU instead of the 11 of IEEE `/`.
-    const bool room_p = kRoom && !RTX_ABL_PPLANE && (active & ~ballot(finite3(vr.ox, vr.oy, vr.oz))) == 0;
+    const bool room_p =
+        kRoom && PHASE != 5 && PHASE != 6 && !RTX_ABL_PPLANE && (active & ~ballot(finite3(vr.ox, vr.oy, vr.oz))) == 0;
     if (room_p) {
         // the view's record through a readfirstlane'd index: scalar loads (the view index
         // itself stays a VGPR value; making it uniform everywhere measured slower)
@@ -1033,7 +1009,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
             best_idx = b ? static_cast<uint32_t>(k * 32) : best_idx;
         });
     }
-    for (uint32_t i = 0; i < ((RTX_ABL_PPLANE || room_p) ? 0u : n_pl * 32u); i += 32u) {
+    for (uint32_t i = 0; i < ((RTX_ABL_PPLANE || room_p || PHASE == 5 || PHASE == 6) ? 0u : n_pl * 32u); i += 32u) {
         float4 p0, p1;
         ldcb32(S.planes, opaque(i), p0, p1);
         if (COUNT && valid) cnt.c[kPlane]++;
@@ -1046,7 +1022,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         best_kind = b ? 2u : best_kind;
         best_idx = b ? i : best_idx;
     }
-    if (PHASE == 0) {
+    if (PHASE == 0 || PHASE == 4) {
         for (uint32_t mi = 0; mi < ((RTX_ABL_PMESH) ? 0u : n_mesh); ++mi) {
             const int4 M = ldcb16i(S.meshes, opaque(mi * 16u));
             uint32_t sc_tri = 0;
@@ -1111,7 +1087,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         if (timed && lane == 0 && wdt) part_cost_add(F.cost + tile, wdt);
         RTX_SPLIT_STAMP();
         return;
-    } else {
+    } else if (PHASE == 2 || PHASE == 3) {
         // the minimum over the parts; strict < against the sphere/plane winner, as after
         // every mesh in Scene::GetClosestHit (Scene.cpp:56-63)
         const unsigned long long key = F.hit_key[slot];
@@ -1120,10 +1096,16 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
     }
 
     // ---- hit record (rebuilt from t: ray.origin + t * ray.direction, Utils.h:62-64)
-    const bool did = best_kind != 0;
+    bool did = best_kind != 0;
     float hx = 0.f, hy = 0.f, hz = 0.f, nx = 0.f, ny = 0.f, nz = 0.f;
     uint32_t mat = 0;
-    if (did) {
+    const size_t lm_slot = 2 * (static_cast<size_t>(tile) * 64u + lane);   // (PHASE 4/5) the pixel's record
+    if (PHASE == 5 || PHASE == 6) {   // PHASE 4's record of this pixel (the previous launch: visible)
+        const float4 r0 = F.lm_rec[lm_slot], r1 = F.lm_rec[lm_slot + 1];
+        hx = r0.x; hy = r0.y; hz = r0.z; nx = r0.w; ny = r1.x; nz = r1.y;
+        mat = __float_as_uint(r1.z);
+        did = __float_as_uint(r1.w) != 0u;
+    } else if (did) {
         hx = vr.ox + vr.dx * best_t; hy = vr.oy + vr.dy * best_t; hz = vr.oz + vr.dz * best_t;
         if (best_kind == 1) {
             const float4 s = ldcb16(S.spheres, best_idx);
@@ -1144,18 +1126,31 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         }
     }
     if (COUNT && did) cnt.c[kHit]++;
+    if (PHASE == 4) {   // light-major: the record for PHASE 5, and this wave's share of the tile's cost
+        F.lm_rec[lm_slot] = make_float4(hx, hy, hz, nx);
+        F.lm_rec[lm_slot + 1] = make_float4(ny, nz, __uint_as_float(mat), __uint_as_float(did ? 1u : 0u));
+        if (F.cost && lane == 0) part_cost_add(F.cost + tile, __builtin_amdgcn_s_memtime() - t_block0);
+        return;
+    }
 
     float shadowFactor = 1.f;
     float fr = 0.f, fg = 0.f, fb = 0.f;
     const unsigned long long hitmask = ballot(did);
+    unsigned long long lm_occ = 0;   // PHASE 5: the lanes whose shadow ray toward `light` is occluded
+    // The reference's light loop (Renderer.cpp:128-176).  Light-major frames run it in two launches:
+    // PHASE 5 casts its one light's shadow ray and only records the occluded lanes; PHASE 6 (lm_shade)
+    // runs it over every light with each light's occlusion the one PHASE 5 published
+    // (FrameArgs::lm_mask), no shadow ray cast.
+    constexpr bool lm_shade = PHASE == 6;
     if (hitmask) {
+        const uint32_t l_first = (PHASE == 2 || PHASE == 5) ? light : 0u;
+        const uint32_t l_end = (PHASE == 2 || PHASE == 5) ? light + 1 : (RTX_ABL_LIGHTS ? 0u : S.n_lights);
         // originOffset = hit.origin + hit.normal * 0.0001f (Renderer.cpp:126)
         const float oox = hx + nx * 0.0001f, ooy = hy + ny * 0.0001f, ooz = hz + nz * 0.0001f;
         const float vx = -dx, vy = -dy, vz = -dz;
         // shadow rays start at originOffset for every light: one finiteness test for all of them
         const bool room_s =
             kRoom && PHASE != 2 && !RTX_ABL_SPLANE && (hitmask & ~ballot(finite3(oox, ooy, ooz))) == 0;
-        const uint32_t l_first = PHASE == 2 ? light : 0u, l_end = PHASE == 2 ? light + 1 : (RTX_ABL_LIGHTS ? 0u : S.n_lights);
         for (uint32_t li = l_first; li < l_end; ++li) {
             float4 L0, L1;
             ldcb32(S.lights, opaque(li * 32u), L0, L1);
@@ -1165,7 +1160,10 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
             const float mag = sqrtf(lx * lx + ly * ly + lz * lz);
             div3_exact(lx, ly, lz, mag);
             bool occ = false;
-            if (f_shadows) {
+            if (lm_shade && f_shadows) {   // PHASE 6: published by the previous launch
+                const unsigned long long mk = F.lm_mask[static_cast<size_t>(tile) * F.lm_lights + li];
+                occ = did && ((mk >> lane) & 1ull);
+            } else if (f_shadows) {
                 // Scene::DoesHit (Scene.cpp:68-96) on Ray{originOffset, l, 1e-4, |l|}; `live` =
                 // lanes still without an occluder (first hit wins, order irrelevant for a bool)
                 unsigned long long sslow;
@@ -1173,10 +1171,10 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                 unsigned long long live = hitmask;
                 const bool sfast = (hitmask & sslow) == 0 && S.tri_fast;
                 const int soct =
-                    (sfast && S.oct_bytes && PHASE == 0 && n_mesh) ? batch_octant(sr, hitmask) : -1;
+                    (sfast && S.oct_bytes && (PHASE == 0 || PHASE == 5) && n_mesh) ? batch_octant(sr, hitmask) : -1;
                 // exact cull of the light's anchor: lanes with mag <= cull_T[li] (and a direction
                 // normalised from at least 2^-30)
-                const bool scull = kCull && S.cull_stride && sfast && (PHASE == 0 || PHASE == 2) && n_mesh;
+                const bool scull = kCull && S.cull_stride && sfast && (PHASE == 0 || PHASE == 2 || PHASE == 5) && n_mesh;
                 CullRay sq{};
                 if (scull)
                     sq = cull_ray(S.cull + static_cast<size_t>(kMaxViews + li) * (S.cull_stride / 16u), sr,
@@ -1215,7 +1213,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                     for (uint32_t i = 0; i < np; i += 32u) {
                         float4 p0, p1;
                         ldcb32(S.planes, opaque(i), p0, p1);
-                        const float num = pnumS[wave][i >> 5][lane];
+                        const float num = pnum[i >> 5][lane];
                         const float den = plane_den(p1, sr);
                         const unsigned long long cand = plane_cand(num, den, sr.tmax) & live;
                         if (!cand) continue;
@@ -1228,7 +1226,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                         ldcb32(S.planes, opaque(i), p0, p1);
                         if (COUNT && ((live >> lane) & 1ull)) cnt.c[kPlane]++;
                         const float num = plane_num(p0, p1, sr), den = plane_den(p1, sr);
-                        if (cache_ok) pnumS[wave][i >> 5][lane] = num;
+                        if (cache_ok) pnum[i >> 5][lane] = num;
                         const unsigned long long cand = plane_cand(num, den, sr.tmax) & live;
                         if (!cand) continue;   // also taken once no lane is live
                         const float t = num / den;
@@ -1238,7 +1236,7 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
 #if RTX_STAMPS
                 const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
 #endif
-                for (uint32_t mi = 0; mi < ((RTX_ABL_SMESH || PHASE != 0) ? 0u : n_mesh); ++mi) {
+                for (uint32_t mi = 0; mi < ((RTX_ABL_SMESH || !(PHASE == 0 || PHASE == 5)) ? 0u : n_mesh); ++mi) {
                     if (!live) break;
                     float st = 0.f;
                     uint32_t stri = 0;
@@ -1293,6 +1291,10 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                 occ = did & !((live >> lane) & 1ull);
                 if (PHASE == 3) occ = occ || (did && ((F.occ_bits[slot] >> li) & 1u));
             }
+            if (PHASE == 5) {
+                lm_occ = ballot(occ);
+                continue;
+            }
             if (!did) continue;
             if (occ) {
                 if (COUNT) cnt.c[kOccluded]++;
@@ -1328,7 +1330,12 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
                 fr += br.r; fg += br.g; fb += br.b;
             }
         }
-        if (did) { fr *= shadowFactor; fg *= shadowFactor; fb *= shadowFactor; }
+        if (did && PHASE != 5) { fr *= shadowFactor; fg *= shadowFactor; fb *= shadowFactor; }
+    }
+    if (PHASE == 5) {   // the light's occluded lanes for PHASE 6
+        if (lane == 0) F.lm_mask[static_cast<size_t>(tile) * F.lm_lights + light] = lm_occ;
+        if (F.cost && lane == 0) part_cost_add(F.cost + tile, __builtin_amdgcn_s_memtime() - t_block0);
+        return;
     }
     if (PHASE == 2) {
         RTX_SPLIT_STAMP();
@@ -1353,6 +1360,9 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         const unsigned long long dt = (__builtin_amdgcn_s_memtime() - t_block0) >> 4;
         atomicMax(&F.cost[tile], static_cast<uint32_t>(dt < 0xffffffffull ? dt : 0xffffffffull));
     }
+    // light-major: the tile's cost is the sum of its waves' (PHASE 4 + every light wave)
+    if ((PHASE == 5 || PHASE == 6) && F.cost && lane == 0)
+        part_cost_add(F.cost + tile, __builtin_amdgcn_s_memtime() - t_block0);
 #if RTX_STAMPS
     if (PHASE == 0 && lane == 0 && F.stamps) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
@@ -1376,6 +1386,64 @@ __global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
         for (int k = 0; k < kNumCounters; ++k)
             if (cnt.c[k]) atomicAdd(&F.counters[k], static_cast<unsigned long long>(cnt.c[k]));
     }
+}
+
+
+template <bool COUNT, int PHASE, bool DEEP = false, int SPEC = 0, bool HSTK = false, bool CULLK = false>
+__global__ void __launch_bounds__(kBlockThreads, (DEEP && !HSTK) ? 2
+                                                  : ((SPEC & (kSpecOneMesh | kSpecNoMesh))
+                                                         ? RTX_SPEC_WAVES
+                                                         : (SPEC ? RTX_SPEC_WAVES_PARTIAL : RTX_MIN_WAVES_PER_EU)))
+    rtx_render_kernel(const DevScene S, const FrameArgs F) {
+    constexpr int kDepth = HSTK ? 1 : (DEEP ? kStackDepthDeep : kStackDepth);
+    __shared__ uint4 stkE[kBlockThreads / 64][kDepth];
+    __shared__ unsigned long long stkT[(COUNT && !HSTK) ? kBlockThreads / 64 : 1][(COUNT && !HSTK) ? kDepth : 1];
+    // per-lane shadow-ray plane numerators, shared by every light (see the light loop)
+    __shared__ float pnumS[kBlockThreads / 64][kPlaneCache][64];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint4* stk = stkE[wave];
+    unsigned long long* sT = stkT[COUNT ? wave : 0];
+
+    // Work unit = one 8x8 wave tile of one view; the waves of a workgroup (one by default,
+    // RTX_BLOCK_THREADS) are independent (no barrier) and take consecutive entries of the
+    // dispatch order.  The order is a permutation (F.order, null = identity) that
+    // rtx_reorder_kernel derives from the previous frame's measured per-tile cost: heavy
+    // tiles start first and do not form a tail.  One-wave workgroups free their slot the
+    // moment the wave ends (4-wave ones held it until the slowest sibling ended: Bunny
+    // -3 %, Synthetic100k -9 %).  Which wave renders a tile never changes a pixel's value.
+    const uint32_t b = blockIdx.x;
+    uint32_t widx = b * kWavesPerBlock + wave;   // wave index in the launch
+    uint32_t tile, part = 0, light = 0;
+    // PHASE 4/5: the light-major frame (FrameArgs::lm_*): PHASE 4 = PHASE 0 up to the hit record,
+    // PHASE 5 = item (tile, light), the tiles in dispatch order and a tile's lights consecutive
+    if (PHASE == 0 || PHASE == 4 || PHASE == 6) {
+        if (widx >= F.n_tiles) return;
+        tile = F.order ? ldc(F.order, widx) : widx;
+        if (F.heavy_flag && ldc(F.heavy_flag, tile)) return;   // rendered by the split launches
+    } else if (PHASE == 5) {
+        // persistent waves, one per resident wave slot: wave w takes items w, w + NW, w + 2 NW, ... of the
+        // cost-ordered list, so every wave gets a share of the heavy items and no per-item workgroup is
+        // dispatched (130k one-wave workgroups at 4K / 8 ranks cost more to launch than to run)
+        const uint32_t L = F.lm_lights, items = F.n_tiles * L, nw = gridDim.x * kWavesPerBlock;
+        for (uint32_t it = uni(widx); it < items; it += nw) {   // (wave-uniform: the light indexes scalar loads)
+            const uint32_t k = it / L;
+            tile = F.order ? ldc(F.order, k) : k;
+            if (F.heavy_flag && ldc(F.heavy_flag, tile)) continue;
+            render_tile<COUNT, PHASE, DEEP, SPEC, HSTK, CULLK>(S, F, it, tile, 0u, it - k * L, stk, sT, pnumS[wave],
+                                                               lane);
+        }
+        return;
+    } else {
+        // grid (heavy tiles / waves per block, parts, lights), tile fastest: every heavy tile's part 0 is
+        // dispatched first, the big top-of-tree parts before the small ones.  (Pinning a
+        // part to one XCD for L2 locality was measured slower: the heavy parts then load a
+        // few XCDs only.)
+        if (widx >= F.heavy_n) return;
+        part = blockIdx.y;
+        light = blockIdx.z;
+        tile = ldc(F.heavy_list, widx);
+    }
+    render_tile<COUNT, PHASE, DEEP, SPEC, HSTK, CULLK>(S, F, widx, tile, part, light, stk, sT, pnumS[wave], lane);
 }
 
 #undef f_mode
@@ -1768,6 +1836,7 @@ __global__ void __launch_bounds__(kReorderThreads) rtx_sched_count(uint32_t* __r
 __global__ void __launch_bounds__(kScanThreads) rtx_sched_scan(uint32_t* __restrict__ hist, uint32_t nchunks,
                                                                const unsigned long long* __restrict__ csum, uint32_t n,
                                                                uint32_t split_slots, uint32_t split_permille,
+                                                               uint32_t split_min,
                                                                unsigned long long* __restrict__ thr_out,
                                                                uint32_t* __restrict__ heavy_n) {
     __shared__ uint32_t part[kScanThreads];
@@ -1800,9 +1869,10 @@ __global__ void __launch_bounds__(kScanThreads) rtx_sched_scan(uint32_t* __restr
     if (tid == 0) {
         const unsigned long long total = cpart[kScanThreads - 1];
         const bool force = split_slots == 0xffffffffu;
-        *thr_out = force ? 0ull
-                         : (split_slots ? total * split_permille / (1000ull * (n < split_slots ? n : split_slots))
-                                        : ~0ull);
+        // (split_min: no tile below it is split, whatever its share of the frame)
+        const unsigned long long thr =
+            split_slots ? total * split_permille / (1000ull * (n < split_slots ? n : split_slots)) : ~0ull;
+        *thr_out = force ? 0ull : (thr > split_min ? thr : static_cast<unsigned long long>(split_min));
         *heavy_n = 0;
     }
 }
@@ -1940,6 +2010,7 @@ struct rtx_ctx {
     uint32_t split_mode = 1;         // 0 off, 1 auto, 2 force (RTX_SPLIT=0 / unset / force)
     uint32_t split_slots = 0;        // concurrent render waves on this device
     uint32_t split_permille = kSplitPermille;   // RTX_SPLIT_FACTOR (fixes it: no tuner)
+    uint32_t split_min = kSplitMinCost;         // RTX_SPLIT_MIN_US: the least cost (16-cycle units) a split tile has
     // Split-threshold tuner: the frame is max(main kernel, split chain), and the
     // threshold that balances the two is the fastest (Synthetic100k: factor 2.0, W4_Optional 1.5).
     // A measured frame with split tiles times both (ev_tune: fork, main kernel end, chain end); at
@@ -1977,6 +2048,16 @@ struct rtx_ctx {
     bool no_spec = false;            // RTX_NO_SPEC=1: always the generic kernel (tests)
     unsigned long long* d_hit_key = nullptr;
     uint32_t* d_occ = nullptr;
+    // Light-major frames (FrameArgs::lm_*, DESIGN.md §6, opt-in): lm_mode 0 never (default), 1 auto
+    // (RTX_LIGHT_MAJOR=auto: a launch of at most lm_tiles wave tiles, kLmSlotsPercent of the resident
+    // wave slots, RTX_LIGHT_MAJOR_TILES), 2 always (RTX_LIGHT_MAJOR=1)
+    uint32_t lm_mode = 0;
+    uint32_t lm_tiles = 0;
+    uint32_t lm_waves = 0;                      // PHASE 5's persistent waves: every resident slot (32 per CU)
+    float4* d_lm_rec = nullptr;                 // 2 float4 per tile pixel
+    unsigned long long* d_lm_mask = nullptr;    // per (tile, light)
+    size_t lm_rec_tiles = 0, lm_mask_cap = 0;
+    bool frame_lm = false;                      // the frame being launched is light-major
     // exact cull (DevScene::cull): on for host uploads (RTX_NO_CULL=1: off); the
     // scratch of its record launches (the segment trees of the per-triangle boxes and of each
     // anchor's margins, the slots' boxes, the trees' arrival counters) and the node-slot ranges
@@ -2176,6 +2257,9 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
         const double v = std::atof(e);
         if (v >= 0.0 && v < 1e30) c->cull_min_sa = v;
     }
+    if (const char* e = std::getenv("RTX_LIGHT_MAJOR"))
+        c->lm_mode = std::strcmp(e, "1") == 0 ? 2u : (std::strcmp(e, "auto") == 0 ? 1u : 0u);
+    if (const char* e = std::getenv("RTX_LIGHT_MAJOR_TILES")) c->lm_tiles = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RTX_SPLIT")) c->split_mode = std::strcmp(e, "0") == 0 ? 0u : (std::strcmp(e, "force") == 0 ? 2u : 1u);
     if (const char* e = std::getenv("RTX_SPLIT_PARTS")) {
         const int v = std::atoi(e);
@@ -2186,6 +2270,10 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
         if (f > 0 && f < 1e6) { c->split_permille = static_cast<uint32_t>(f * 1000.0); c->tune_on = false; }
     }
     if (const char* e = std::getenv("RTX_SPLIT_TUNE")) c->tune_on = c->tune_on && std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RTX_SPLIT_MIN_US")) {
+        const double us = std::atof(e);
+        if (us >= 0 && us < 1e6) c->split_min = static_cast<uint32_t>(us * kSplitMinCost / kSplitMinUs);
+    }
     const size_t heavy_px = static_cast<size_t>(kMaxHeavyTiles) * 64;   // pixels of the heavy wave tiles
     int cus = 0, lo_prio = 0, hi_prio = 0;
 #define RTX_CREATE_TRY(call)                                                             \
@@ -2227,6 +2315,8 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
 #undef RTX_CREATE_TRY
     // waves resident at once: 7 per SIMD, 4 SIMDs per CU at the render kernel's occupancy
     c->split_slots = static_cast<uint32_t>(cus > 0 ? cus : 1) * 28u;
+    if (!std::getenv("RTX_LIGHT_MAJOR_TILES")) c->lm_tiles = c->split_slots * kLmSlotsPercent / 100u;
+    c->lm_waves = static_cast<uint32_t>(cus > 0 ? cus : 1) * 32u;
     *out = c;
     return RTX_OK;
 }
@@ -2256,6 +2346,8 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     if (c->h_heavy_n) (void)hipHostFree(c->h_heavy_n);
     (void)hipFree(c->d_hit_key);
     (void)hipFree(c->d_occ);
+    (void)hipFree(c->d_lm_rec);
+    (void)hipFree(c->d_lm_mask);
     (void)hipFree(c->d_hstk);
     (void)hipFree(c->d_hstkT);
     (void)hipFree(c->d_cull_btree);
@@ -3109,6 +3201,33 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     F.heavy_n = split ? c->heavy_n : 0u;
     F.hit_key = c->d_hit_key;
     F.occ_bits = c->d_occ;
+    // light-major (FrameArgs::lm_*): a launch small enough that its slowest tiles, not its work, set
+    // its time (a few tiles per resident wave slot: a stripe share of a frame), with shadows and 2+
+    // lights; the deep-stack variants render one piece
+    const uint32_t nl = c->dev.n_lights;
+    c->frame_lm = F.shadows && nl >= 2 && nl <= kMaxLmLights && !c->deep_stack && !c->hbm_stack &&
+                  (c->lm_mode == 2 || (c->lm_mode == 1 && ntiles <= c->lm_tiles));
+    if (c->frame_lm) {
+        if (ntiles > c->lm_rec_tiles) {
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            (void)hipFree(c->d_lm_rec);
+            c->d_lm_rec = nullptr;
+            c->lm_rec_tiles = 0;
+            HIP_TRY(c, hipMalloc(&c->d_lm_rec, static_cast<size_t>(ntiles) * 64 * 2 * sizeof(float4)));
+            c->lm_rec_tiles = ntiles;
+        }
+        if (static_cast<size_t>(ntiles) * nl > c->lm_mask_cap) {
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            (void)hipFree(c->d_lm_mask);
+            c->d_lm_mask = nullptr;
+            c->lm_mask_cap = 0;
+            HIP_TRY(c, hipMalloc(&c->d_lm_mask, static_cast<size_t>(ntiles) * nl * 8));
+            c->lm_mask_cap = static_cast<size_t>(ntiles) * nl;
+        }
+        F.lm_lights = nl;
+        F.lm_rec = c->d_lm_rec;
+        F.lm_mask = c->d_lm_mask;
+    }
     // Measure tile costs on the first frame of a shape and then every kSchedPeriod frames;
     // the frames in between reuse the last order and pay nothing for scheduling.
     // while the split threshold is being tuned (a scene with split tiles), every other frame is measured
@@ -3249,7 +3368,15 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, true, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
     else if (c->deep_stack)
         hipLaunchKernelGGL((rtx_render_kernel<false, 0, true>), grid, dim3(kBlockThreads), 0, c->stream, c->dev, F);
-    else if (!(RTX_ABL_MAIN && F.heavy_flag && !F.cost))
+    else if (F.lm_lights) {   // light-major: hit records, then the (tile, light) waves
+        launch_phase<4>(v, grid, c->stream, c->dev, F);
+        HIP_TRY(c, hipGetLastError());
+        // persistent light waves: one per resident wave slot (at most one per item)
+        const uint32_t items = F.n_tiles * F.lm_lights, waves = std::min(items, c->lm_waves);
+        launch_phase<5>(v, dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock), c->stream, c->dev, F);
+        HIP_TRY(c, hipGetLastError());
+        launch_phase<6>(v, grid, c->stream, c->dev, F);
+    } else if (!(RTX_ABL_MAIN && F.heavy_flag && !F.cost))
         launch_phase<0>(v, grid, c->stream, c->dev, F);
     HIP_TRY(c, hipGetLastError());
     if (F.heavy_flag && c->tune_rec && F.cost) HIP_TRY(c, hipEventRecord(c->ev_tune[1], c->stream));
@@ -3268,7 +3395,7 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         HIP_TRY(c, hipGetLastError());
         hipLaunchKernelGGL(rtx_sched_scan, dim3(1), dim3(kScanThreads), 0, c->stream, c->d_hist, nch,
                            c->d_csum,
-                           F.n_tiles, slots, permille, c->d_thr, c->d_heavy_n);
+                           F.n_tiles, slots, permille, c->split_min, c->d_thr, c->d_heavy_n);
         HIP_TRY(c, hipGetLastError());
         hipLaunchKernelGGL(rtx_sched_scatter, dim3(nch), dim3(kReorderThreads), 0, c->stream, F.cost, c->d_order,
                            F.n_tiles, c->d_hist, nch, c->d_thr, slots == 0xffffffffu ? 1u : 0u,
@@ -3541,6 +3668,13 @@ extern "C" int rtx_split_tune_info(rtx_ctx* c, float* factor, float* main_ms, fl
     if (main_ms) *main_ms = c->tune_main_ms;
     if (chain_ms) *chain_ms = c->tune_chain_ms;
     if (done) *done = (!c->tune_on ? 2u : (c->tune_done ? 1u : 0u));
+    return RTX_OK;
+}
+
+extern "C" int rtx_light_major_info(rtx_ctx* c, uint32_t* last_frame, uint32_t* max_tiles) {
+    if (!c) return RTX_E_INVALID;
+    if (last_frame) *last_frame = c->frame_lm ? 1u : 0u;
+    if (max_tiles) *max_tiles = c->lm_mode == 0 ? 0u : (c->lm_mode == 2 ? 0xffffffffu : c->lm_tiles);
     return RTX_OK;
 }
 

@@ -41,6 +41,14 @@ constexpr uint32_t kThroughputPermille = 2600;
 // noise of 2.0; below 1.25 the split overhead outgrows the tail it removes
 constexpr int kSplitPermille = 1500;
 constexpr int kMaxSplitLights = 32;    // occlusion bits per pixel
+// A tile is split only if its cost is also at least kSplitMinUs (in the cost unit, 16 shader cycles at
+// 2.4 GHz): a launch with fewer tiles than wave slots (a stripe share) starts every tile at once, and
+// there a tile of a few tens of us finishes sooner in one piece than behind the split chain's three
+// dependent launches.  Floor sweep (profiles/r06/split_min_sweep.txt, serialized ms, floors 0 / 30 / 60 /
+// 100 us): W4_Bunny 1080p share of 8 ranks 0.067 / 0.071 / 0.052 / 0.052, Bunny + 8 lights 4K share of 8
+// 0.098 / 0.100 / 0.100 / 0.110, W4_Optional and Synthetic100k (full frames and shares) within 2 %.
+constexpr uint32_t kSplitMinUs = 60;
+constexpr uint32_t kSplitMinCost = kSplitMinUs * 2400 / 16;
 // Kernel specialisation (rtx_render_kernel's SPEC): uniform facts compiled in.
 // Bits 0-3: the material kinds the geometry references (bit RTX_MAT_*; none set = any kind).
 constexpr int kSpecKindSolid = 1 << 0;
@@ -194,6 +202,20 @@ struct FrameArgs {
     uint32_t heavy_n;                           // entries of heavy_list in use
     unsigned long long* __restrict__ hit_key;   // per heavy pixel: min {t bits, triangle}
     uint32_t* __restrict__ occ_bits;            // per heavy pixel: bit l = mesh occludes light l
+    // Light-major frame (small shares): PHASE 4 writes each pixel's hit record, PHASE 5
+    // runs one (tile, light) shadow ray per wave (items in cost order, the light fastest), publishes
+    // the occluded lanes and the tile's last light wave shades every light in the reference's order.
+    uint32_t lm_lights;                         // lights per tile (PHASE 5 items = n_tiles x lm_lights)
+    float4* __restrict__ lm_rec;                // per tile pixel: {h, n.x}, {n.y, n.z, mat bits, did}
+    unsigned long long* __restrict__ lm_mask;   // per (tile, light): the lanes whose shadow ray is occluded
+    uint32_t* __restrict__ lm_arrive;           // per tile: light waves done (0 between frames)
 };
+
+// Light-major frames (opt-in: RTX_LIGHT_MAJOR=1 always, =auto while a launch has at most kLmSlotsPercent /
+// 100 wave tiles per resident wave slot, RTX_LIGHT_MAJOR_TILES overrides; default never: each (tile, light)
+// item repeats ~200 instructions of set-up for ~200 of shadow walk, measured 1.5x slower than one piece
+// at 4K / 8 ranks, profiles/r06), with shadows on and 2..kMaxLmLights lights.
+constexpr uint32_t kLmSlotsPercent = 250;
+constexpr uint32_t kMaxLmLights = 32;
 
 }  // namespace rtxd

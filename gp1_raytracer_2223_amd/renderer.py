@@ -102,6 +102,12 @@ class DeviceContext:
         return {"factor": round(f.value, 4), "main_ms": round(m.value, 5), "chain_ms": round(ch.value, 5),
                 "state": ["tuning", "converged", "off"][d.value]}
 
+    def light_major_info(self) -> tuple[bool, int]:
+        """(the last prepared frame was light-major, the largest light-major launch in wave tiles)."""
+        a, b = C.c_uint32(), C.c_uint32()
+        abi.check(self.lib.rtx_light_major_info(self.h, C.byref(a), C.byref(b)), "rtx_light_major_info", self.h)
+        return bool(a.value), int(b.value)
+
     def cull_info(self) -> tuple[bool, int]:
         """(the uploaded scene renders with the exact cull, camera-record rebuilds so far)."""
         on, n = C.c_uint32(), C.c_uint64()

@@ -24,6 +24,11 @@
  *
  * Threading: like Renderer::Render (called only from the main thread), one caller
  * thread per rtx_ctx.  Different contexts (one per GPU) may be driven concurrently.
+ *
+ * This header is the product boundary: contexts, scene upload, rendering, the host gather, one frame
+ * over several GPUs (rtx_group_*) and the device-side Update (rtx_anim_*).  Timing, work counters
+ * and the scheduler's / exact cull's internals are in rtx_diag.h; the environment knobs the library
+ * reads are listed in INTEGRATION.md (none of them changes a pixel).
  */
 #ifndef RTX_H_
 #define RTX_H_
@@ -35,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 1
+#define RTX_ABI_VERSION 2
 
 enum {
     RTX_OK = 0,
@@ -215,66 +220,6 @@ int rtx_host_register(rtx_ctx* ctx, void* ptr, size_t bytes);
 int rtx_host_unregister(rtx_ctx* ctx, void* ptr);
 /* Device pointers of the HBM frame buffer (width*height uint32 / 3*width*height f32). */
 int rtx_device_buffers(rtx_ctx* ctx, void** d_pixels, void** d_rgb);
-/* Time `iters` back-to-back launches of the render kernel(s) with HIP events recorded
- * on the context stream; writes the mean per-frame device time in ms. */
-int rtx_time_frames(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
-                    int iters, float* mean_ms);
-int rtx_time_views(rtx_ctx* ctx, const rtx_camera* cams, int n_views, const rtx_render_params* params,
-                   int iters, float* mean_ms);
-/* Bytes of HBM the uploaded scene image occupies. */
-int rtx_scene_bytes(const rtx_ctx* ctx, uint64_t* bytes);
-/* Diagnostics: copy the context's current scene image (DESIGN.md §2 layout) after its queued
- * work; `bytes` gets the image size (out may be NULL to query it). */
-int rtx_scene_image(rtx_ctx* ctx, void* out, size_t capacity, size_t* bytes);
-/* Instrumented render: the same traversal with per-ray work counters (12 x uint64, in
- * the order pixels, sphere, plane, slab, tri, hit, shadow, occluded, shade_base,
- * shade_lambert, shade_phong, shade_ct — the SURVEY §8(d) FLOP model).  Not timed. */
-int rtx_count_work(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
-                   uint64_t* counts12);
-/* Same, plus diagnostics appended after the 12 model counters: [12] node-pair tests and
- * [13] triangle tests executed per WAVE (packet work, one count per wave per step). */
-int rtx_count_work_ex(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
-                      uint64_t* counts, int n_counts);
-/* The same counters for the walk the product executes when the scene has exact-cull records
- * (otherwise identical to rtx_count_work_ex): slab [3] and triangle [4] tests the
- * culled, ordered walk performs per lane (a lane in a node's mask is tested against both
- * children), [12]/[13] per-wave steps, and [14] the exact-cull box tests.  One-piece frame (the
- * split launches' extra path tests not included).  Not timed. */
-int rtx_count_work_culled(rtx_ctx* ctx, const rtx_camera* cam, const rtx_render_params* params,
-                          uint64_t* counts, int n_counts);
-/* Split rendering of heavy tiles (no reference counterpart: a scheduling detail of this
- * path).  Tiles whose measured cost exceeds their share of the frame are re-rendered with
- * their BVH traversals cut into `parts` subtree pieces run by separate workgroups; the
- * pixels are identical either way.  Reports the heavy-tile count the next frame will use
- * and the frontier size of the uploaded scene (0 = the scene is rendered unsplit).
- * Environment: RTX_SPLIT=0 disables, RTX_SPLIT=force splits every tile (tests). */
-int rtx_split_info(rtx_ctx* ctx, uint32_t* heavy_tiles, uint32_t* parts);
-/* The split threshold's tuner: the current factor (a tile is split when its cost
- * exceeds factor x its share of the frame), the last timed frame's main kernel and split chain
- * (ms, from the fork), and the tuner's state (0 tuning, 1 converged, 2 off: RTX_SPLIT_TUNE=0 or a
- * fixed RTX_SPLIT_FACTOR).  Re-tuned for every new launch shape. */
-int rtx_split_tune_info(rtx_ctx* ctx, float* factor, float* main_ms, float* chain_ms, uint32_t* done);
-/* Exact cull (no reference counterpart: a pruning of the reference's own BVH walk that never
- * changes a pixel).  Reports whether the uploaded scene renders with it (on for
- * host uploads whose reference boxes are inflated enough to pay, see upload_scene) and how
- * many times a camera's records were (re)built.  Environment: RTX_NO_CULL=1 disables;
- * RTX_CULL_MIN_SA, RTX_CULL_RATIO tune the enabling test and the per-node flag (tests). */
-int rtx_cull_info(rtx_ctx* ctx, uint32_t* enabled, uint64_t* camera_updates);
-/* Diagnostics of the exact cull (tests): waits for the context stream, then copies the current
- * image's records of record copy `anchor` (view v < 8: its camera; 8 + l: light l) — n_slots x
- * 8 floats, {c, E.x}, {E.y, E.z, dt, flag bits} — and their inputs: per slot the triangle range
- * [first, end) (2 x u32), node copy 0 (8 floats per slot), the triangle records (16 floats
- * each: {v0, n.x}, {E1, n.y}, {E2, n.z}, {mat}), and the anchor the copy was last built for
- * (x, y, z, w = 0 camera / tmax bound of a light, bt).  Null pointers are skipped; sizes via
- * *n_slots / *n_tris.  RTX_E_INVALID when the scene has no records. */
-int rtx_cull_dump(rtx_ctx* ctx, uint32_t anchor, uint32_t* n_slots, uint32_t* n_tris, float* anchor_p,
-                  float* records, uint32_t* ranges, float* nodes, float* tris);
-/* Diagnostics of the cost-ordered dispatch (tests): after a measured frame, the dispatch
- * permutation of the first n tiles' slots (`order`) and the one-piece tile costs it was
- * sorted by (`cost`).  *n_tiles = tiles of the current schedule (0 = none measured yet;
- * then nothing is copied). */
-int rtx_schedule_state(rtx_ctx* ctx, uint32_t* order, uint32_t* cost, uint32_t n, uint32_t* n_tiles);
-
 /* ---- one frame over several GPUs from one process ------------------
  * The reference's Renderer::Render covers the frame with parallel_for
  * (source/Renderer.cpp:79-85); a group covers it with G render contexts instead.  Rows are
@@ -335,10 +280,6 @@ int rtx_anim_update(rtx_anim* anim, rtx_ctx* ctx, const float* transforms);
  * rendered from it are invalid), deepest level, nodesUsed, frontier parts}; returns
  * RTX_E_UNSUPPORTED when error bits are set. */
 int rtx_anim_status(rtx_anim* anim, uint32_t i, uint32_t status[4]);
-/* Diagnostics: 128 status words of the last update of registered mesh i (0-3 as above,
- * 4-6 subtrees / task-split ids / nodes split as tasks, 8-27 phase stamps of the device build
- * at 100 MHz; csrc/rtx_anim.h). */
-int rtx_anim_stamps(rtx_anim* anim, uint32_t i, uint32_t out[128]);
 /* Waits for the last update and copies registered mesh i's state in the reference's own
  * form: transformedPositions (3V), indices (3T), normals (object space, 3T),
  * transformedNormals (3T), the node array pBVHNodes (3T entries).  NULL skips a part. */

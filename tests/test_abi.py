@@ -68,7 +68,7 @@ def _declared(header: Path) -> list[str]:
 
 def test_hip_library_exports_every_declared_symbol():
     lib = abi.load_hip()   # loads without a GPU; no compute call is made here
-    names = _declared(INC / "rtx.h")
+    names = _declared(INC / "rtx.h") + _declared(INC / "rtx_diag.h")
     assert len(names) >= 14
     for n in names:
         assert hasattr(lib, n), n
@@ -77,8 +77,22 @@ def test_hip_library_exports_every_declared_symbol():
 
 def test_host_library_exports_every_declared_symbol():
     lib = abi.load_host()
-    for n in _declared(INC / "rtx_host.h"):
+    for n in _declared(INC / "rtx_host.h") + _declared(INC / "rtx_view.h"):
         assert hasattr(lib, n), n
+
+
+def test_product_header_has_no_diagnostics():
+    """rtx.h is the product boundary (render, group, device Update, gather); timing, counters and the
+    scheduler's internals live in rtx_diag.h."""
+    prod = set(_declared(INC / "rtx.h"))
+    diag = set(_declared(INC / "rtx_diag.h"))
+    assert not prod & diag
+    for n in ("rtx_time_views", "rtx_count_work", "rtx_split_info", "rtx_cull_dump", "rtx_schedule_state",
+              "rtx_anim_stamps", "rtx_light_major_info"):
+        assert n in diag and n not in prod, n
+    for n in ("rtx_create", "rtx_upload_scene", "rtx_render", "rtx_last_error", "rtx_destroy", "rtx_gather_async",
+              "rtx_group_render", "rtx_anim_update"):
+        assert n in prod, n
 
 
 def test_product_does_not_link_oracle():
@@ -89,7 +103,7 @@ def test_product_does_not_link_oracle():
 
 
 def test_abi_version():
-    assert abi.load_hip().rtx_abi_version() == 1
+    assert abi.load_hip().rtx_abi_version() == 2   # 2: diagnostics moved to rtx_diag.h (same symbols)
 
 
 def test_create_reports_why_it_failed():

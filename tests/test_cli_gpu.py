@@ -83,3 +83,24 @@ def test_pipelined_frame_loop_matches_oracle(tmp_path, scene, inflight, exact, d
             assert np.array_equal(got, ref), f"frame {k}: {int((got != ref).sum())} pixels differ"
         else:   # powf (Phong) is the device libm's: the north star's 1-LSB bound
             assert int(np.abs(_channels(got) - _channels(ref)).max()) <= 1, f"frame {k}"
+
+
+def test_viewer_keys_headless(tmp_path):
+    """The viewer's frame loop (lib/rtx_view, csrc/cli/rtx_view.cpp) with a scripted key sequence and no
+    window: F3 F3 (Combined -> ObservedArea -> Radiance), F2 (shadows off), X (screenshot of that
+    frame), F6 (benchmark started), then one more frame.  Each frame's state is printed, and the
+    screenshot is the oracle's frame in the state the keys left (main.cpp:63-107)."""
+    view = ROOT / "gp1_raytracer_2223_amd" / "lib" / "rtx_view"
+    if not view.exists():
+        pytest.skip("rtx_view not built")
+    W, H = 160, 120
+    r = subprocess.run([str(view), "W3", str(W), str(H), "--keys", "F3,F3,F2,X,F6", "--out", "shot.bmp"], check=True,
+                       cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    states = re.findall(r"frame (\d+): mode (\d) shadows (\d)", r.stdout)
+    assert states == [("0", "0", "1"), ("1", "1", "1"), ("2", "1", "0"), ("3", "1", "0"), ("4", "1", "0"),
+                      ("5", "1", "0")], r.stdout
+    assert "Screenshot saved!" in r.stdout and "**BENCHMARK STARTED**" in r.stdout
+    hs = HostScene("W3")
+    s, cam = hs.view()
+    ref, _ = oracle_bind.render(s, cam, abi.make_params(W, H, mode=1, shadows=False))   # Radiance: no powf
+    assert np.array_equal(_bmp_pixels(tmp_path / "shot.bmp", W, H), ref)

@@ -596,3 +596,30 @@ def test_cull_records_across_uploads(top):
                 assert bad.size == 0, f"upload {k} ({name}@{t}) anchor {j}: {bad.size} records differ, slot {bad[0]}"
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("fail_at", ["1", "2"])
+def test_failed_record_build_renders_unculled(plain_ctx, fail_at):
+    """A record build that fails (RTX_CULL_FAIL=k injects the k-th build's failure: an allocation in a
+    real run) turns the cull off for the image before any frame can read records that were never
+    written: that frame and every later one render the reference's full traversal.
+    k = 1: the upload's build (boxes, lights, camera); k = 2: a camera move's rebuild."""
+    ctx = _ctx_env(RTX_CULL_FAIL=fail_at, RTX_CULL_ANIMATED="1")
+    try:
+        hs = HostScene("Synthetic100k")
+        s, cam = hs.view()
+        p = abi.make_params(320, 180)
+        ctx.upload(s)
+        plain_ctx.upload(s)
+        assert ctx.cull_info()[0]
+        frames = []
+        for k in range(4):
+            c2 = abi.Camera()
+            C.memmove(C.byref(c2), C.byref(cam), C.sizeof(abi.Camera))
+            c2.origin[0] = cam.origin[0] + (0.05 if k >= 2 else 0.0)   # frame 3: a camera move
+            frames.append((c2, ctx.render(c2, p)))
+        assert not ctx.cull_info()[0], "the failed build must turn the cull off for the image"
+        for k, (c2, g) in enumerate(frames):
+            _same(g, plain_ctx.render(c2, p), f"frame {k} after an injected failure at build {fail_at}")
+    finally:
+        ctx.close()

@@ -81,8 +81,11 @@ def test_vector_loads_only_for_per_lane_gathers(isa):
 
 
 def test_registers_and_scratch(isa):
+    """No scratch anywhere.  The specialised kernels (every BASELINE config's but W1's) keep >= 7 waves
+    per SIMD (<= 72 VGPRs; the one-mesh ones ask for 8); the generic kernel (SPEC = 0: scenes matching
+    no variant, W1 / W2 / W3_Test) is built for >= 6 (RTX_MIN_WAVES_PER_EU, <= 80)."""
     for name, _, meta in _product(isa):
         assert meta.get("private_segment_fixed_size") == 0, (name, meta)
-        assert meta.get("vgpr_count", 999) <= 72, (name, meta)
+        assert meta.get("vgpr_count", 999) <= (72 if _spec(name) else 80), (name, meta)
     deep = [(n, m) for n, (_, m) in isa.items() if n.startswith(DEEP)]
     assert deep and all(m.get("private_segment_fixed_size") == 0 for _, m in deep), deep
