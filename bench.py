@@ -16,9 +16,9 @@ The JSON line has four parts:
    every rank renders one frame's worth of pixels per step: weak scaling.  At N = 1 a step is
    exactly one reference Renderer::Render frame.  `--mode frame` tiles ONE frame per step over
    the N ranks (strong scaling).
-2. `multi_gpu_configs`, at every N (N = 1 anchors the curve): the north star's multi-GPU
-   workloads, Synthetic100k 1920x1080 and Bunny + 8 lights 3840x2160, each as ONE image per
-   step tiled in 16-row stripes over the N ranks (the reference's one-frame parallel_for,
+2. `multi_gpu_configs`, at every N (N = 1 anchors the curve): the headline scene and the north
+   star's multi-GPU workloads, W4_Bunny and Synthetic100k 1920x1080 and Bunny + 8 lights 3840x2160
+   (+ W4_Optional), each as ONE image per step tiled in 16-row stripes over the N ranks (the reference's one-frame parallel_for,
    Renderer.cpp:79-85) — Mpix/s device-resident and gathered into the page-locked host frame,
    each rank's HBM traffic from the PMC record of this build, and the gathered frame's parity.
 3. `parity_configs` (N = 1): every BASELINE config, plus W4_Reference and W4_Optional, rendered
@@ -92,7 +92,9 @@ K_KERNEL_LAUNCHES = 1000   # launches averaged for the headline's roofline.kerne
 # BASELINE.json's multi-GPU workloads: one image per step, tiled over the ranks (steps per run)
 # (+ W4_Optional: with Synthetic100k a scene the exact cull runs on; on those two lines the roofline
 # counts the work the culled walk executes, the reference-equivalent rate beside it)
-MULTI_GPU_CONFIGS = [("Synthetic100k", 1920, 1080, 100), ("Bunny8Lights", 3840, 2160, 300),
+# W4_Bunny 1080p first: the headline scene as ONE frame per step over the N ranks (strong scaling), the
+# curve beside `value`'s weak-scaling one in the driver's N = 1, 2, 4, 8 runs
+MULTI_GPU_CONFIGS = [("W4_Bunny", 1920, 1080, 300), ("Synthetic100k", 1920, 1080, 100), ("Bunny8Lights", 3840, 2160, 300),
                      ("W4_Optional", 1920, 1080, 300)]
 # parity_configs: (scene, W, H, bit-exact required).  Cook-Torrance / Phong use powf, where the
 # device libm may differ from glibc by an ulp: those are held to the north star's tolerance.
@@ -548,12 +550,16 @@ def wl_ref_counts(wl: "Workload") -> list:
     return [int(x) for x in wl.ctxs[0].count_work(wl.views[0], pv)]
 
 
-def stripe_predictor(ctx: DeviceContext, wl: "Workload", lib_hash: str, steps=(2, 4, 8), launches: int = 30) -> dict:
+def stripe_predictor(ctxs, wl: "Workload", lib_hash: str, steps=(2, 4, 8), launches: int = 30) -> dict:
     """One-GPU predictor of strong scaling (N = 1 only): the frame cut into 16-row stripes dealt
     over s ranks, each rank's share timed alone on this GPU (serialized launches, HIP events,
     after a warm-up that builds the share's cost order).  The step time at s GPUs is the slowest
     share's, so efficiency(s) = t_full / (s * max_r t_share(r)); `rank0` uses rank 0's share only.
-    What it leaves out: the host gather and the ranks' clocks (one GPU times every share)."""
+    `inflight`: the same with the rank's frames in flight as the N-GPU bench runs them (--inflight:
+    the rank's contexts alternating frames, wall time per frame over 200 frames after 40), the full
+    frame likewise.  What it leaves out: the host gather and the ranks' clocks (one GPU times every
+    share)."""
+    ctx = ctxs[0]
     lib = ctx.lib
     cam = wl.views
 
@@ -566,17 +572,38 @@ def stripe_predictor(ctx: DeviceContext, wl: "Workload", lib_hash: str, steps=(2
             best = ms.value if best is None else min(best, ms.value)
         return best
 
+    def t_inflight(p, frames=200, warm=40):
+        for i in range(warm):
+            abi.check(lib.rtx_render_views_async(ctxs[i % len(ctxs)].h, cam, 1, C.byref(p), 0), "render", ctx.h)
+        for c in ctxs:
+            c.synchronize()
+        t0 = time.perf_counter()
+        for i in range(frames):
+            abi.check(lib.rtx_render_views_async(ctxs[i % len(ctxs)].h, cam, 1, C.byref(p), 0), "render", ctx.h)
+        for c in ctxs:
+            c.synchronize()
+        return (time.perf_counter() - t0) / frames * 1e3
+
     t_full = t(abi.make_params(wl.W, wl.H))
+    t_full_if = t_inflight(abi.make_params(wl.W, wl.H))
     out = {"method": f"each share timed alone (rtx_time_views, best of 2 x {launches} launches after 5 warm-up "
-                     "launches); efficiency = t_full / (s * slowest share)", "t_full_ms": round(t_full, 5)}
+                     "launches); efficiency = t_full / (s * slowest share)", "t_full_ms": round(t_full, 5),
+           "inflight": {"method": f"each share with {len(ctxs)} frames in flight (the rank's contexts alternating, "
+                                  "wall time per frame of 200 frames after 40), the full frame likewise: the "
+                                  "N-GPU bench's own mode", "frames_in_flight": len(ctxs),
+                        "t_full_ms": round(t_full_if, 5)}}
     for s_ in steps:
-        shares = [t(abi.make_params(wl.W, wl.H, stripe_rows=16, stripe_first=r, stripe_step=s_)) for r in range(s_)]
+        ps = [abi.make_params(wl.W, wl.H, stripe_rows=16, stripe_first=r, stripe_step=s_) for r in range(s_)]
+        shares = [t(p) for p in ps]
+        shares_if = [t_inflight(p) for p in ps]
         rec, src = pmc_traffic(wl.scene, wl.W, wl.H, 1, s_, lib_hash)
         out[f"s{s_}"] = {"share_ms": [round(x, 5) for x in shares],
                          "efficiency": round(t_full / (s_ * max(shares)), 4),
                          "efficiency_rank0": round(t_full / (s_ * shares[0]), 4),
                          "hbm_bytes_per_frame_rank0": rec.get("hbm_bytes_per_frame") if rec else None,
                          "hbm_source": src}
+        out["inflight"][f"s{s_}"] = {"share_ms": [round(x, 5) for x in shares_if],
+                                     "efficiency": round(t_full_if / (s_ * max(shares_if)), 4)}
     return out
 
 
@@ -718,7 +745,7 @@ def main() -> int:
                 exact = next((x for sc, w_, h_, x in PARITY_CONFIGS if (sc, w_, h_) == (scene, mw, mh)), True)
                 entry["parity"] = parity_report(r["px0"], r["rgb0"], scene, mw, mh, exact=exact, with_fnv=False)
             if N == 1:
-                entry["strong_scaling_predictor"] = stripe_predictor(ctxs[0], wl, lib_hash)
+                entry["strong_scaling_predictor"] = stripe_predictor(ctxs, wl, lib_hash)
             multi.append(entry)
 
     # ---- 3. parity of every config at full size (N = 1; one rank per GPU renders stripes at N > 1)

@@ -1942,6 +1942,73 @@ __global__ void __launch_bounds__(kReorderThreads) rtx_sched_scatter(uint32_t* _
     }
 }
 
+// XCD-affine dispatch (RTX_XCD_ORDER=1, rtx_ctx::xcd_order): workgroups are dealt round robin over the 8
+// XCDs (MI355X_MICROARCH.md, workgroup dispatch), so positions p and p + 8 of the dispatch order run on
+// one XCD.  This pass re-deals the cost order so that position 8k + r holds the k-th tile, in cost order,
+// of class r (each view cut into 8 x 8 blocks, block (i, j) in class (i + 3 j) mod 8): each XCD's L2 then
+// serves eight blocks' BVH nodes, triangles and cull records instead of the whole screen's.  (One
+// compact region per class, a 4 x 2 grid, measured 1.4-2x slower: the in-order round-robin dispatch
+// then waits on the XCD of the heaviest region, profiles/r06/xcd_ab.txt.)  Regions hold unequal
+// counts; once the smallest is exhausted the remaining tiles follow in cost order.  One workgroup, three
+// passes over each thread's consecutive positions (counts, ranks, writes); a permutation, so no pixel
+// changes.
+#ifndef RTX_XCD_BLOCKS
+#define RTX_XCD_BLOCKS 8   // the view cut into B x B blocks, dealt to the 8 classes as a Latin square
+#endif
+__device__ __forceinline__ uint32_t xcd_region(uint32_t tile, uint32_t tiles_x, uint32_t tiles_y) {
+    const uint32_t per_view = tiles_x * tiles_y;
+    const uint32_t rem = tile % per_view, bx = rem % tiles_x, gy = rem / tiles_x;
+    const uint32_t i = bx * RTX_XCD_BLOCKS / tiles_x, j = gy * RTX_XCD_BLOCKS / tiles_y;
+    // every row and column of blocks holds each class (RTX_XCD_BLOCKS = 8) or each class equally often:
+    // a compact heavy area (the Bunny, the heightfield's grazing band) spreads over the classes
+    return (i + 3u * j) % 8u;
+}
+__global__ void __launch_bounds__(kScanThreads) rtx_sched_xcd(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                              uint32_t n, uint32_t tiles_x, uint32_t tiles_y) {
+    __shared__ uint32_t cnt[8][kScanThreads];
+    __shared__ uint32_t ovf[kScanThreads];
+    __shared__ uint32_t tot[8];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t per = (n + kScanThreads - 1) / kScanThreads;
+    const uint32_t lo = tid * per < n ? tid * per : n, hi = lo + per < n ? lo + per : n;
+    uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t p = lo; p < hi; ++p) ++c[xcd_region(in[p], tiles_x, tiles_y)];
+    for (int r = 0; r < 8; ++r) cnt[r][tid] = c[r];
+    __syncthreads();
+    if (tid < 8) {   // exclusive scan of region tid's counts over the threads
+        uint32_t acc = 0;
+        for (uint32_t t = 0; t < kScanThreads; ++t) {
+            const uint32_t v = cnt[tid][t];
+            cnt[tid][t] = acc;
+            acc += v;
+        }
+        tot[tid] = acc;
+    }
+    __syncthreads();
+    uint32_t m = tot[0];
+    for (int r = 1; r < 8; ++r) m = tot[r] < m ? tot[r] : m;
+    uint32_t k[8], o = 0;
+    for (int r = 0; r < 8; ++r) k[r] = cnt[r][tid];
+    for (uint32_t p = lo; p < hi; ++p) o += k[xcd_region(in[p], tiles_x, tiles_y)]++ >= m ? 1u : 0u;
+    ovf[tid] = o;
+    __syncthreads();
+    if (tid == 0) {   // exclusive scan of the overflow counts
+        uint32_t acc = 0;
+        for (uint32_t t = 0; t < kScanThreads; ++t) {
+            const uint32_t v = ovf[t];
+            ovf[t] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    for (int r = 0; r < 8; ++r) k[r] = cnt[r][tid];
+    o = ovf[tid];
+    for (uint32_t p = lo; p < hi; ++p) {
+        const uint32_t t = in[p], r = xcd_region(t, tiles_x, tiles_y), kr = k[r]++;
+        out[kr < m ? 8u * kr + r : 8u * m + o++] = t;
+    }
+}
+
 // ====================================================================== host side
 struct rtx_ctx {
     int device = 0;
@@ -1975,6 +2042,8 @@ struct rtx_ctx {
     // last render
     // cost-ordered tile dispatch
     uint32_t* d_order = nullptr;
+    uint32_t* d_order_xcd = nullptr;    // the XCD-affine re-deal of d_order (rtx_sched_xcd)
+    bool xcd_order = false;             // RTX_XCD_ORDER=1
     uint32_t* d_cost = nullptr;
     uint32_t* d_saved_cost = nullptr;   // last one-piece cost per tile
     uint32_t* d_hist = nullptr;         // per (class, chunk) tile counts -> slot bases (rtx_sched_*)
@@ -2238,6 +2307,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     // RTX_TILE_ORDER=0 disables cost-ordered tile dispatch (identity order every frame)
     if (const char* e = std::getenv("RTX_TILE_ORDER")) c->sched_enabled = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_MOTION")) c->motion_off = std::strcmp(e, "0") == 0;
+    if (const char* e = std::getenv("RTX_XCD_ORDER")) c->xcd_order = std::strcmp(e, "1") == 0;
     if (const char* e = std::getenv("RTX_THROUGHPUT")) c->throughput_off = std::strcmp(e, "0") == 0;
     if (const char* e = std::getenv("RTX_SCHED_PERIOD"))
         c->sched_period = std::max<uint32_t>(1u, static_cast<uint32_t>(std::strtoul(e, nullptr, 10)));
@@ -2336,6 +2406,7 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     (void)hipFree(c->d_rgb);
     (void)hipFree(c->d_counters);
     (void)hipFree(c->d_order);
+    (void)hipFree(c->d_order_xcd);
     (void)hipFree(c->d_cost);
     (void)hipFree(c->d_saved_cost);
     (void)hipFree(c->d_hist);
@@ -3097,6 +3168,8 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     if (ntiles > c->sched_cap) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         (void)hipFree(c->d_order);
+        (void)hipFree(c->d_order_xcd);
+        c->d_order_xcd = nullptr;
         (void)hipFree(c->d_cost);
         for (int k = 0; k < 2; ++k) { (void)hipFree(c->d_heavy_flag[k]); c->d_heavy_flag[k] = nullptr; }
         (void)hipFree(c->d_saved_cost);
@@ -3109,6 +3182,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         c->d_cost = nullptr;
         c->sched_cap = 0;
         HIP_TRY(c, hipMalloc(&c->d_order, ntiles * 4));
+        if (c->xcd_order) HIP_TRY(c, hipMalloc(&c->d_order_xcd, ntiles * 4));
         HIP_TRY(c, hipMalloc(&c->d_cost, ntiles * 4));
         for (int k = 0; k < 2; ++k) HIP_TRY(c, hipMalloc(&c->d_heavy_flag[k], ntiles * 4));
         HIP_TRY(c, hipMalloc(&c->d_saved_cost, ntiles * 4));
@@ -3240,7 +3314,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     const bool measure = c->sched_enabled && !c->heavy_pending &&
                          (!c->sched_ready || motion || c->sched_frame % (tuning ? 2u : c->sched_period) == 0);
     ++c->sched_frame;
-    F.order = (c->sched_enabled && c->sched_ready) ? c->d_order : nullptr;
+    F.order = (c->sched_enabled && c->sched_ready) ? (c->xcd_order ? c->d_order_xcd : c->d_order) : nullptr;
     F.cost = measure ? c->d_cost : nullptr;
     F.part_cost = (measure && motion) ? 1u : 0u;
     return RTX_OK;
@@ -3401,6 +3475,11 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
                            F.n_tiles, c->d_hist, nch, c->d_thr, slots == 0xffffffffu ? 1u : 0u,
                            c->d_heavy_flag[stage], c->d_heavy_list[stage], c->d_heavy_n);
         HIP_TRY(c, hipGetLastError());
+        if (c->xcd_order) {
+            hipLaunchKernelGGL(rtx_sched_xcd, dim3(1), dim3(kScanThreads), 0, c->stream, c->d_order, c->d_order_xcd,
+                               F.n_tiles, F.tiles_x, F.tiles_y);
+            HIP_TRY(c, hipGetLastError());
+        }
         HIP_TRY(c, hipMemcpyAsync(c->h_heavy_n, c->d_heavy_n, 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_heavy, c->stream));
         c->heavy_pending = true;

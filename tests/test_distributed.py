@@ -191,6 +191,10 @@ def test_bench_one_gpu_contract(tmp_path):
             x = sp[f"s{s}"]
             assert len(x["share_ms"]) == s
             assert abs(x["efficiency"] - sp["t_full_ms"] / (s * max(x["share_ms"]))) < 1e-3
+            y = sp["inflight"][f"s{s}"]   # the same with the bench's frames in flight
+            assert len(y["share_ms"]) == s
+            assert abs(y["efficiency"] - sp["inflight"]["t_full_ms"] / (s * max(y["share_ms"]))) < 1e-3
+    assert "W4_Bunny" in scenes   # the headline scene's one-frame leg
     assert "flop_basis" in scenes["Synthetic100k"]["roofline_rank0"]
     assert "flop_basis" not in scenes["Bunny8Lights"]["roofline_rank0"]
     for name in ("Synthetic100k", "W4_Optional"):   # the culled scenes: `frac` is executed work
