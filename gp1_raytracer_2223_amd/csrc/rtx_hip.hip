@@ -40,11 +40,15 @@
 using namespace rtxd;
 
 [[maybe_unused]] constexpr int kStampWords = 8;   // + primary-hit time, shadow-walk time (RTX_STAMPS)
+// split waves' {sum, max, steps} per (phase, part) in 64 shards by wave index: one address per
+// (phase, part) took every split wave's atomics into one L2 channel and slowed the whole frame ~6x
+[[maybe_unused]] constexpr int kStampShards = 64;
 #if RTX_STAMPS
 #define RTX_SPLIT_STAMP()                                                                          \
     if (lane == 0 && F.split_stamps) {                                                             \
         const unsigned long long d_ = __builtin_amdgcn_s_memrealtime() - t_start;                 \
-        unsigned long long* x_ = F.split_stamps + 3 * ((PHASE - 1) * kMaxParts + part);            \
+        unsigned long long* x_ =                                                                   \
+            F.split_stamps + 3 * (((PHASE - 1) * kMaxParts + part) * kStampShards + widx % kStampShards); \
         atomicAdd(x_, d_);                                                                         \
         atomicMax(x_ + 1, d_);                                                                     \
         atomicAdd(x_ + 2, static_cast<unsigned long long>(cnt.c[kWaveNodeTests] + cnt.c[kWaveTriTests])); \
@@ -3783,16 +3787,31 @@ extern "C" int rtx_debug_stamps(rtx_ctx* c, const rtx_camera* cam, const rtx_ren
     if (kStampWords * nw > capacity) return RTX_E_INVALID;
     if (kStampWords * nw + 6 * kMaxParts > capacity) return RTX_E_INVALID;
     unsigned long long* d = nullptr;
-    const size_t words = kStampWords * nw + 6 * kMaxParts;   // + per (phase 1/2, part) {sum, max, steps}
+    // + per (phase 1/2, part, shard) {sum, max, steps}, reduced over the shards below
+    const size_t words = kStampWords * nw + 6 * kMaxParts * kStampShards;
     HIP_TRY(c, hipMalloc(&d, words * 8));
     HIP_TRY(c, hipMemsetAsync(d, 0, words * 8, c->stream));
     F.stamps = d;
     F.split_stamps = d + kStampWords * nw;
     rc = launch(c, F, grid, false);
     if (rc != RTX_OK) return rc;
-    HIP_TRY(c, hipMemcpyAsync(out, d, words * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(out, d, kStampWords * nw * 8, hipMemcpyDeviceToHost, c->stream));
+    std::vector<unsigned long long> sh(6 * kMaxParts * kStampShards);
+    HIP_TRY(c, hipMemcpyAsync(sh.data(), d + kStampWords * nw, sh.size() * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     (void)hipFree(d);
+    for (size_t k = 0; k < 2u * kMaxParts; ++k) {
+        unsigned long long sum = 0, mx = 0, steps = 0;
+        for (int j = 0; j < kStampShards; ++j) {
+            const unsigned long long* x = sh.data() + 3 * (k * kStampShards + j);
+            sum += x[0];
+            mx = std::max(mx, x[1]);
+            steps += x[2];
+        }
+        out[kStampWords * nw + 3 * k] = sum;
+        out[kStampWords * nw + 3 * k + 1] = mx;
+        out[kStampWords * nw + 3 * k + 2] = steps;
+    }
     return RTX_OK;
 }
 #endif

@@ -13,7 +13,7 @@ if [ "$2" != "--no-tests" ]; then
   tail -2 $OUT/gpu_tests.log
   timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" >> $OUT/gpu_tests.log 2>&1 || { echo "smoke failed"; exit 1; }
 fi
-timeout -k 10 400 bash tools/pmc_configs.sh ${R}_pmc > $OUT/pmc.log 2>&1 || { echo "pmc failed"; tail -5 $OUT/pmc.log; exit 1; }
+timeout -k 10 600 bash tools/pmc_configs.sh ${R}_pmc > $OUT/pmc.log 2>&1 || { echo "pmc failed"; tail -5 $OUT/pmc.log; exit 1; }
 cp gpurun_out/${R}_pmc/pmc_configs.json profiles/$R/pmc_configs.json
 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_driver.json 2> $OUT/bench_driver.err || { echo "bench driver failed"; tail -5 $OUT/bench_driver.err; exit 1; }
 timeout -k 10 400 python3 bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { echo "bench default failed"; tail -5 $OUT/bench_default.err; exit 1; }

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 NAME=${1:-pmc_configs}
 OUT=gpurun_out/$NAME
 mkdir -p $OUT
-CONFIGS=${2:-"W4_Bunny 1920 1080 1;W4_Optional 1920 1080 1;Synthetic100k 1920 1080 1;Synthetic100k 1920 1080 2;Synthetic100k 1920 1080 4;Synthetic100k 1920 1080 8;Bunny8Lights 3840 2160 1;Bunny8Lights 3840 2160 2;Bunny8Lights 3840 2160 4;Bunny8Lights 3840 2160 8"}
+CONFIGS=${2:-"W4_Bunny 1920 1080 1;W4_Bunny 1920 1080 2;W4_Bunny 1920 1080 4;W4_Bunny 1920 1080 8;W4_Optional 1920 1080 1;Synthetic100k 1920 1080 1;Synthetic100k 1920 1080 2;Synthetic100k 1920 1080 4;Synthetic100k 1920 1080 8;Bunny8Lights 3840 2160 1;Bunny8Lights 3840 2160 2;Bunny8Lights 3840 2160 4;Bunny8Lights 3840 2160 8"}
 FRAMES=${FRAMES:-40}
 IFS=';' read -ra CFG <<< "$CONFIGS"
 for c in "${CFG[@]}"; do
