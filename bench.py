@@ -454,10 +454,10 @@ class Workload:
         self.d.barrier()
         return self.d.max(time.perf_counter() - t0)
 
-    def kernel_ms(self, launches: int) -> float:
+    def kernel_ms(self, launches: int, ctx=None) -> float:
         """Mean launch time of ONE context's serialized launches (HIP events on its stream)."""
         ms = C.c_float()
-        ctx = self.ctxs[0]
+        ctx = ctx or self.ctxs[0]
         abi.check(self.lib.rtx_time_views(ctx.h, self.views, self.nviews, C.byref(self.params), launches,
                                           C.byref(ms)), "rtx_time_views", ctx.h)
         return ms.value
@@ -491,7 +491,10 @@ class Workload:
 
     def run(self, steps: int, warmup: int, launches: int, gather: bool, tag: str) -> dict:
         d, W, H = self.d, self.W, self.H
-        self.kernel_ms(launches)   # (untimed here: the serialized launches also bring the GPU clock up)
+        # untimed: serialized launches on EVERY context (each context's tile schedule measured and its
+        # split threshold tuned before its frames go in flight), which also bring the GPU clock up
+        for c in self.ctxs:
+            self.kernel_ms(launches, c)
         for i in range(warmup):
             self.step(i)
         self.sync_all()
@@ -556,7 +559,8 @@ def stripe_predictor(ctxs, wl: "Workload", lib_hash: str, steps=(2, 4, 8), launc
     after a warm-up that builds the share's cost order).  The step time at s GPUs is the slowest
     share's, so efficiency(s) = t_full / (s * max_r t_share(r)); `rank0` uses rank 0's share only.
     `inflight`: the same with the rank's frames in flight as the N-GPU bench runs them (--inflight:
-    the rank's contexts alternating frames, wall time per frame over 200 frames after 40), the full
+    the rank's contexts alternating frames, wall time per frame over 200 frames after each context's
+    serialized warm-up and 200 alternating frames), the full
     frame likewise.  What it leaves out: the host gather and the ranks' clocks (one GPU times every
     share)."""
     ctx = ctxs[0]
@@ -572,7 +576,10 @@ def stripe_predictor(ctxs, wl: "Workload", lib_hash: str, steps=(2, 4, 8), launc
             best = ms.value if best is None else min(best, ms.value)
         return best
 
-    def t_inflight(p, frames=200, warm=40):
+    def t_inflight(p, frames=200, warm=200):
+        for c in ctxs:   # every context's schedule measured and tuned first, as Workload.run does
+            ms = C.c_float()
+            abi.check(lib.rtx_time_views(c.h, cam, 1, C.byref(p), launches, C.byref(ms)), "rtx_time_views", c.h)
         for i in range(warm):
             abi.check(lib.rtx_render_views_async(ctxs[i % len(ctxs)].h, cam, 1, C.byref(p), 0), "render", ctx.h)
         for c in ctxs:
@@ -589,7 +596,8 @@ def stripe_predictor(ctxs, wl: "Workload", lib_hash: str, steps=(2, 4, 8), launc
     out = {"method": f"each share timed alone (rtx_time_views, best of 2 x {launches} launches after 5 warm-up "
                      "launches); efficiency = t_full / (s * slowest share)", "t_full_ms": round(t_full, 5),
            "inflight": {"method": f"each share with {len(ctxs)} frames in flight (the rank's contexts alternating, "
-                                  "wall time per frame of 200 frames after 40), the full frame likewise: the "
+                                  f"wall time per frame of 200 frames after {launches} serialized launches per context "
+                                  "and 200 in flight), the full frame likewise: the "
                                   "N-GPU bench's own mode", "frames_in_flight": len(ctxs),
                         "t_full_ms": round(t_full_if, 5)}}
     for s_ in steps:
@@ -699,7 +707,8 @@ def main() -> int:
     if not args.no_extra:
         for scene, mw, mh, msteps in MULTI_GPU_CONFIGS:
             wl = Workload(ctxs, d, scene, mw, mh, "frame")
-            r = wl.run(msteps, 10, 100, not args.no_gather, f"{tag}_{scene}")
+            # (150 warm-up steps: the contexts' in-flight probe, rtx_inflight_info, settles in ~130)
+            r = wl.run(msteps, 150, 100, not args.no_gather, f"{tag}_{scene}")
             rec, src = pmc_traffic(scene, mw, mh, 1, N, lib_hash)
             # every rank's HBM rate over its own launches (the PMC record is rank 0's stripes)
             per_rank = d.gather([r["kernel_ms"], r["flop"]])

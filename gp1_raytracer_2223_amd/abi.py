@@ -155,7 +155,8 @@ HIP_SYMBOLS = ["rtx_abi_version", "rtx_create", "rtx_destroy", "rtx_last_error",
                "rtx_group_create", "rtx_group_destroy", "rtx_group_last_error", "rtx_group_size",
                "rtx_group_context", "rtx_group_upload_scene", "rtx_group_render", "rtx_schedule_state",
                "rtx_anim_create", "rtx_anim_destroy", "rtx_anim_last_error", "rtx_anim_update", "rtx_anim_status",
-               "rtx_anim_download", "rtx_scene_image", "rtx_anim_stamps", "rtx_cull_info", "rtx_cull_dump", "rtx_light_major_info"]
+               "rtx_anim_download", "rtx_scene_image", "rtx_anim_stamps", "rtx_cull_info", "rtx_cull_dump", "rtx_light_major_info",
+               "rtx_inflight_info"]
 
 
 def load_hip() -> C.CDLL:
@@ -222,6 +223,10 @@ def load_hip() -> C.CDLL:
         if hasattr(lib, "rtx_light_major_info"):   # absent only in older experiment builds (RTX_HIP_LIB)
             lib.rtx_light_major_info.argtypes = [VP, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
             lib.rtx_light_major_info.restype = C.c_int
+        if hasattr(lib, "rtx_inflight_info"):
+            lib.rtx_inflight_info.argtypes = [VP, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_float),
+                                              C.POINTER(C.c_float), C.POINTER(C.c_float)]
+            lib.rtx_inflight_info.restype = C.c_int
         if hasattr(lib, "rtx_split_info"):   # absent only in older experiment builds (RTX_HIP_LIB)
             lib.rtx_split_info.argtypes = [VP, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
             lib.rtx_split_info.restype = C.c_int

@@ -1802,14 +1802,20 @@ __global__ void __launch_bounds__(kReorderThreads) rtx_sched_count(uint32_t* __r
                                                                    uint32_t* __restrict__ saved,
                                                                    uint32_t* __restrict__ hist,
                                                                    unsigned long long* __restrict__ csum,
-                                                                   uint32_t nchunks, uint32_t parts) {
+                                                                   uint32_t nchunks, uint32_t parts,
+                                                                   uint32_t* __restrict__ max_cost) {
     __shared__ uint32_t h[kCostBuckets];
     __shared__ unsigned long long tot;
+    __shared__ uint32_t mx;
     const uint32_t tid = threadIdx.x, base = blockIdx.x * kSchedChunk;
     if (tid < kCostBuckets) h[tid] = 0;
-    if (tid == 0) tot = 0;
+    if (tid == 0) {
+        tot = 0;
+        mx = 0;
+    }
     __syncthreads();
     unsigned long long my = 0;
+    uint32_t my_max = 0;
     for (uint32_t k = 0; k < kSchedChunk / kReorderThreads; ++k) {
         const uint32_t t = base + k * kReorderThreads + tid;   // coalesced; counting ignores order
         if (t >= n) break;
@@ -1828,11 +1834,16 @@ __global__ void __launch_bounds__(kReorderThreads) rtx_sched_count(uint32_t* __r
         }
         atomicAdd(&h[cost_class(c)], 1u);
         my += c;
+        my_max = c > my_max ? c : my_max;
     }
     atomicAdd(&tot, my);
+    atomicMax(&mx, my_max);
     __syncthreads();
     if (tid < kCostBuckets) hist[tid * nchunks + blockIdx.x] = h[tid];
-    if (tid == 0) csum[blockIdx.x] = tot;
+    if (tid == 0) {
+        csum[blockIdx.x] = tot;
+        atomicMax(max_cost, mx);
+    }
 }
 
 // Exclusive prefix of hist[class][chunk] in class-major order (in place), the total cost and
@@ -1840,7 +1851,7 @@ __global__ void __launch_bounds__(kReorderThreads) rtx_sched_count(uint32_t* __r
 __global__ void __launch_bounds__(kScanThreads) rtx_sched_scan(uint32_t* __restrict__ hist, uint32_t nchunks,
                                                                const unsigned long long* __restrict__ csum, uint32_t n,
                                                                uint32_t split_slots, uint32_t split_permille,
-                                                               uint32_t split_min,
+                                                               uint32_t split_min, uint32_t wave_slots,
                                                                unsigned long long* __restrict__ thr_out,
                                                                uint32_t* __restrict__ heavy_n) {
     __shared__ uint32_t part[kScanThreads];
@@ -1877,7 +1888,13 @@ __global__ void __launch_bounds__(kScanThreads) rtx_sched_scan(uint32_t* __restr
         const unsigned long long thr =
             split_slots ? total * split_permille / (1000ull * (n < split_slots ? n : split_slots)) : ~0ull;
         *thr_out = force ? 0ull : (thr > split_min ? thr : static_cast<unsigned long long>(split_min));
-        *heavy_n = 0;
+        heavy_n[0] = 0;
+        // the frame's heaviest tile (rtx_sched_count's maximum, zeroed for the next measurement) and
+        // its cost per wave slot, for the in-flight choice (kInflightCritPermille)
+        heavy_n[2] = heavy_n[1];
+        heavy_n[1] = 0;
+        const unsigned long long per = wave_slots ? total / (n < wave_slots ? n : wave_slots) : 0ull;
+        heavy_n[3] = static_cast<uint32_t>(per < 0xffffffffull ? per : 0xffffffffull);
     }
 }
 
@@ -2077,6 +2094,19 @@ struct rtx_ctx {
     bool in_registry = false;                   // listed in g_frames (its ev_frame is recorded per frame)
     bool concurrent = false;
     bool throughput_off = false;                // RTX_THROUGHPUT=0
+    // in flight (kInflightCritPermille): the heaviest tile's one-piece cost measured in the last
+    // serialized measurement (cost units), the threshold (RTX_INFLIGHT_CRIT), and whether the last
+    // frame rendered one piece because of it
+    uint32_t max_cost_serial = 0;
+    // the split frames' interval in flight on this context's stream (inflight_onepiece): 0 skipping
+    // kInflightWindowSkip frames, 2 timing kInflightWindow frames, 3 waiting for the end event, 4 done
+    uint32_t win_state = 0;
+    uint32_t win_frames = 0;
+    int win_rec = -1;                           // the ev_win slot this frame's end records (-1 none)
+    float win_interval_ms = 0.f;
+    hipEvent_t ev_win[2] = {};
+    uint32_t inflight_crit = kInflightCritPermille;
+    bool frame_onepiece = false;
     int heavy_cur = 0;
     uint32_t heavy_n = 0;
     bool heavy_pending = false;
@@ -2266,18 +2296,19 @@ thread_local std::string g_create_err;
 std::mutex g_frames_m;
 std::vector<rtx_ctx*> g_frames;
 
-// Another context on c's device with a frame still in flight (its ev_frame not reached).
-bool frames_concurrent(rtx_ctx* c) {
+// The other contexts on c's device with a frame still in flight (their ev_frame not reached).
+uint32_t frames_concurrent(rtx_ctx* c) {
     std::lock_guard<std::mutex> l(g_frames_m);
+    uint32_t n = 0;
     for (rtx_ctx* o : g_frames) {
         if (o == c || o->device != c->device) continue;
         const hipError_t q = hipEventQuery(o->ev_frame);
         if (q == hipErrorNotReady) {
             (void)hipGetLastError();   // (not-ready is no error for the caller's checks)
-            return true;
+            ++n;
         }
     }
-    return false;
+    return n;
 }
 void frames_note(rtx_ctx* c) {
     std::lock_guard<std::mutex> l(g_frames_m);
@@ -2313,6 +2344,10 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     if (const char* e = std::getenv("RTX_MOTION")) c->motion_off = std::strcmp(e, "0") == 0;
     if (const char* e = std::getenv("RTX_XCD_ORDER")) c->xcd_order = std::strcmp(e, "1") == 0;
     if (const char* e = std::getenv("RTX_THROUGHPUT")) c->throughput_off = std::strcmp(e, "0") == 0;
+    if (const char* e = std::getenv("RTX_INFLIGHT_CRIT")) {
+        const double f = std::atof(e);
+        if (f >= 0 && f < 1e6) c->inflight_crit = static_cast<uint32_t>(f * 1000.0);
+    }
     if (const char* e = std::getenv("RTX_SCHED_PERIOD"))
         c->sched_period = std::max<uint32_t>(1u, static_cast<uint32_t>(std::strtoul(e, nullptr, 10)));
     // RTX_SPLIT=0 renders heavy tiles in one piece; RTX_SPLIT=force splits every tile
@@ -2370,12 +2405,16 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     RTX_CREATE_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     RTX_CREATE_TRY(hipEventCreateWithFlags(&c->ev_frame, hipEventDisableTiming));
     for (auto& e : c->ev_tune) RTX_CREATE_TRY(hipEventCreate(&e));
+    for (auto& e : c->ev_win) RTX_CREATE_TRY(hipEventCreate(&e));
     RTX_CREATE_TRY(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+    if (const char* e = std::getenv("RTX_SPLIT_PRIO"); e && std::strcmp(e, "0") == 0) hi_prio = lo_prio;
     RTX_CREATE_TRY(hipStreamCreateWithPriority(&c->split_stream, hipStreamNonBlocking, hi_prio));
     RTX_CREATE_TRY(hipMalloc(&c->d_counters, sizeof(unsigned long long) * kNumCounters));
-    RTX_CREATE_TRY(hipMalloc(&c->d_heavy_n, 4));
+    // {heavy tiles, max tile cost (rtx_sched_count), max tile cost, cost per wave slot (rtx_sched_scan)}
+    RTX_CREATE_TRY(hipMalloc(&c->d_heavy_n, 16));
+    RTX_CREATE_TRY(hipMemset(c->d_heavy_n, 0, 16));
     RTX_CREATE_TRY(hipMalloc(&c->d_thr, 8));
-    RTX_CREATE_TRY(hipHostMalloc(&c->h_heavy_n, 4));
+    RTX_CREATE_TRY(hipHostMalloc(&c->h_heavy_n, 16));
     RTX_CREATE_TRY(hipMalloc(&c->d_heavy_list[0], 4 * kMaxHeavyTiles));
     RTX_CREATE_TRY(hipMalloc(&c->d_heavy_list[1], 4 * kMaxHeavyTiles));
     RTX_CREATE_TRY(hipMalloc(&c->d_hit_key, 8 * heavy_px));
@@ -2434,6 +2473,8 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->ev_frame) (void)hipEventDestroy(c->ev_frame);
     for (auto& e : c->ev_tune)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->ev_win)
         if (e) (void)hipEventDestroy(e);
     if (c->split_stream) {
         (void)hipStreamSynchronize(c->split_stream);
@@ -3080,6 +3121,50 @@ void split_tune(rtx_ctx* c, float main_ms, float chain_ms) {
     c->split_permille = static_cast<uint32_t>(std::min(4000.0, std::max(1000.0, f)));
 }
 
+// The heaviest tile's serialized one-piece time over the split frame's serialized span (the tuner's
+// best: main kernel or chain); 0 until both are known.
+float inflight_ratio(const rtx_ctx* c);
+
+// Whether a frame in flight (k frames of this device's contexts at once) renders one piece
+// (kInflightCritPermille): its heaviest tile is short next to the split frame's serialized span, or
+// the split frames in flight were measured not to overlap (their interval on this context's stream
+// ~ k x the serialized span: the chain's work fills the GPU, so the frames only queue).  Times the
+// interval over kInflightWindow split frames in flight first (rtx_ctx::win_*).
+bool inflight_onepiece(rtx_ctx* c, uint32_t k) {
+    c->win_rec = -1;
+    if (c->inflight_crit == 0) return false;
+    const float r = inflight_ratio(c);
+    if (r > 0.f && r * 1000.f < static_cast<float>(c->inflight_crit)) return true;
+    if (c->win_state == 4)   // measured: overlap = k x span / interval
+        return c->tune_best_span > 0.f && c->win_interval_ms > 0.f &&
+               static_cast<float>(k) * c->tune_best_span < kInflightOverlapMin * c->win_interval_ms;
+    if (c->win_state == 0 && ++c->win_frames >= kInflightWindowSkip) {
+        c->win_state = 2;
+        c->win_frames = 0;
+        c->win_rec = 0;
+    } else if (c->win_state == 2 && ++c->win_frames == kInflightWindow) {
+        c->win_state = 3;
+        c->win_rec = 1;
+    } else if (c->win_state == 3) {
+        const hipError_t q = hipEventQuery(c->ev_win[1]);
+        (void)hipGetLastError();   // (not-ready is no error for the caller's checks)
+        if (q == hipSuccess) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, c->ev_win[0], c->ev_win[1]) == hipSuccess && ms > 0.f)
+                c->win_interval_ms = ms / static_cast<float>(kInflightWindow);
+            (void)hipGetLastError();
+            c->win_state = 4;
+        }
+    }
+    return false;
+}
+float inflight_ratio(const rtx_ctx* c) {
+    if (c->max_cost_serial == 0 || c->tune_best_span <= 0.f) return 0.f;
+    const float tile_ms = static_cast<float>(c->max_cost_serial) * static_cast<float>(kSplitMinUs) /
+                          static_cast<float>(kSplitMinCost) * 1e-3f;
+    return tile_ms / c->tune_best_span;
+}
+
 int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_params* p, bool want_rgb, FrameArgs& F,
             dim3& grid) {
     if (!c || !cams || !p) return RTX_E_INVALID;
@@ -3226,6 +3311,10 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         c->sched_ready = false;
         c->sched_frame = 0;
         c->motion_left = 0;
+        c->max_cost_serial = 0;
+        c->win_state = 0;
+        c->win_frames = 0;
+        c->win_interval_ms = 0.f;
         if (c->tune_on) {   // a new shape: tune again from the default
             c->split_permille = kSplitPermille;
             c->tune_done = false;
@@ -3256,7 +3345,8 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         }
         if (ready) {
             c->heavy_pending = false;
-            c->heavy_n = std::min<uint32_t>(*c->h_heavy_n, kMaxHeavyTiles);
+            c->heavy_n = std::min<uint32_t>(c->h_heavy_n[0], kMaxHeavyTiles);
+            if (!c->concurrent) c->max_cost_serial = c->h_heavy_n[2];
             c->heavy_cur ^= 1;
             // nothing to balance while no tile is heavy at the default factor (the tuner only
             // raises the factor from there when the split chain is the longer)
@@ -3273,7 +3363,14 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
             }
         }
     }
-    const bool split = c->split_mode != 0 && c->split_ok && c->sched_enabled && c->heavy_n > 0;
+    // throughput mode: other contexts' frames in flight on this device (rtx_ctx::ev_frame; asked only
+    // where a tile can be split: the other contexts' event queries are not free in a GPU-bound loop)
+    const uint32_t others = (!c->throughput_off && c->tune_on && c->split_ok && (c->heavy_n > 0 || !c->tune_done))
+                                ? frames_concurrent(c) : 0u;
+    c->concurrent = others > 0;
+    // in flight: one piece while the heaviest tile is short next to the split frame (kInflightCritPermille)
+    c->frame_onepiece = c->concurrent && c->heavy_n > 0 && inflight_onepiece(c, others + 1);
+    const bool split = c->split_mode != 0 && c->split_ok && c->sched_enabled && c->heavy_n > 0 && !c->frame_onepiece;
     F.heavy_flag = split ? c->d_heavy_flag[c->heavy_cur] : nullptr;
     F.heavy_list = c->d_heavy_list[c->heavy_cur];
     F.heavy_n = split ? c->heavy_n : 0u;
@@ -3309,10 +3406,6 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     // Measure tile costs on the first frame of a shape and then every kSchedPeriod frames;
     // the frames in between reuse the last order and pay nothing for scheduling.
     // while the split threshold is being tuned (a scene with split tiles), every other frame is measured
-    // (rtx_ctx::ev_frame; asked only where a tile can be split: the other contexts' event queries
-    // are not free in a GPU-bound loop)
-    c->concurrent = !c->throughput_off && c->tune_on && c->split_ok && (c->heavy_n > 0 || !c->tune_done) &&
-                    frames_concurrent(c);
     const bool tuning = c->tune_on && !c->tune_done && c->heavy_n > 0 && c->split_mode == 1 && c->split_ok && !motion &&
                         !c->concurrent;
     const bool measure = c->sched_enabled && !c->heavy_pending &&
@@ -3469,11 +3562,11 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         c->set_permille[stage] = permille;
         const uint32_t nch = (F.n_tiles + kSchedChunk - 1) / kSchedChunk;
         hipLaunchKernelGGL(rtx_sched_count, dim3(nch), dim3(kReorderThreads), 0, c->stream, F.cost, F.n_tiles,
-                           F.heavy_flag, c->d_saved_cost, c->d_hist, c->d_csum, nch, F.part_cost);
+                           F.heavy_flag, c->d_saved_cost, c->d_hist, c->d_csum, nch, F.part_cost, c->d_heavy_n + 1);
         HIP_TRY(c, hipGetLastError());
         hipLaunchKernelGGL(rtx_sched_scan, dim3(1), dim3(kScanThreads), 0, c->stream, c->d_hist, nch,
                            c->d_csum,
-                           F.n_tiles, slots, permille, c->split_min, c->d_thr, c->d_heavy_n);
+                           F.n_tiles, slots, permille, c->split_min, c->split_slots, c->d_thr, c->d_heavy_n);
         HIP_TRY(c, hipGetLastError());
         hipLaunchKernelGGL(rtx_sched_scatter, dim3(nch), dim3(kReorderThreads), 0, c->stream, F.cost, c->d_order,
                            F.n_tiles, c->d_hist, nch, c->d_thr, slots == 0xffffffffu ? 1u : 0u,
@@ -3484,7 +3577,7 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
                                F.n_tiles, F.tiles_x, F.tiles_y);
             HIP_TRY(c, hipGetLastError());
         }
-        HIP_TRY(c, hipMemcpyAsync(c->h_heavy_n, c->d_heavy_n, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(c->h_heavy_n, c->d_heavy_n, 16, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipEventRecord(c->ev_heavy, c->stream));
         c->heavy_pending = true;
         c->sched_ready = true;
@@ -3493,6 +3586,7 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
     // be split records it: one that has nothing to split (no frontier, or no heavy tile at a converged
     // factor: W4_Bunny) skips the event and the registry's lock on every frame.
     const bool tracked = c->split_ok && c->split_mode != 0 && !(c->heavy_n == 0 && c->tune_done);
+    if (c->win_rec >= 0) HIP_TRY(c, hipEventRecord(c->ev_win[c->win_rec], c->stream));
     if (tracked) {
         HIP_TRY(c, hipEventRecord(c->ev_frame, c->stream));
         if (!c->in_registry) {
@@ -3754,6 +3848,17 @@ extern "C" int rtx_split_tune_info(rtx_ctx* c, float* factor, float* main_ms, fl
     return RTX_OK;
 }
 
+extern "C" int rtx_inflight_info(rtx_ctx* c, uint32_t* concurrent, uint32_t* onepiece, float* crit,
+                                 float* crit_threshold, float* split_interval_ms) {
+    if (!c) return RTX_E_INVALID;
+    if (split_interval_ms) *split_interval_ms = c->win_interval_ms;
+    if (concurrent) *concurrent = c->concurrent ? 1u : 0u;
+    if (onepiece) *onepiece = c->frame_onepiece ? 1u : 0u;
+    if (crit) *crit = inflight_ratio(c);
+    if (crit_threshold) *crit_threshold = static_cast<float>(c->inflight_crit) / 1000.f;
+    return RTX_OK;
+}
+
 extern "C" int rtx_light_major_info(rtx_ctx* c, uint32_t* last_frame, uint32_t* max_tiles) {
     if (!c) return RTX_E_INVALID;
     if (last_frame) *last_frame = c->frame_lm ? 1u : 0u;
@@ -3767,7 +3872,7 @@ extern "C" int rtx_split_info(rtx_ctx* c, uint32_t* heavy_tiles, uint32_t* parts
         HIP_TRY(c, hipSetDevice(c->device));
         HIP_TRY(c, hipEventSynchronize(c->ev_heavy));
     }
-    const uint32_t n = c->heavy_pending ? std::min<uint32_t>(*c->h_heavy_n, kMaxHeavyTiles) : c->heavy_n;
+    const uint32_t n = c->heavy_pending ? std::min<uint32_t>(c->h_heavy_n[0], kMaxHeavyTiles) : c->heavy_n;
     const bool on = c->split_mode != 0 && c->split_ok && c->sched_enabled;
     if (heavy_tiles) *heavy_tiles = on ? n : 0u;
     if (parts) *parts = c->split_ok ? c->dev.n_parts : 0u;

@@ -37,6 +37,22 @@ constexpr int kMaxParts = 1024;        // all meshes together
 constexpr int kMaxHeavyTiles = 8192;   // heavy wave tiles per frame (hit-key buffer: 64 px each)
 // split factor floor while other contexts' frames are in flight (rtx_ctx::ev_frame)
 constexpr uint32_t kThroughputPermille = 2600;
+// In flight (rtx_ctx::concurrent) a split frame's extra work (the chain's repeated path walks, its
+// launches) can cost more than its shorter critical path saves, since the other contexts' frames fill
+// the GPU beside a long tile (2 frames in flight, profiles/r06/inflight_split_ab.txt: Bunny + 8 lights
+// 4K share of 8 0.067 split / 0.059 ms one piece, W4_Optional share of 8 0.110 / 0.088, Synthetic100k
+// share of 8 0.405 / 0.622).  Two frames in flight hide a tile as long as about two frames' time: a
+// frame in flight renders one piece when its heaviest tile's one-piece cost (measured serialized) is
+// below kInflightCritPermille / 1000 x the split frame's serialized span (the tuner's best, main
+// kernel or chain), which holds for the first two and not for Synthetic100k (profiles/r06/
+// inflight_crit_ab.txt).  RTX_INFLIGHT_CRIT=f sets the factor (0: split as serialized frames do).
+constexpr uint32_t kInflightCritPermille = 1600;
+// ... or when split frames in flight do not overlap: k frames in flight at once, their interval on a
+// context's stream at least k x the serialized span / kInflightOverlapMin (timed over kInflightWindow
+// frames after kInflightWindowSkip; W4_Optional's shares: the chain's work fills the GPU)
+constexpr float kInflightOverlapMin = 1.15f;
+constexpr uint32_t kInflightWindow = 32;
+constexpr uint32_t kInflightWindowSkip = 16;
 // 1.5 (v14 sweep, tools/split_sweep.sh): Synthetic100k 4.38 -> 3.51 ms, W4_Optional within
 // noise of 2.0; below 1.25 the split overhead outgrows the tail it removes
 constexpr int kSplitPermille = 1500;

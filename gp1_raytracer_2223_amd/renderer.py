@@ -102,6 +102,16 @@ class DeviceContext:
         return {"factor": round(f.value, 4), "main_ms": round(m.value, 5), "chain_ms": round(ch.value, 5),
                 "state": ["tuning", "converged", "off"][d.value]}
 
+    def inflight_info(self) -> dict:
+        """Frames in flight: the last frame saw another context's frame in flight / rendered one piece
+        for it; the heaviest tile's serialized time over the split frame's serialized span, the
+        threshold, and the split frames' interval in flight on this context's stream (ms)."""
+        a, b, r, t, w = C.c_uint32(), C.c_uint32(), C.c_float(), C.c_float(), C.c_float()
+        abi.check(self.lib.rtx_inflight_info(self.h, C.byref(a), C.byref(b), C.byref(r), C.byref(t), C.byref(w)),
+                  "rtx_inflight_info", self.h)
+        return {"concurrent": bool(a.value), "onepiece": bool(b.value), "crit": round(r.value, 3),
+                "threshold": round(t.value, 3), "split_interval_ms": round(w.value, 5)}
+
     def light_major_info(self) -> tuple[bool, int]:
         """(the last prepared frame was light-major, the largest light-major launch in wave tiles)."""
         a, b = C.c_uint32(), C.c_uint32()

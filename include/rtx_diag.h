@@ -61,6 +61,15 @@ int rtx_light_major_info(rtx_ctx* ctx, uint32_t* last_frame, uint32_t* max_tiles
  * (ms, from the fork), and the tuner's state (0 tuning, 1 converged, 2 off: RTX_SPLIT_TUNE=0 or a
  * fixed RTX_SPLIT_FACTOR).  Re-tuned for every new launch shape. */
 int rtx_split_tune_info(rtx_ctx* ctx, float* factor, float* main_ms, float* chain_ms, uint32_t* done);
+/* Frames in flight: while another context's frame is in flight on the device, a frame
+ * whose tiles would split renders one piece when its heaviest tile's serialized one-piece time is
+ * below crit_threshold x the split frame's serialized span (the split tuner's best; RTX_INFLIGHT_CRIT,
+ * 0: always split as serialized frames do), or when split frames in flight, timed on this context's
+ * stream, were found not to overlap.  Reports whether the last prepared frame saw another context's
+ * frame in flight, whether it rendered one piece for that, the ratio (heaviest tile / split span; 0
+ * until both are measured), the threshold and the split frames' interval in flight (ms, 0 before). */
+int rtx_inflight_info(rtx_ctx* ctx, uint32_t* concurrent, uint32_t* onepiece, float* crit, float* crit_threshold,
+                      float* split_interval_ms);
 /* Exact cull (no reference counterpart: a pruning of the reference's own BVH walk that never
  * changes a pixel).  Reports whether the uploaded scene renders with it (on for
  * host uploads whose reference boxes are inflated enough to pay, see upload_scene) and how

@@ -88,7 +88,7 @@ def test_product_header_has_no_diagnostics():
     diag = set(_declared(INC / "rtx_diag.h"))
     assert not prod & diag
     for n in ("rtx_time_views", "rtx_count_work", "rtx_split_info", "rtx_cull_dump", "rtx_schedule_state",
-              "rtx_anim_stamps", "rtx_light_major_info"):
+              "rtx_anim_stamps", "rtx_light_major_info", "rtx_inflight_info"):
         assert n in diag and n not in prod, n
     for n in ("rtx_create", "rtx_upload_scene", "rtx_render", "rtx_last_error", "rtx_destroy", "rtx_gather_async",
               "rtx_group_render", "rtx_anim_update"):

@@ -1,0 +1,73 @@
+"""Frames in flight (rtx_inflight_info): while another context's frame is in flight on the
+device, a frame whose tiles would split may render one piece instead.  Either way every pixel is the
+same: the frames rendered in flight, split or one piece, equal the one-piece frame and the reference."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from gp1_raytracer_2223_amd import abi
+from gp1_raytracer_2223_amd.renderer import DeviceContext
+from gp1_raytracer_2223_amd.scene import HostScene
+
+pytestmark = pytest.mark.gpu
+
+DEV = int(os.environ.get("RTX_TEST_DEVICE", "0"))
+KNOBS = ("RTX_INFLIGHT_CRIT", "RTX_SPLIT")
+
+
+def _ctx(**env):
+    saved = {k: os.environ.pop(k, None) for k in KNOBS}
+    os.environ.update(env)
+    try:
+        return DeviceContext(DEV)
+    finally:
+        for k in KNOBS:
+            os.environ.pop(k, None)
+            if saved[k] is not None:
+                os.environ[k] = saved[k]
+
+
+def _share(ctx, frame):
+    ctx.synchronize()
+    abi.check(ctx.lib.rtx_gather_async(ctx.h, frame.ctypes.data_as(C.POINTER(C.c_uint32)), None), "gather", ctx.h)
+    ctx.synchronize()
+    return frame
+
+
+@pytest.mark.parametrize("crit,onepiece", [("1000", True), ("0", False), (None, None)])
+@pytest.mark.parametrize("name,W,H,s_", [("W4_Optional", 1920, 1080, 8), ("Bunny8Lights", 3840, 2160, 8)])
+def test_inflight_frames_equal_one_piece(name, W, H, s_, crit, onepiece):
+    """Rank 0's share of a frame cut over s ranks, two contexts alternating frames in flight after
+    their serialized warm-up (the split tuner measured): RTX_INFLIGHT_CRIT=1000 makes every frame in
+    flight one piece, 0 keeps them split, unset lets the rule choose; the last frames of both contexts
+    (rendered in flight) equal a one-piece context's share."""
+    hs = HostScene(name)
+    s, cam = hs.view()
+    p = abi.make_params(W, H, stripe_rows=16, stripe_first=0, stripe_step=s_)
+    env = {} if crit is None else {"RTX_INFLIGHT_CRIT": crit}
+    pair = [_ctx(**env), _ctx(**env)]
+    ref_ctx = _ctx(RTX_SPLIT="0")
+    try:
+        for c in pair + [ref_ctx]:
+            c.upload(s)
+        ms = C.c_float()
+        for c in pair:
+            abi.check(c.lib.rtx_time_views(c.h, C.byref(cam), 1, C.byref(p), 60, C.byref(ms)), "time", c.h)
+            assert c.split_info()[0] > 0, f"{name}: no heavy tiles to split in the share"
+        for i in range(240):
+            abi.check(pair[i % 2].lib.rtx_render_async(pair[i % 2].h, C.byref(cam), C.byref(p), 0), "render",
+                      pair[i % 2].h)
+        infos = [c.inflight_info() for c in pair]
+        assert all(x["concurrent"] for x in infos), infos
+        if onepiece is not None:
+            assert all(x["onepiece"] == onepiece for x in infos), infos
+        abi.check(ref_ctx.lib.rtx_render_async(ref_ctx.h, C.byref(cam), C.byref(p), 0), "render", ref_ctx.h)
+        ref = _share(ref_ctx, np.zeros(W * H, np.uint32))
+        for c in pair:
+            got = _share(c, np.zeros(W * H, np.uint32))
+            assert np.array_equal(got, ref), f"{name} crit={crit}: {(got != ref).sum()} pixels differ"
+    finally:
+        for c in pair + [ref_ctx]:
+            c.close()
