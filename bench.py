@@ -671,6 +671,8 @@ def main() -> int:
     ap.add_argument("--no-gather", action="store_true", help="skip the host-gather timed region")
     ap.add_argument("--no-extra", action="store_true", help="headline only: no multi_gpu_configs / parity_configs")
     ap.add_argument("--inflight", type=int, default=2, help="frames in flight (render contexts per GPU)")
+    ap.add_argument("--inflight-frame", type=int, default=3,
+                    help="frames in flight for the one-frame-per-step workloads (multi_gpu_configs)")
     args = ap.parse_args()
 
     # RTX_BENCH_DEVICE pins every rank to one device: rehearsing the N-rank path on a one-GPU
@@ -704,9 +706,14 @@ def main() -> int:
 
     # ---- 2. the north star's multi-GPU workloads, one image per step tiled over the N ranks
     multi = []
+    # the one-frame-per-step workloads keep --inflight-frame frames in flight (3: a frame's slowest
+    # tile overlaps two other frames; profiles/r06/bench_inflight3.json: W4_Optional 14.9k -> 17.3k,
+    # Synthetic100k 3.4k -> 4.0k Mpix/s; 4 contexts share hardware queues and lose)
+    fctxs = ctxs + [DeviceContext(dev) for _ in range(max(0, args.inflight_frame - len(ctxs)))]
+    fctxs = fctxs[:max(1, args.inflight_frame)]
     if not args.no_extra:
         for scene, mw, mh, msteps in MULTI_GPU_CONFIGS:
-            wl = Workload(ctxs, d, scene, mw, mh, "frame")
+            wl = Workload(fctxs, d, scene, mw, mh, "frame")
             # (150 warm-up steps: the contexts' in-flight probe, rtx_inflight_info, settles in ~130)
             r = wl.run(msteps, 150, 100, not args.no_gather, f"{tag}_{scene}")
             rec, src = pmc_traffic(scene, mw, mh, 1, N, lib_hash)
@@ -714,6 +721,7 @@ def main() -> int:
             per_rank = d.gather([r["kernel_ms"], r["flop"]])
             entry = {"config": f"{scene} {mw}x{mh}, one frame per step tiled over {N} rank(s) in 16-row stripes",
                      "scene": scene, "width": mw, "height": mh, "n_gpus": N, "steps": msteps,
+                     "frames_in_flight": len(fctxs),
                      "mpix_s": round(r["value"], 3), "ms_per_step": round(r["ms_per_step"], 5),
                      "gathered_mpix_s": r["gathered"]["mpix_s"] if r["gathered"] else None,
                      "roofline_rank0": roofline(r["flop"], r["kernel_ms"], rec, src),
@@ -754,7 +762,7 @@ def main() -> int:
                 exact = next((x for sc, w_, h_, x in PARITY_CONFIGS if (sc, w_, h_) == (scene, mw, mh)), True)
                 entry["parity"] = parity_report(r["px0"], r["rgb0"], scene, mw, mh, exact=exact, with_fnv=False)
             if N == 1:
-                entry["strong_scaling_predictor"] = stripe_predictor(ctxs, wl, lib_hash)
+                entry["strong_scaling_predictor"] = stripe_predictor(fctxs, wl, lib_hash)
             multi.append(entry)
 
     # ---- 3. parity of every config at full size (N = 1; one rank per GPU renders stripes at N > 1)
@@ -837,7 +845,7 @@ def main() -> int:
             out["speedup_vs_cpu_full_host_upper_bound"] = round(hr["value"] / cpu["full_host_upper_bound_mpix_s"], 1)
     if d.rank == 0:
         print(json.dumps(out), flush=True)
-    for c in ctxs:
+    for c in {id(c): c for c in ctxs + fctxs}.values():
         c.close()
     d.close()
     return 0
