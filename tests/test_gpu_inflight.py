@@ -56,13 +56,20 @@ def test_inflight_frames_equal_one_piece(name, W, H, s_, crit, onepiece):
         for c in pair:
             abi.check(c.lib.rtx_time_views(c.h, C.byref(cam), 1, C.byref(p), 60, C.byref(ms)), "time", c.h)
             assert c.split_info()[0] > 0, f"{name}: no heavy tiles to split in the share"
+        seen = {"concurrent": 0, "onepiece": 0}
         for i in range(240):
-            abi.check(pair[i % 2].lib.rtx_render_async(pair[i % 2].h, C.byref(cam), C.byref(p), 0), "render",
-                      pair[i % 2].h)
-        infos = [c.inflight_info() for c in pair]
-        assert all(x["concurrent"] for x in infos), infos
-        if onepiece is not None:
-            assert all(x["onepiece"] == onepiece for x in infos), infos
+            c = pair[i % 2]
+            abi.check(c.lib.rtx_render_async(c.h, C.byref(cam), C.byref(p), 0), "render", c.h)
+            info = c.inflight_info()   # (of the frame just queued)
+            seen["concurrent"] += info["concurrent"]
+            seen["onepiece"] += info["onepiece"]
+        # whether a given frame finds the other context's frame still in flight depends on timing;
+        # most do, and only those may render one piece
+        assert seen["concurrent"] > 0, seen
+        if onepiece is True:
+            assert seen["onepiece"] == seen["concurrent"], seen
+        if onepiece is False:
+            assert seen["onepiece"] == 0, seen
         abi.check(ref_ctx.lib.rtx_render_async(ref_ctx.h, C.byref(cam), C.byref(p), 0), "render", ref_ctx.h)
         ref = _share(ref_ctx, np.zeros(W * H, np.uint32))
         for c in pair:
