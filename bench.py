@@ -569,7 +569,8 @@ def stripe_predictor(ctxs, wl: "Workload", lib_hash: str, steps=(2, 4, 8), launc
 
     def t(p):
         ms = C.c_float()
-        abi.check(lib.rtx_time_views(ctx.h, cam, 1, C.byref(p), 5, C.byref(ms)), "rtx_time_views", ctx.h)
+        # 100 warm-up launches: the share's schedule, split tuner and frontier refinement settle
+        abi.check(lib.rtx_time_views(ctx.h, cam, 1, C.byref(p), 100, C.byref(ms)), "rtx_time_views", ctx.h)
         best = None
         for _ in range(2):
             abi.check(lib.rtx_time_views(ctx.h, cam, 1, C.byref(p), launches, C.byref(ms)), "rtx_time_views", ctx.h)
@@ -579,7 +580,7 @@ def stripe_predictor(ctxs, wl: "Workload", lib_hash: str, steps=(2, 4, 8), launc
     def t_inflight(p, frames=200, warm=200):
         for c in ctxs:   # every context's schedule measured and tuned first, as Workload.run does
             ms = C.c_float()
-            abi.check(lib.rtx_time_views(c.h, cam, 1, C.byref(p), launches, C.byref(ms)), "rtx_time_views", c.h)
+            abi.check(lib.rtx_time_views(c.h, cam, 1, C.byref(p), 100, C.byref(ms)), "rtx_time_views", c.h)
         for i in range(warm):
             abi.check(lib.rtx_render_views_async(ctxs[i % len(ctxs)].h, cam, 1, C.byref(p), 0), "render", ctx.h)
         for c in ctxs:
@@ -593,10 +594,10 @@ def stripe_predictor(ctxs, wl: "Workload", lib_hash: str, steps=(2, 4, 8), launc
 
     t_full = t(abi.make_params(wl.W, wl.H))
     t_full_if = t_inflight(abi.make_params(wl.W, wl.H))
-    out = {"method": f"each share timed alone (rtx_time_views, best of 2 x {launches} launches after 5 warm-up "
+    out = {"method": f"each share timed alone (rtx_time_views, best of 2 x {launches} launches after 100 warm-up "
                      "launches); efficiency = t_full / (s * slowest share)", "t_full_ms": round(t_full, 5),
            "inflight": {"method": f"each share with {len(ctxs)} frames in flight (the rank's contexts alternating, "
-                                  f"wall time per frame of 200 frames after {launches} serialized launches per context "
+                                  "wall time per frame of 200 frames after 100 serialized launches per context "
                                   "and 200 in flight), the full frame likewise: the "
                                   "N-GPU bench's own mode", "frames_in_flight": len(ctxs),
                         "t_full_ms": round(t_full_if, 5)}}

@@ -893,6 +893,16 @@ __device__ __forceinline__ uint32_t q8(float c) {
 // One wave tile of one phase (rtx_render_kernel below dispatches the tiles and describes the phases): `widx` = the
 // wave's index in the launch (PHASE 5: its item), `stk` / `sT` its DFS stacks, `pnum` its shadow-ray
 // plane numerators in LDS.
+// A split wave's duration for the frontier refinement (FrameArgs::part_max), sharded by wave.
+template <int PHASE>
+__device__ __forceinline__ void part_stat(const FrameArgs& F, uint32_t part, uint32_t widx, uint32_t lane,
+                                          unsigned long long t0) {
+    if (!F.part_max || lane != 0) return;
+    const unsigned long long d = (__builtin_amdgcn_s_memtime() - t0) >> 4;
+    atomicMax(F.part_max + ((static_cast<uint32_t>(PHASE) - 1u) * kMaxParts + part) * kPartShards + widx % kPartShards,
+              static_cast<uint32_t>(d < 0xffffffffull ? d : 0xffffffffull));
+}
+
 template <bool COUNT, int PHASE, bool DEEP, int SPEC, bool HSTK, bool CULLK>
 __device__ __forceinline__ void render_tile(const DevScene& S, const FrameArgs& F, uint32_t widx, uint32_t tile,
                                             uint32_t part, uint32_t light, uint4* stk, unsigned long long* sT,
@@ -921,7 +931,7 @@ __device__ __forceinline__ void render_tile(const DevScene& S, const FrameArgs& 
     const ViewCam& V = F.cam[view];
     uint32_t gy = rem / F.tiles_x;
     unsigned long long t_block0 = 0;
-    if (F.cost) t_block0 = __builtin_amdgcn_s_memtime();
+    if (F.cost || ((PHASE == 1 || PHASE == 2) && F.part_max)) t_block0 = __builtin_amdgcn_s_memtime();
     if (F.groups_per_stripe) {
         // view v owns the stripes s with s % step == (first - v) mod step (rtx.h)
         const uint32_t first = (F.stripe_first + F.stripe_step - view % F.stripe_step) % F.stripe_step;
@@ -1089,6 +1099,7 @@ __device__ __forceinline__ void render_tile(const DevScene& S, const FrameArgs& 
         if (valid && sc_t < sc0)   // accepted t >= tmin > 0: the float bits order like the values
             atomicMin(&F.hit_key[slot], (static_cast<unsigned long long>(__float_as_uint(sc_t)) << 32) | sc_tri);
         if (timed && lane == 0 && wdt) part_cost_add(F.cost + tile, wdt);
+        part_stat<PHASE>(F, part, widx, lane, t_block0);
         RTX_SPLIT_STAMP();
         return;
     } else if (PHASE == 2 || PHASE == 3) {
@@ -1342,6 +1353,7 @@ __device__ __forceinline__ void render_tile(const DevScene& S, const FrameArgs& 
         return;
     }
     if (PHASE == 2) {
+        part_stat<PHASE>(F, part, widx, lane, t_block0);
         RTX_SPLIT_STAMP();
         return;
     }
@@ -2139,6 +2151,23 @@ struct rtx_ctx {
     int prev_views = 0;
     ViewCam prev_cam[kMaxViews] = {};
     uint32_t split_parts = kPartsPerMesh;            // RTX_SPLIT_PARTS (tuning)
+    // frontier refinement (kRefineRounds): the current image's parts (host copy of the real entries;
+    // the image reserves kMaxParts), its parts section, the round and state (0 waiting for a split
+    // frame, 1 measured frame queued, 2 done), frames to wait, the last round's longest part wave
+    bool refinable = false;
+    bool refine_off = false;                         // RTX_REFINE=0
+    std::vector<int4> h_parts;
+    std::vector<int4> h_parts_base;                  // the upload's frontier (each launch shape starts from it)
+    int4* parts_dev = nullptr;
+    uint32_t refine_round = 0;
+    int refine_state = 2;
+    uint32_t refine_wait = 0;
+    uint32_t refine_quiet = 0;                       // frames of this shape still to wait
+    uint32_t refine_prev_max = 0;
+    bool refine_rec = false;
+    hipEvent_t ev_refine = nullptr;
+    uint32_t* d_part_max = nullptr;
+    std::vector<uint32_t> h_part_max;
     bool split_ok = false;           // the uploaded scene admits split rendering
     bool deep_stack = false;         // the uploaded scene needs rtx_render_kernel<..., DEEP = true>
     bool hbm_stack = false;          // ... with its stacks in HBM (HSTK = true): kStackDepthDeep or more levels
@@ -2278,6 +2307,24 @@ bool build_parts(const std::vector<float4>& nodes, uint32_t root, uint32_t mesh,
         fr[best] = {link(e.node), e.path, e.depth + 1};
         fr.insert(fr.begin() + best + 1, P{link(e.node) + 1, e.path | (1u << e.depth), e.depth + 1});
     }
+    if (const char* ev = std::getenv("RTX_PART_REFINE")) {   // experiment: split the listed parts once more
+        std::vector<int> idx;
+        for (const char* q = ev; *q;) {
+            char* end = nullptr;
+            const long v = std::strtol(q, &end, 10);
+            if (end == q) break;
+            idx.push_back(static_cast<int>(v));
+            q = *end ? end + 1 : end;
+        }
+        std::sort(idx.begin(), idx.end(), std::greater<int>());
+        for (int k : idx) {
+            if (k < 0 || k >= static_cast<int>(fr.size())) continue;
+            const P e = fr[k];
+            if (ntri(e.node) || e.depth >= 31) continue;
+            fr[k] = {link(e.node), e.path, e.depth + 1};
+            fr.insert(fr.begin() + k + 1, P{link(e.node) + 1, e.path | (1u << e.depth), e.depth + 1});
+        }
+    }
     for (const P& e : fr)
         parts.push_back(make_int4(static_cast<int>(mesh), static_cast<int>(e.node), static_cast<int>(e.path),
                                   static_cast<int>(e.depth)));
@@ -2344,6 +2391,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     if (const char* e = std::getenv("RTX_MOTION")) c->motion_off = std::strcmp(e, "0") == 0;
     if (const char* e = std::getenv("RTX_XCD_ORDER")) c->xcd_order = std::strcmp(e, "1") == 0;
     if (const char* e = std::getenv("RTX_THROUGHPUT")) c->throughput_off = std::strcmp(e, "0") == 0;
+    if (const char* e = std::getenv("RTX_REFINE")) c->refine_off = std::strcmp(e, "0") == 0;
     if (const char* e = std::getenv("RTX_INFLIGHT_CRIT")) {
         const double f = std::atof(e);
         if (f >= 0 && f < 1e6) c->inflight_crit = static_cast<uint32_t>(f * 1000.0);
@@ -2406,6 +2454,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     RTX_CREATE_TRY(hipEventCreateWithFlags(&c->ev_frame, hipEventDisableTiming));
     for (auto& e : c->ev_tune) RTX_CREATE_TRY(hipEventCreate(&e));
     for (auto& e : c->ev_win) RTX_CREATE_TRY(hipEventCreate(&e));
+    RTX_CREATE_TRY(hipEventCreateWithFlags(&c->ev_refine, hipEventDisableTiming));
     RTX_CREATE_TRY(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
     if (const char* e = std::getenv("RTX_SPLIT_PRIO"); e && std::strcmp(e, "0") == 0) hi_prio = lo_prio;
     RTX_CREATE_TRY(hipStreamCreateWithPriority(&c->split_stream, hipStreamNonBlocking, hi_prio));
@@ -2476,6 +2525,8 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : c->ev_win)
         if (e) (void)hipEventDestroy(e);
+    if (c->ev_refine) (void)hipEventDestroy(c->ev_refine);
+    (void)hipFree(c->d_part_max);
     if (c->split_stream) {
         (void)hipStreamSynchronize(c->split_stream);
         (void)hipStreamDestroy(c->split_stream);
@@ -2811,6 +2862,14 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
     }
     if (parts.size() > static_cast<size_t>(kMaxParts)) split_ok = false;
     if (!split_ok) parts.clear();
+    // static uploads reserve kMaxParts entries for the frontier refinement (refine_round); meshes
+    // with device-rebuild reserves keep theirs exactly
+    bool any_reserve = false;
+    if (lay)
+        for (uint8_t r : lay->reserve) any_reserve = any_reserve || r != 0;
+    const size_t n_parts_real = parts.size();
+    const bool refinable = split_ok && n_parts_real > 0 && !any_reserve;
+    if (refinable) parts.resize(kMaxParts, make_int4(-1, 0, 0, 0));
     // Cull records' inputs: per node slot the range of device triangles under it (leaf order is
     // contiguous within a subtree; children's slots follow their parent's, so one backward sweep)
     // and per light the tmax up to which its shadow rays are culled: 4x the farthest mesh-box
@@ -3008,7 +3067,7 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
     d.lights = reinterpret_cast<const float4*>(base + secs[6].off);
     d.materials = reinterpret_cast<const float4*>(base + secs[7].off);
     d.parts = reinterpret_cast<const int4*>(base + secs[8].off);
-    d.n_parts = static_cast<uint32_t>(parts.size());
+    d.n_parts = static_cast<uint32_t>(n_parts_real);
     d.n_spheres = s->n_spheres; d.n_planes = s->n_planes; d.n_meshes = s->n_meshes;
     d.n_lights = s->n_lights; d.n_materials = nm;
     d.tri_fast = max_ee <= 0x1p56 ? 1u : 0u;
@@ -3066,6 +3125,14 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
                         (cull_back ? kSpecCullBack : 0);
     }
     c->split_ok = split_ok && !parts.empty() && !c->deep_stack;
+    c->refinable = refinable && c->split_ok && !c->refine_off;
+    c->h_parts.assign(parts.begin(), parts.begin() + static_cast<std::ptrdiff_t>(n_parts_real));
+    c->h_parts_base = c->h_parts;
+    c->parts_dev = reinterpret_cast<int4*>(base + secs[8].off);
+    c->refine_round = 0;
+    c->refine_state = c->refinable ? 0 : 2;
+    c->refine_wait = 0;
+    c->refine_prev_max = 0;
     c->has_scene = true;
     ++c->scene_gen;
     c->scene_sig = std::to_string(d.n_spheres) + "/" + std::to_string(d.n_planes) + "/" + std::to_string(d.n_meshes) +
@@ -3119,6 +3186,97 @@ void split_tune(rtx_ctx* c, float main_ms, float chain_ms) {
     c->tune_dir = dir;
     const double f = static_cast<double>(base) * (dir > 0 ? c->tune_step : 1.0 / c->tune_step);
     c->split_permille = static_cast<uint32_t>(std::min(4000.0, std::max(1000.0, f)));
+}
+
+// One round of the frontier refinement (kRefineRounds), once the measured frame has completed
+// (rtx_ctx::ev_refine; not waited for): per part the longest closest-hit wave plus the longest
+// shadow wave; the parts within kRefineTopPermille of the longest are replaced by their two
+// children (inner nodes only; the order of the frontier kept), and the new frontier is copied into
+// the image's parts section on the frame stream, behind every frame already queued.
+int refine_round(rtx_ctx* c) {
+    const hipError_t q = hipEventQuery(c->ev_refine);
+    (void)hipGetLastError();   // (not-ready is no error for the caller's checks)
+    if (q == hipErrorNotReady) return RTX_OK;
+    HIP_TRY(c, q);
+    HIP_TRY(c, hipMemcpy(c->h_part_max.data(), c->d_part_max, c->h_part_max.size() * sizeof(uint32_t),
+                         hipMemcpyDeviceToHost));
+    const size_t np = c->h_parts.size();
+    std::vector<uint64_t> m(np, 0);
+    uint64_t top = 0;
+    for (size_t p = 0; p < np; ++p) {
+        uint32_t a = 0, b = 0;
+        for (int k = 0; k < kPartShards; ++k) {
+            a = std::max(a, c->h_part_max[(0 * kMaxParts + p) * kPartShards + k]);
+            b = std::max(b, c->h_part_max[(1 * kMaxParts + p) * kPartShards + k]);
+        }
+        m[p] = static_cast<uint64_t>(a) + b;
+        top = std::max(top, m[p]);
+    }
+    ++c->refine_round;
+    // done: nothing measured, the last round gained under 10 %, or the rounds are spent
+    const bool gained = c->refine_prev_max == 0 || top * 10 < static_cast<uint64_t>(c->refine_prev_max) * 9;
+    c->refine_prev_max = static_cast<uint32_t>(std::min<uint64_t>(top, 0xffffffffull));
+    c->refine_state = 2;
+    if (top * kSplitMinUs < static_cast<uint64_t>(kRefineMinUs) * kSplitMinCost || !gained) return RTX_OK;
+    // only a chain whose longest waves outlast the main kernel by kRefineOverMain: with less, the
+    // frame is bound by its work (more parts only add waves; frames in flight lose throughput)
+    const double top_ms = static_cast<double>(top) * kSplitMinUs / kSplitMinCost * 1e-3;
+    if (c->tune_main_ms > 0.f && top_ms * 1000.0 < static_cast<double>(kRefineOverMainPermille) * c->tune_main_ms)
+        return RTX_OK;
+    std::vector<size_t> cand;
+    for (size_t p = 0; p < np; ++p)
+        if (c->h_parts[p].x >= 0 && m[p] * 1000 >= top * kRefineTopPermille && c->h_parts[p].w < 31) cand.push_back(p);
+    std::sort(cand.begin(), cand.end(), [&](size_t x, size_t y) { return m[x] > m[y]; });
+    if (cand.size() > kRefineSplits) cand.resize(kRefineSplits);
+    std::vector<char> cut(np, 0);
+    size_t n_new = np;
+    for (size_t p : cand) {
+        // the part's node record (copy 0 of the node array): children only under an inner node
+        float4 rec[2];
+        HIP_TRY(c, hipMemcpy(rec, c->dev.nodes + 2ull * static_cast<uint32_t>(c->h_parts[p].y), sizeof rec,
+                             hipMemcpyDeviceToHost));
+        uint32_t link, ntri;
+        std::memcpy(&link, &rec[1].z, 4);
+        std::memcpy(&ntri, &rec[1].w, 4);
+        if (ntri != 0 || n_new + 1 > static_cast<size_t>(kMaxParts)) continue;
+        cut[p] = 1;
+        ++n_new;
+        // (device layout: an inner node's link is its child pair's byte offset, 32 B a slot)
+        c->h_parts[p].y = static_cast<int>(link / 32u);   // the left child; the right one is inserted below
+    }
+    if (n_new == np) return RTX_OK;
+    std::vector<int4> fr;
+    fr.reserve(n_new);
+    for (size_t p = 0; p < np; ++p) {
+        const int4 e = c->h_parts[p];
+        if (!cut[p]) {
+            fr.push_back(e);
+            continue;
+        }
+        fr.push_back(make_int4(e.x, e.y, e.z, e.w + 1));
+        fr.push_back(make_int4(e.x, e.y + 1, e.z | (1 << e.w), e.w + 1));
+    }
+    c->h_parts.swap(fr);
+    HIP_TRY(c, hipMemcpyAsync(c->parts_dev, c->h_parts.data(), c->h_parts.size() * sizeof(int4), hipMemcpyHostToDevice,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));   // (the host copy is replaced by the next round)
+    c->dev.n_parts = static_cast<uint32_t>(c->h_parts.size());
+    if (c->tune_on) {   // a shorter chain: the split factor is balanced again from where it is
+        c->tune_done = false;
+        c->tune_steps = 0;
+        c->tune_dir = 0;
+        c->tune_step = 1.15f;
+        c->tune_best_span = 0.f;
+        c->tune_best_permille = 0;
+        c->win_state = 0;
+        c->win_frames = 0;
+        c->win_interval_ms = 0.f;
+    }
+    if (c->refine_round < kRefineRounds) {
+        c->refine_state = 0;
+        c->refine_wait = 8;   // frames of the new frontier before it is measured
+    }
+    return RTX_OK;
 }
 
 // The heaviest tile's serialized one-piece time over the split frame's serialized span (the tuner's
@@ -3312,6 +3470,21 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         c->sched_frame = 0;
         c->motion_left = 0;
         c->max_cost_serial = 0;
+        if (c->refinable) {   // a new shape refines from the upload's frontier
+            if (c->h_parts.size() != c->h_parts_base.size()) {
+                c->h_parts = c->h_parts_base;
+                HIP_TRY(c, hipMemcpyAsync(c->parts_dev, c->h_parts.data(), c->h_parts.size() * sizeof(int4),
+                                          hipMemcpyHostToDevice, c->stream));
+                HIP_TRY(c, hipStreamSynchronize(c->stream));
+                c->dev.n_parts = static_cast<uint32_t>(c->h_parts.size());
+            }
+            c->refine_round = 0;
+            c->refine_state = 0;
+            c->refine_wait = 0;
+            c->refine_prev_max = 0;
+            c->refine_rec = false;
+            c->refine_quiet = kRefineQuiet;
+        }
         c->win_state = 0;
         c->win_frames = 0;
         c->win_interval_ms = 0.f;
@@ -3372,6 +3545,22 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
     c->frame_onepiece = c->concurrent && c->heavy_n > 0 && inflight_onepiece(c, others + 1);
     const bool split = c->split_mode != 0 && c->split_ok && c->sched_enabled && c->heavy_n > 0 && !c->frame_onepiece;
     F.heavy_flag = split ? c->d_heavy_flag[c->heavy_cur] : nullptr;
+    F.part_max = nullptr;
+    if (c->refine_state == 1) {
+        const int rc = refine_round(c);
+        if (rc != RTX_OK) return rc;
+    }
+    if (c->refine_quiet) --c->refine_quiet;
+    if (split && c->refine_state == 0 && !motion && c->renders_since_upload >= kRefineQuiet && c->refine_quiet == 0 &&
+        (c->refine_wait == 0 || --c->refine_wait == 0)) {
+        if (!c->d_part_max) {
+            HIP_TRY(c, hipMalloc(&c->d_part_max, 2ull * kMaxParts * kPartShards * sizeof(uint32_t)));
+            c->h_part_max.resize(2ull * kMaxParts * kPartShards);
+        }
+        HIP_TRY(c, hipMemsetAsync(c->d_part_max, 0, 2ull * kMaxParts * kPartShards * sizeof(uint32_t), c->stream));
+        F.part_max = c->d_part_max;
+        c->refine_rec = true;
+    }
     F.heavy_list = c->d_heavy_list[c->heavy_cur];
     F.heavy_n = split ? c->heavy_n : 0u;
     F.hit_key = c->d_hit_key;
@@ -3587,6 +3776,11 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
     // factor: W4_Bunny) skips the event and the registry's lock on every frame.
     const bool tracked = c->split_ok && c->split_mode != 0 && !(c->heavy_n == 0 && c->tune_done);
     if (c->win_rec >= 0) HIP_TRY(c, hipEventRecord(c->ev_win[c->win_rec], c->stream));
+    if (c->refine_rec) {   // the measured frame's end (its chain joined): its part statistics are complete
+        HIP_TRY(c, hipEventRecord(c->ev_refine, c->stream));
+        c->refine_rec = false;
+        c->refine_state = 1;
+    }
     if (tracked) {
         HIP_TRY(c, hipEventRecord(c->ev_frame, c->stream));
         if (!c->in_registry) {

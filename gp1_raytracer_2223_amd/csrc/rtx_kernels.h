@@ -34,6 +34,24 @@ constexpr uint32_t kCullWorthReuse = 16;  // animated uploads per cull worth est
 constexpr int kPartsPerMesh = 64;      // target frontier size per mesh BVH (with the exact cull, Synthetic100k
                                        // 1080p: 64 parts 1.00 ms, 128 1.12, 256 1.46; before it 128 beat 64 by 6 %)
 constexpr int kMaxParts = 1024;        // all meshes together
+// Frontier refinement (rtx_ctx::refine_*): a static scene's split frame is measured per part (its
+// longest closest-hit and shadow waves), and the parts whose waves are within kRefineTopPermille /
+// 1000 of the longest are cut into their two children (at most kRefineSplits per round, kRefineRounds
+// rounds, kRefineQuiet frames after an upload): the chain's critical path is its longest part waves
+// (profiles/r06/floor_hist_chain.jsonl), and cutting the few heaviest parts shortens it
+// (profiles/r06/part_refine.txt: Synthetic100k share of 8 0.607 -> 0.441-0.473 ms).
+constexpr int kPartShards = 16;
+constexpr uint32_t kRefineRounds = 3;
+constexpr uint32_t kRefineSplits = 8;
+constexpr uint32_t kRefineTopPermille = 600;
+constexpr uint32_t kRefineQuiet = 32;
+// ... and only while the longest part waves (closest hit + shadow) exceed kRefineMinUs: shorter ones
+// are not the chain's cost (its launches are), and more parts only add waves (Bunny + 8 lights)
+constexpr uint32_t kRefineMinUs = 100;
+// ... and than kRefineOverMainPermille / 1000 x the split frame's main kernel (the tuner's last): a
+// whole 1080p Synthetic100k frame (main kernel ~0.8 ms, longest part waves ~0.7) is bound by its work,
+// and its frames in flight lost throughput to the extra part waves (0.51 -> 0.56 ms per frame)
+constexpr uint32_t kRefineOverMainPermille = 1500;
 constexpr int kMaxHeavyTiles = 8192;   // heavy wave tiles per frame (hit-key buffer: 64 px each)
 // split factor floor while other contexts' frames are in flight (rtx_ctx::ev_frame)
 constexpr uint32_t kThroughputPermille = 2600;
@@ -218,6 +236,9 @@ struct FrameArgs {
     uint32_t heavy_n;                           // entries of heavy_list in use
     unsigned long long* __restrict__ hit_key;   // per heavy pixel: min {t bits, triangle}
     uint32_t* __restrict__ occ_bits;            // per heavy pixel: bit l = mesh occludes light l
+    // split launches of a frame the frontier refinement measures (rtx_ctx::refine_*; else null): per
+    // (phase 1/2, part, shard) the longest wave, 16-cycle units (atomicMax; shard = wave % kPartShards)
+    uint32_t* __restrict__ part_max;
     // Light-major frame (small shares): PHASE 4 writes each pixel's hit record, PHASE 5
     // runs one (tile, light) shadow ray per wave (items in cost order, the light fastest), publishes
     // the occluded lanes and the tile's last light wave shades every light in the reference's order.

@@ -26,5 +26,5 @@ abi.check(ctx.lib.rtx_time_views(ctx.h, cam, 1, C.byref(p), int(1000 * 0.05 / ma
           ctx.h)
 abi.check(ctx.lib.rtx_time_views(ctx.h, cam, 1, C.byref(p), frames, C.byref(ms)), "t", ctx.h)
 print(f"{scene} {W}x{H} s={st}: {ms.value:.5f} ms per frame (serialized), light-major {ctx.light_major_info()[0]}, "
-      f"heavy {ctx.split_info()[0]}")
+      f"heavy {ctx.split_info()[0]}, parts {ctx.split_info()[1]}")
 ctx.close()
