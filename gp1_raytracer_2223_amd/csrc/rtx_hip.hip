@@ -2156,6 +2156,8 @@ struct rtx_ctx {
     // frame, 1 measured frame queued, 2 done), frames to wait, the last round's longest part wave
     bool refinable = false;
     bool refine_off = false;                         // RTX_REFINE=0
+    // RTX_REFINE_ROUNDS / _SPLITS / _TOP (permille): the kRefine* constants (tuning)
+    uint32_t refine_rounds = kRefineRounds, refine_splits = kRefineSplits, refine_top = kRefineTopPermille;
     std::vector<int4> h_parts;
     std::vector<int4> h_parts_base;                  // the upload's frontier (each launch shape starts from it)
     int4* parts_dev = nullptr;
@@ -2392,6 +2394,9 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     if (const char* e = std::getenv("RTX_XCD_ORDER")) c->xcd_order = std::strcmp(e, "1") == 0;
     if (const char* e = std::getenv("RTX_THROUGHPUT")) c->throughput_off = std::strcmp(e, "0") == 0;
     if (const char* e = std::getenv("RTX_REFINE")) c->refine_off = std::strcmp(e, "0") == 0;
+    if (const char* e = std::getenv("RTX_REFINE_ROUNDS")) c->refine_rounds = static_cast<uint32_t>(std::atoi(e));
+    if (const char* e = std::getenv("RTX_REFINE_SPLITS")) c->refine_splits = static_cast<uint32_t>(std::atoi(e));
+    if (const char* e = std::getenv("RTX_REFINE_TOP")) c->refine_top = static_cast<uint32_t>(std::atoi(e));
     if (const char* e = std::getenv("RTX_INFLIGHT_CRIT")) {
         const double f = std::atof(e);
         if (f >= 0 && f < 1e6) c->inflight_crit = static_cast<uint32_t>(f * 1000.0);
@@ -3225,9 +3230,9 @@ int refine_round(rtx_ctx* c) {
         return RTX_OK;
     std::vector<size_t> cand;
     for (size_t p = 0; p < np; ++p)
-        if (c->h_parts[p].x >= 0 && m[p] * 1000 >= top * kRefineTopPermille && c->h_parts[p].w < 31) cand.push_back(p);
+        if (c->h_parts[p].x >= 0 && m[p] * 1000 >= top * c->refine_top && c->h_parts[p].w < 31) cand.push_back(p);
     std::sort(cand.begin(), cand.end(), [&](size_t x, size_t y) { return m[x] > m[y]; });
-    if (cand.size() > kRefineSplits) cand.resize(kRefineSplits);
+    if (cand.size() > c->refine_splits) cand.resize(c->refine_splits);
     std::vector<char> cut(np, 0);
     size_t n_new = np;
     for (size_t p : cand) {
@@ -3272,7 +3277,7 @@ int refine_round(rtx_ctx* c) {
         c->win_frames = 0;
         c->win_interval_ms = 0.f;
     }
-    if (c->refine_round < kRefineRounds) {
+    if (c->refine_round < c->refine_rounds) {
         c->refine_state = 0;
         c->refine_wait = 8;   // frames of the new frontier before it is measured
     }
