@@ -2110,6 +2110,19 @@ struct rtx_ctx {
     // serialized measurement (cost units), the threshold (RTX_INFLIGHT_CRIT), and whether the last
     // frame rendered one piece because of it
     uint32_t max_cost_serial = 0;
+    // deferred join (rtx_ctx::join_pending): the last frame's split chain has not been joined into the
+    // frame stream; the next frame's main kernel may start beside it when it repeats the frame exactly
+    // (same parameters, cameras, scene image and heavy set: the two write disjoint tiles) — anything
+    // else joins first (join_split).  join_*: that frame's identity.
+    bool join_pending = false;
+    bool join_off = false;                      // RTX_DEFER_JOIN=0
+    rtx_render_params join_p{};
+    rtx_camera join_cams[kMaxViews]{};
+    int join_views = 0;
+    uint64_t join_gen = 0;
+    int join_sb = -1;
+    const uint32_t* join_heavy = nullptr;
+    uint32_t join_heavy_n = 0;
     // the split frames' interval in flight on this context's stream (inflight_onepiece): 0 skipping
     // kInflightWindowSkip frames, 2 timing kInflightWindow frames, 3 waiting for the end event, 4 done
     uint32_t win_state = 0;
@@ -2394,6 +2407,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     if (const char* e = std::getenv("RTX_XCD_ORDER")) c->xcd_order = std::strcmp(e, "1") == 0;
     if (const char* e = std::getenv("RTX_THROUGHPUT")) c->throughput_off = std::strcmp(e, "0") == 0;
     if (const char* e = std::getenv("RTX_REFINE")) c->refine_off = std::strcmp(e, "0") == 0;
+    if (const char* e = std::getenv("RTX_DEFER_JOIN")) c->join_off = std::strcmp(e, "0") == 0;
     if (const char* e = std::getenv("RTX_REFINE_ROUNDS")) c->refine_rounds = static_cast<uint32_t>(std::atoi(e));
     if (const char* e = std::getenv("RTX_REFINE_SPLITS")) c->refine_splits = static_cast<uint32_t>(std::atoi(e));
     if (const char* e = std::getenv("RTX_REFINE_TOP")) c->refine_top = static_cast<uint32_t>(std::atoi(e));
@@ -2492,6 +2506,7 @@ extern "C" void rtx_destroy(rtx_ctx* c) {
     if (!c) return;
     frames_forget(c);
     (void)hipSetDevice(c->device);
+    if (c->split_stream) (void)hipStreamSynchronize(c->split_stream);   // (a deferred chain, join_pending)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& B : c->sb) {
         (void)hipFree(B.d);
@@ -2567,6 +2582,7 @@ struct UploadLayout {
 };
 
 int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay);
+int join_split(rtx_ctx* c);
 
 // Queue the record launches on the context stream: with `boxes` (at upload) the box tree and
 // every slot's box, then, for the anchors in A, their margin trees and records.  Grows the
@@ -2697,6 +2713,7 @@ extern "C" int rtx_upload_scene(rtx_ctx* c, const rtx_scene* s) {
         c->short_uploads = (c->has_scene && c->renders_since_upload <= 1) ? c->short_uploads + 1 : 0;
         c->renders_since_upload = 0;
         c->upload_motion = c->short_uploads >= 1;
+        if (const int rc = join_split(c); rc != RTX_OK) return rc;   // (the last chain reads the current image)
     }
     return upload_scene(c, s, nullptr);
 }
@@ -3193,6 +3210,15 @@ void split_tune(rtx_ctx* c, float main_ms, float chain_ms) {
     c->split_permille = static_cast<uint32_t>(std::min(4000.0, std::max(1000.0, f)));
 }
 
+// Join the last frame's split chain into the frame stream (rtx_ctx::join_pending) before anything
+// that reads its pixels, reallocates or rewrites what it reads, or needs the frame complete.
+int join_split(rtx_ctx* c) {
+    if (!c->join_pending) return RTX_OK;
+    c->join_pending = false;
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    return RTX_OK;
+}
+
 // One round of the frontier refinement (kRefineRounds), once the measured frame has completed
 // (rtx_ctx::ev_refine; not waited for): per part the longest closest-hit wave plus the longest
 // shadow wave; the parts within kRefineTopPermille of the longest are replaced by their two
@@ -3262,6 +3288,7 @@ int refine_round(rtx_ctx* c) {
         fr.push_back(make_int4(e.x, e.y + 1, e.z | (1 << e.w), e.w + 1));
     }
     c->h_parts.swap(fr);
+    if (const int rc = join_split(c); rc != RTX_OK) return rc;   // (the chain may still read the parts)
     HIP_TRY(c, hipMemcpyAsync(c->parts_dev, c->h_parts.data(), c->h_parts.size() * sizeof(int4), hipMemcpyHostToDevice,
                               c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));   // (the host copy is replaced by the next round)
@@ -3343,6 +3370,18 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         return fail(c, RTX_E_INVALID, "stripe_rows must be a multiple of 16 and stripe_first < stripe_step");
     const size_t npx = static_cast<size_t>(p->width) * p->height * static_cast<size_t>(n_views);
     HIP_TRY(c, hipSetDevice(c->device));
+    if (c->join_pending &&
+        !(n_views == c->join_views && c->scene_gen == c->join_gen && c->sb_cur == c->join_sb &&
+          std::memcmp(p, &c->join_p, sizeof *p) == 0 &&
+          std::memcmp(cams, c->join_cams, sizeof(rtx_camera) * static_cast<size_t>(n_views)) == 0)) {
+        const int rc = join_split(c);
+        if (rc != RTX_OK) return rc;
+    }
+    c->join_p = *p;   // this frame's identity, for the next frame's test above
+    std::memcpy(c->join_cams, cams, sizeof(rtx_camera) * static_cast<size_t>(n_views));
+    c->join_views = n_views;
+    c->join_gen = c->scene_gen;
+    c->join_sb = c->sb_cur;
     if (npx > c->px_cap) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         (void)hipFree(c->d_px);
@@ -3477,6 +3516,7 @@ int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_pa
         c->max_cost_serial = 0;
         if (c->refinable) {   // a new shape refines from the upload's frontier
             if (c->h_parts.size() != c->h_parts_base.size()) {
+                if (const int rc = join_split(c); rc != RTX_OK) return rc;
                 c->h_parts = c->h_parts_base;
                 HIP_TRY(c, hipMemcpyAsync(c->parts_dev, c->h_parts.data(), c->h_parts.size() * sizeof(int4),
                                           hipMemcpyHostToDevice, c->stream));
@@ -3669,6 +3709,12 @@ int ensure_hbm_stacks(rtx_ctx* c, uint32_t groups) {
 // executed tests (its counting variant, rtx_count_work_culled; the plain one without records)
 int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
     if (grid.x == 0 || grid.y == 0) return RTX_OK;
+    // (prepare joined already unless this frame repeats the last one's parameters and cameras)
+    if (c->join_pending && (count || F.cost || F.part_max || F.lm_lights || c->concurrent || c->hbm_stack ||
+                            c->deep_stack || F.heavy_flag != c->join_heavy || F.heavy_n != c->join_heavy_n)) {
+        const int rc = join_split(c);
+        if (rc != RTX_OK) return rc;
+    }
     if (c->hbm_stack) {
         const int rc = ensure_hbm_stacks(c, grid.x);
         if (rc != RTX_OK) return rc;
@@ -3745,7 +3791,17 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
         launch_phase<0>(v, grid, c->stream, c->dev, F);
     HIP_TRY(c, hipGetLastError());
     if (F.heavy_flag && c->tune_rec && F.cost) HIP_TRY(c, hipEventRecord(c->ev_tune[1], c->stream));
-    if (F.heavy_flag) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    if (F.heavy_flag) {
+        // a plain repeat of the frame defers the join to the next frame or reader (rtx_ctx::join_pending);
+        // a measured, tuned, refined or in-flight one joins now
+        if (F.cost || F.part_max || c->concurrent || c->join_off || c->tune_rec || c->refine_rec) {
+            HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+        } else {
+            c->join_pending = true;
+            c->join_heavy = F.heavy_flag;
+            c->join_heavy_n = F.heavy_n;
+        }
+    }
     if (F.cost) {
         const uint32_t slots = (c->split_mode == 0 || !c->split_ok) ? 0u
                                : (c->split_mode == 2 ? 0xffffffffu : c->split_slots);
@@ -3827,6 +3883,7 @@ extern "C" int rtx_render_async(rtx_ctx* c, const rtx_camera* cam, const rtx_ren
 extern "C" int rtx_synchronize(rtx_ctx* c) {
     if (!c) return RTX_E_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));
+    if (const int rc = join_split(c); rc != RTX_OK) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return RTX_OK;
 }
@@ -3843,6 +3900,7 @@ int queue_owned_copy(rtx_ctx* c, uint32_t* out_px, float* out_rgb) {
     if (out_rgb && !c->last_rgb) return fail(c, RTX_E_STATE, "last render did not produce colours");
     const rtx_render_params& p = c->last;
     HIP_TRY(c, hipSetDevice(c->device));
+    if (const int rc = join_split(c); rc != RTX_OK) return rc;
     const size_t W = p.width, H = p.height;
     const bool striped = p.stripe_rows != 0 && p.stripe_step > 1;
     for (int v = 0; v < c->last_views; ++v) {
@@ -3916,6 +3974,7 @@ extern "C" int rtx_render(rtx_ctx* c, const rtx_camera* cam, const rtx_render_pa
 
 extern "C" int rtx_device_buffers(rtx_ctx* c, void** d_px, void** d_rgb) {
     if (!c) return RTX_E_INVALID;
+    if (const int rc = join_split(c); rc != RTX_OK) return rc;   // (the caller orders its work after the stream)
     if (d_px) *d_px = c->d_px;
     if (d_rgb) *d_rgb = c->d_rgb;
     return RTX_OK;
@@ -3941,6 +4000,7 @@ extern "C" int rtx_time_views(rtx_ctx* c, const rtx_camera* cams, int n_views, c
         rc = launch(c, F, grid, false);
         if (rc != RTX_OK) return rc;
     }
+    if (const int rc2 = join_split(c); rc2 != RTX_OK) return rc2;   // (the last chain inside the timing)
     HIP_TRY(c, hipEventRecord(c->ev1, c->stream));
     HIP_TRY(c, hipEventSynchronize(c->ev1));
     float ms = 0.f;
@@ -4006,6 +4066,7 @@ extern "C" int rtx_schedule_state(rtx_ctx* c, uint32_t* order, uint32_t* cost, u
     if (!c->sched_ready || !order || !cost) return RTX_OK;
     if (n > c->sched_cap) return fail(c, RTX_E_INVALID, "n exceeds the schedule size");
     HIP_TRY(c, hipSetDevice(c->device));
+    if (const int rc = join_split(c); rc != RTX_OK) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipMemcpy(order, c->d_order, n * 4, hipMemcpyDeviceToHost));
     HIP_TRY(c, hipMemcpy(cost, c->d_saved_cost, n * 4, hipMemcpyDeviceToHost));
@@ -4098,6 +4159,8 @@ extern "C" int rtx_debug_stamps(rtx_ctx* c, const rtx_camera* cam, const rtx_ren
     F.stamps = d;
     F.split_stamps = d + kStampWords * nw;
     rc = launch(c, F, grid, false);
+    if (rc != RTX_OK) return rc;
+    rc = join_split(c);
     if (rc != RTX_OK) return rc;
     HIP_TRY(c, hipMemcpyAsync(out, d, kStampWords * nw * 8, hipMemcpyDeviceToHost, c->stream));
     std::vector<unsigned long long> sh(6 * kMaxParts * kStampShards);
@@ -4219,6 +4282,7 @@ extern "C" int rtx_anim_create(rtx_anim** out, rtx_ctx* c, const rtx_scene* s, c
     *out = nullptr;
     g_anim_err.clear();
     if (!c || !s || !ids || !src || n == 0) return afail(nullptr, RTX_E_INVALID, "null argument or no mesh");
+    if (join_split(c) != RTX_OK) return afail(nullptr, RTX_E_DEVICE, "joining the last split chain");
     if (n > static_cast<uint32_t>(rtxa::kMaxAnimMeshes)) return afail(nullptr, RTX_E_UNSUPPORTED, "more than 32 animated meshes");
     if (c->split_parts > static_cast<uint32_t>(rtxa::kMaxAnimParts))
         return afail(nullptr, RTX_E_UNSUPPORTED, "frontier target above the device builder's 128 parts");
@@ -4376,6 +4440,7 @@ extern "C" int rtx_anim_update(rtx_anim* a, rtx_ctx* c, const float* transforms)
     if (!a || !c || !transforms) return RTX_E_INVALID;
     if (c->device != a->device) return afail(a, RTX_E_INVALID, "context on another device");
     ANIM_TRY(a, hipSetDevice(a->device));
+    if (join_split(c) != RTX_OK) return afail(a, RTX_E_DEVICE, "joining the last split chain");
     // the context's next scene image (as rtx_upload_scene picks it)
     const int k = c->sb_cur < 0 ? 0 : (c->sb_cur ^ 1);
     rtx_ctx::SceneBuf& B = c->sb[k];
@@ -4516,6 +4581,7 @@ extern "C" int rtx_scene_image(rtx_ctx* c, void* out, size_t capacity, size_t* b
     if (!out) return RTX_OK;
     if (capacity < c->scene_bytes) return fail(c, RTX_E_INVALID, "capacity below the image size");
     HIP_TRY(c, hipSetDevice(c->device));
+    if (const int rc = join_split(c); rc != RTX_OK) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipMemcpy(out, c->sb[c->sb_cur].d, c->scene_bytes, hipMemcpyDeviceToHost));
     return RTX_OK;

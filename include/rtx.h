@@ -218,7 +218,9 @@ int rtx_gather_async(rtx_ctx* ctx, uint32_t* out_pixels, float* out_rgb);
  * device of the process (hipHostRegister, portable), and undo it. */
 int rtx_host_register(rtx_ctx* ctx, void* ptr, size_t bytes);
 int rtx_host_unregister(rtx_ctx* ctx, void* ptr);
-/* Device pointers of the HBM frame buffer (width*height uint32 / 3*width*height f32). */
+/* Device pointers of the HBM frame buffer (width*height uint32 / 3*width*height f32).  The
+ * frames queued so far are complete in it after rtx_synchronize (a repeated frame may leave
+ * its split launches running after rtx_render_async returns, on a stream of its own). */
 int rtx_device_buffers(rtx_ctx* ctx, void** d_pixels, void** d_rgb);
 /* ---- one frame over several GPUs from one process ------------------
  * The reference's Renderer::Render covers the frame with parallel_for
