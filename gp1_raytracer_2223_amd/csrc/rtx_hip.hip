@@ -36,8 +36,10 @@
 #include "rtx_fastdiv.h"
 #include "rtx_kernels.h"
 #include "rtx_variants.h"
+#include "rtx_ctx.h"
 
 using namespace rtxd;
+using namespace rtxh;
 
 [[maybe_unused]] constexpr int kStampWords = 8;   // + primary-hit time, shadow-walk time (RTX_STAMPS)
 // split waves' {sum, max, steps} per (phase, part) in 64 shards by wave index: one address per
@@ -1559,12 +1561,7 @@ __device__ __forceinline__ bool cull_domain(float x) { return fabsf(x) <= 0x1p40
 // maps NaN to +inf), so their identity is 0; box bounds never hold a NaN either (an out-of-domain
 // triangle's box is (-inf, +inf)), so min / max are exact folds in any order (only the sign of a
 // zero bound can depend on the order, and no record test observes it).
-struct alignas(8) CullMD {
-    float m, dt;
-};
-struct alignas(16) CullBox {
-    float lo[3], pad0, hi[3], pad1;
-};
+// (CullMD, CullBox: rtx_ctx.h)
 __device__ __forceinline__ CullMD cull_ident(CullMD*) { return {0.f, 0.f}; }
 __device__ __forceinline__ CullBox cull_ident(CullBox*) {
     return {{INFINITY, INFINITY, INFINITY}, 0.f, {-INFINITY, -INFINITY, -INFINITY}, 0.f};
@@ -2043,231 +2040,11 @@ __global__ void __launch_bounds__(kScanThreads) rtx_sched_xcd(const uint32_t* __
 }
 
 // ====================================================================== host side
-struct rtx_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    std::string err;
-    // scene image in HBM (one allocation, 256-B aligned sections)
-    // Two scene images (device + pinned staging), alternated by uploads: an upload packs
-    // into the image no queued frame reads and copies it asynchronously, so the host can
-    // prepare the next animated frame while the GPU renders this one.
-    struct SceneBuf {
-        char* d = nullptr;
-        char* h = nullptr;
-        size_t cap = 0;
-        hipEvent_t done = nullptr;   // recorded after the last frame that reads this image
-        bool pending = false;
-        float4* cull = nullptr;      // the image's cull records (DevScene::cull), device only
-        size_t cull_cap = 0;
-    };
-    SceneBuf sb[2];
-    int sb_cur = -1;
-    size_t scene_bytes = 0;
-    std::string scene_sig;   // topology of the uploaded scene (keeps the tile schedule across re-uploads)
-    DevScene dev{};
-    bool has_scene = false;
-    // frame buffer in HBM
-    uint32_t* d_px = nullptr;
-    float* d_rgb = nullptr;
-    size_t px_cap = 0, rgb_cap = 0;
-    unsigned long long* d_counters = nullptr;
-    // last render
-    // cost-ordered tile dispatch
-    uint32_t* d_order = nullptr;
-    uint32_t* d_order_xcd = nullptr;    // the XCD-affine re-deal of d_order (rtx_sched_xcd)
-    bool xcd_order = false;             // RTX_XCD_ORDER=1
-    uint32_t* d_cost = nullptr;
-    uint32_t* d_saved_cost = nullptr;   // last one-piece cost per tile
-    uint32_t* d_hist = nullptr;         // per (class, chunk) tile counts -> slot bases (rtx_sched_*)
-    unsigned long long* d_csum = nullptr;   // per chunk cost sums
-    unsigned long long* d_thr = nullptr;    // heavy threshold of the measured frame
-    uint32_t sched_cap = 0;
-    std::string sched_key;
-    bool sched_ready = false;
-    bool sched_enabled = true;
-    uint64_t sched_frame = 0;
-    uint64_t scene_gen = 0;
-    // split rendering of heavy tiles: double-buffered flag/list sets (the reorder kernel
-    // fills the staging set; the host adopts it, with its count, at the next frame)
-    uint32_t* d_heavy_flag[2] = {nullptr, nullptr};
-    uint32_t* d_heavy_list[2] = {nullptr, nullptr};
-    uint32_t* d_heavy_n = nullptr;
-    uint32_t* h_heavy_n = nullptr;   // pinned
-    hipEvent_t ev_heavy = nullptr;
-    hipStream_t split_stream = nullptr;   // split launches run beside the main kernel
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    // Throughput mode (prepare): another context of this process on the same device still had a frame
-    // in flight when this one was queued (ev_frame, the end of each queued frame; g_frames).  The
-    // GPU then interleaves the contexts' frames and a tile's critical path is hidden by the other
-    // frames, so the split launches only add work: the measured frames select heavy tiles with at
-    // least kThroughputPermille and the tuner (whose timings the other frames distort) waits.
-    hipEvent_t ev_frame = nullptr;
-    bool in_registry = false;                   // listed in g_frames (its ev_frame is recorded per frame)
-    bool concurrent = false;
-    bool throughput_off = false;                // RTX_THROUGHPUT=0
-    // in flight (kInflightCritPermille): the heaviest tile's one-piece cost measured in the last
-    // serialized measurement (cost units), the threshold (RTX_INFLIGHT_CRIT), and whether the last
-    // frame rendered one piece because of it
-    uint32_t max_cost_serial = 0;
-    // deferred join (rtx_ctx::join_pending): the last frame's split chain has not been joined into the
-    // frame stream; the next frame's main kernel may start beside it when it repeats the frame exactly
-    // (same parameters, cameras, scene image and heavy set: the two write disjoint tiles) — anything
-    // else joins first (join_split).  join_*: that frame's identity.
-    bool join_pending = false;
-    bool join_off = false;                      // RTX_DEFER_JOIN=0
-    rtx_render_params join_p{};
-    rtx_camera join_cams[kMaxViews]{};
-    int join_views = 0;
-    uint64_t join_gen = 0;
-    int join_sb = -1;
-    const uint32_t* join_heavy = nullptr;
-    uint32_t join_heavy_n = 0;
-    // the split frames' interval in flight on this context's stream (inflight_onepiece): 0 skipping
-    // kInflightWindowSkip frames, 2 timing kInflightWindow frames, 3 waiting for the end event, 4 done
-    uint32_t win_state = 0;
-    uint32_t win_frames = 0;
-    int win_rec = -1;                           // the ev_win slot this frame's end records (-1 none)
-    float win_interval_ms = 0.f;
-    hipEvent_t ev_win[2] = {};
-    uint32_t inflight_crit = kInflightCritPermille;
-    bool frame_onepiece = false;
-    int heavy_cur = 0;
-    uint32_t heavy_n = 0;
-    bool heavy_pending = false;
-    uint32_t split_mode = 1;         // 0 off, 1 auto, 2 force (RTX_SPLIT=0 / unset / force)
-    uint32_t split_slots = 0;        // concurrent render waves on this device
-    uint32_t split_permille = kSplitPermille;   // RTX_SPLIT_FACTOR (fixes it: no tuner)
-    uint32_t split_min = kSplitMinCost;         // RTX_SPLIT_MIN_US: the least cost (16-cycle units) a split tile has
-    // Split-threshold tuner: the frame is max(main kernel, split chain), and the
-    // threshold that balances the two is the fastest (Synthetic100k: factor 2.0, W4_Optional 1.5).
-    // A measured frame with split tiles times both (ev_tune: fork, main kernel end, chain end); at
-    // its adoption the factor the timed set was selected with moves toward the balance, by steps
-    // that shrink when the direction flips, until the two are within 4 % or the step is < 1.5 %.
-    bool tune_on = true;                        // RTX_SPLIT_TUNE=0 / RTX_SPLIT_FACTOR: off
-    bool tune_done = false;
-    bool tune_rec = false;                      // the measured frame in flight recorded ev_tune
-    uint32_t tune_rec_permille = 0;             // ... and the factor its (current) heavy set was selected with
-    uint32_t set_permille[2] = {0, 0};          // per heavy set: the factor the schedule selected it with
-    uint32_t tune_steps = 0;
-    int tune_dir = 0;
-    float tune_step = 1.15f;
-    float tune_main_ms = 0.f, tune_chain_ms = 0.f;   // the last timed frame (rtx_split_tune_info)
-    float tune_best_span = 0.f;                 // the fastest max(main, chain) seen, and its factor
-    uint32_t tune_best_permille = 0;
-    hipEvent_t ev_tune[3] = {nullptr, nullptr, nullptr};
-    uint32_t sched_period = kSchedPeriod;       // RTX_SCHED_PERIOD (tuning)
-    // motion mode (kMotionFrames): frames left, and the previous frame's cameras it compares
-    uint32_t motion_left = 0;
-    bool frame_motion = false;                  // the frame being prepared / launched is in motion mode
-    bool motion_off = false;                    // RTX_MOTION=0: always the static schedule (A/B)
-    int prev_views = 0;
-    ViewCam prev_cam[kMaxViews] = {};
-    uint32_t split_parts = kPartsPerMesh;            // RTX_SPLIT_PARTS (tuning)
-    // frontier refinement (kRefineRounds): the current image's parts (host copy of the real entries;
-    // the image reserves kMaxParts), its parts section, the round and state (0 waiting for a split
-    // frame, 1 measured frame queued, 2 done), frames to wait, the last round's longest part wave
-    bool refinable = false;
-    bool refine_off = false;                         // RTX_REFINE=0
-    // RTX_REFINE_ROUNDS / _SPLITS / _TOP (permille): the kRefine* constants (tuning)
-    uint32_t refine_rounds = kRefineRounds, refine_splits = kRefineSplits, refine_top = kRefineTopPermille;
-    std::vector<int4> h_parts;
-    std::vector<int4> h_parts_base;                  // the upload's frontier (each launch shape starts from it)
-    int4* parts_dev = nullptr;
-    uint32_t refine_round = 0;
-    int refine_state = 2;
-    uint32_t refine_wait = 0;
-    uint32_t refine_quiet = 0;                       // frames of this shape still to wait
-    uint32_t refine_prev_max = 0;
-    bool refine_rec = false;
-    hipEvent_t ev_refine = nullptr;
-    uint32_t* d_part_max = nullptr;
-    std::vector<uint32_t> h_part_max;
-    bool split_ok = false;           // the uploaded scene admits split rendering
-    bool deep_stack = false;         // the uploaded scene needs rtx_render_kernel<..., DEEP = true>
-    bool hbm_stack = false;          // ... with its stacks in HBM (HSTK = true): kStackDepthDeep or more levels
-    uint32_t max_depth = 0;          // deepest BVH level of the uploaded scene
-    uint4* d_hstk = nullptr;         // the HBM stacks (and the instrumented variant's masks), grown on demand
-    unsigned long long* d_hstkT = nullptr;
-    size_t hstk_entries = 0;
-    int scene_spec = 0;              // kSpec* facts of the uploaded scene (kernel specialisation)
-    float room_p0[5] = {};           // kSpecRoomPlanes: plane k's origin on axis kRoomAxes[k]
-    bool no_spec = false;            // RTX_NO_SPEC=1: always the generic kernel (tests)
-    unsigned long long* d_hit_key = nullptr;
-    uint32_t* d_occ = nullptr;
-    // Light-major frames (FrameArgs::lm_*, DESIGN.md §6, opt-in): lm_mode 0 never (default), 1 auto
-    // (RTX_LIGHT_MAJOR=auto: a launch of at most lm_tiles wave tiles, kLmSlotsPercent of the resident
-    // wave slots, RTX_LIGHT_MAJOR_TILES), 2 always (RTX_LIGHT_MAJOR=1)
-    uint32_t lm_mode = 0;
-    uint32_t lm_tiles = 0;
-    uint32_t lm_waves = 0;                      // PHASE 5's persistent waves: every resident slot (32 per CU)
-    float4* d_lm_rec = nullptr;                 // 2 float4 per tile pixel
-    unsigned long long* d_lm_mask = nullptr;    // per (tile, light)
-    size_t lm_rec_tiles = 0, lm_mask_cap = 0;
-    bool frame_lm = false;                      // the frame being launched is light-major
-    // exact cull (DevScene::cull): on for host uploads (RTX_NO_CULL=1: off); the
-    // scratch of its record launches (the segment trees of the per-triangle boxes and of each
-    // anchor's margins, the slots' boxes, the trees' arrival counters) and the node-slot ranges
-    // in the current image
-    bool no_cull = false;
-    float cull_ratio = 1.5f;              // CullParams (RTX_CULL_RATIO, RTX_CULL_LEAVES: tuning)
-    double cull_min_sa = 1.5;             // upload_scene's worth test (RTX_CULL_MIN_SA)
-    bool cull_leaves = false;
-    // Animated loops re-upload every frame and render it once, so the records are rebuilt per
-    // frame.  Round 4's records cost more than a frame and were skipped after two such uploads;
-    // the segment-tree records (tens of us) are built for every upload.  RTX_CULL_ANIMATED=0
-    // restores the skip (after two consecutive uploads rendered at most once each, until an
-    // upload is rendered twice).
-    bool cull_animated = true;
-    uint32_t renders_since_upload = 0;
-    uint32_t short_uploads = 0;
-    // An upload in that pattern (the previous upload was rendered at most once too) moves the
-    // geometry under a fixed tile schedule as a moving camera does: the next frame starts motion
-    // mode when the scene has split tiles (prepare; RTX_MOTION=0 turns both off).
-    bool upload_motion = false;
-    // The cull's worth estimate (upload_scene: the surface areas of every node's reference box and
-    // tight box, tens of us of host time per upload) is reused by the uploads of such a loop for
-    // kCullWorthReuse uploads while the scene's counts stay the same: the decision only picks the
-    // faster of two exact walks.
-    int cull_worth = -1;
-    uint32_t cull_worth_age = 0;
-    std::string cull_worth_sig;
-    CullBox* d_cull_btree = nullptr;      // 2n entries
-    CullMD* d_cull_mtree = nullptr;       // 2n entries per anchor of one launch
-    size_t cull_mtree_cap = 0;            // entries d_cull_mtree holds
-    uint32_t cull_failures = 0;           // record builds that failed (the image then renders unculled)
-    uint32_t cull_fail_at = 0, cull_launches = 0;   // RTX_CULL_FAIL=k: the k-th record build fails (tests)
-    CullBox* d_cull_nbox = nullptr;       // per node slot of the current image
-    uint32_t* d_cull_arrive = nullptr;    // per tree (kCullMaxAnchors margin trees, then the box tree)
-    size_t cull_tree_cap = 0, cull_nbox_cap = 0;   // leaves n the trees hold, slots nbox holds
-    uint32_t cull_top_lds = kCullTopLds;  // RTX_CULL_TOP_LDS (tests: the global-memory top levels)
-    const uint2* cull_rng = nullptr;
-    uint32_t cull_nslots = 0, cull_ntris = 0, cull_n = 0;
-    float cull_view[kMaxViews][3] = {};   // camera origin each view's records of the current image were made for
-    uint32_t cull_view_valid = 0;         // bit v: view v's records are current
-    double cull_bmin[3] = {}, cull_bmax[3] = {};   // the meshes' box (a camera anchor's t bound, cull_bt)
-    uint64_t cull_updates = 0;            // camera-anchor record launches so far (rtx_cull_info)
-    float cull_anchor[kMaxViews + kMaxCullLights][5] = {};   // per record copy: anchor xyz, w, bt (rtx_cull_dump)
-    std::vector<std::array<float, 4>> cull_lights;   // the uploaded lights' anchors {origin, T}
-    bool cull_boxes_pending = false;      // an upload's boxes and light records wait for its first frame
-    rtx_render_params last{};
-    int last_views = 1;
-    bool last_valid = false, last_rgb = false;
-};
+// (the context, rtx_ctx, and the frame policies — split tuner, throughput and in-flight choice,
+// frontier refinement, deferred join — live in rtx_ctx.h / rtx_policy.hip)
 
 namespace {
 
-int fail(rtx_ctx* c, int code, const std::string& msg) {
-    if (c) c->err = msg;
-    return code;
-}
-
-#define HIP_TRY(ctx, call)                                                                  \
-    do {                                                                                    \
-        hipError_t e_ = (call);                                                             \
-        if (e_ != hipSuccess)                                                               \
-            return fail((ctx), RTX_E_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
-    } while (0)
 
 inline float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
 inline float bits(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
@@ -2354,32 +2131,6 @@ namespace {
 // Reason for the last failed rtx_create on this thread (rtx_last_error(NULL)).
 thread_local std::string g_create_err;
 
-// The process's contexts that have queued a frame (rtx_ctx::ev_frame), for throughput mode.
-std::mutex g_frames_m;
-std::vector<rtx_ctx*> g_frames;
-
-// The other contexts on c's device with a frame still in flight (their ev_frame not reached).
-uint32_t frames_concurrent(rtx_ctx* c) {
-    std::lock_guard<std::mutex> l(g_frames_m);
-    uint32_t n = 0;
-    for (rtx_ctx* o : g_frames) {
-        if (o == c || o->device != c->device) continue;
-        const hipError_t q = hipEventQuery(o->ev_frame);
-        if (q == hipErrorNotReady) {
-            (void)hipGetLastError();   // (not-ready is no error for the caller's checks)
-            ++n;
-        }
-    }
-    return n;
-}
-void frames_note(rtx_ctx* c) {
-    std::lock_guard<std::mutex> l(g_frames_m);
-    if (std::find(g_frames.begin(), g_frames.end(), c) == g_frames.end()) g_frames.push_back(c);
-}
-void frames_forget(rtx_ctx* c) {
-    std::lock_guard<std::mutex> l(g_frames_m);
-    g_frames.erase(std::remove(g_frames.begin(), g_frames.end(), c), g_frames.end());
-}
 }  // namespace
 
 extern "C" int rtx_create(rtx_ctx** out, int device_id) {
@@ -2582,7 +2333,6 @@ struct UploadLayout {
 };
 
 int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay);
-int join_split(rtx_ctx* c);
 
 // Queue the record launches on the context stream: with `boxes` (at upload) the box tree and
 // every slot's box, then, for the anchors in A, their margin trees and records.  Grows the
@@ -3174,186 +2924,6 @@ int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay) {
 
 namespace {
 
-// One step of the split-threshold tuner (rtx_ctx::tune_*): the timed frame rendered the heavy set
-// selected with factor tune_rec_permille; main = its main kernel, chain = the split launches (both
-// from the fork).  The next factor is a step away from THAT factor (a set selected with an older
-// factor is not evidence about the current one), toward the balance of the two.
-// The frame span max(main, chain) of every factor tried is kept: a step that makes it 5 % worse
-// than the best seen returns to the best and stops (a GPU that cannot run the chain beside the main
-// kernel — a profiler serialising dispatches, another process — would otherwise drift the factor).
-void split_tune(rtx_ctx* c, float main_ms, float chain_ms) {
-    const uint32_t base = c->tune_rec_permille;
-    if (!base || main_ms <= 0.f || chain_ms <= 0.f) return;
-    if (base != c->split_permille) return;   // a set from before the last step: wait for the current one
-    const float span = std::max(main_ms, chain_ms);
-    if (c->tune_best_permille == 0 || span < c->tune_best_span) {
-        c->tune_best_span = span;
-        c->tune_best_permille = base;
-    } else if (span > 1.05f * c->tune_best_span) {
-        c->split_permille = c->tune_best_permille;
-        c->tune_done = true;
-        return;
-    }
-    const float r = chain_ms / main_ms;
-    const int dir = r > 1.04f ? 1 : (r < 0.96f ? -1 : 0);
-    if (dir == 0 || ++c->tune_steps > 16) {
-        c->tune_done = true;
-        return;
-    }
-    if (c->tune_dir != 0 && dir != c->tune_dir) c->tune_step = std::sqrt(c->tune_step);   // overshot
-    if (c->tune_step < 1.015f) {
-        c->tune_done = true;
-        return;
-    }
-    c->tune_dir = dir;
-    const double f = static_cast<double>(base) * (dir > 0 ? c->tune_step : 1.0 / c->tune_step);
-    c->split_permille = static_cast<uint32_t>(std::min(4000.0, std::max(1000.0, f)));
-}
-
-// Join the last frame's split chain into the frame stream (rtx_ctx::join_pending) before anything
-// that reads its pixels, reallocates or rewrites what it reads, or needs the frame complete.
-int join_split(rtx_ctx* c) {
-    if (!c->join_pending) return RTX_OK;
-    c->join_pending = false;
-    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-    return RTX_OK;
-}
-
-// One round of the frontier refinement (kRefineRounds), once the measured frame has completed
-// (rtx_ctx::ev_refine; not waited for): per part the longest closest-hit wave plus the longest
-// shadow wave; the parts within kRefineTopPermille of the longest are replaced by their two
-// children (inner nodes only; the order of the frontier kept), and the new frontier is copied into
-// the image's parts section on the frame stream, behind every frame already queued.
-int refine_round(rtx_ctx* c) {
-    const hipError_t q = hipEventQuery(c->ev_refine);
-    (void)hipGetLastError();   // (not-ready is no error for the caller's checks)
-    if (q == hipErrorNotReady) return RTX_OK;
-    HIP_TRY(c, q);
-    HIP_TRY(c, hipMemcpy(c->h_part_max.data(), c->d_part_max, c->h_part_max.size() * sizeof(uint32_t),
-                         hipMemcpyDeviceToHost));
-    const size_t np = c->h_parts.size();
-    std::vector<uint64_t> m(np, 0);
-    uint64_t top = 0;
-    for (size_t p = 0; p < np; ++p) {
-        uint32_t a = 0, b = 0;
-        for (int k = 0; k < kPartShards; ++k) {
-            a = std::max(a, c->h_part_max[(0 * kMaxParts + p) * kPartShards + k]);
-            b = std::max(b, c->h_part_max[(1 * kMaxParts + p) * kPartShards + k]);
-        }
-        m[p] = static_cast<uint64_t>(a) + b;
-        top = std::max(top, m[p]);
-    }
-    ++c->refine_round;
-    // done: nothing measured, the last round gained under 10 %, or the rounds are spent
-    const bool gained = c->refine_prev_max == 0 || top * 10 < static_cast<uint64_t>(c->refine_prev_max) * 9;
-    c->refine_prev_max = static_cast<uint32_t>(std::min<uint64_t>(top, 0xffffffffull));
-    c->refine_state = 2;
-    if (top * kSplitMinUs < static_cast<uint64_t>(kRefineMinUs) * kSplitMinCost || !gained) return RTX_OK;
-    // only a chain whose longest waves outlast the main kernel by kRefineOverMain: with less, the
-    // frame is bound by its work (more parts only add waves; frames in flight lose throughput)
-    const double top_ms = static_cast<double>(top) * kSplitMinUs / kSplitMinCost * 1e-3;
-    if (c->tune_main_ms > 0.f && top_ms * 1000.0 < static_cast<double>(kRefineOverMainPermille) * c->tune_main_ms)
-        return RTX_OK;
-    std::vector<size_t> cand;
-    for (size_t p = 0; p < np; ++p)
-        if (c->h_parts[p].x >= 0 && m[p] * 1000 >= top * c->refine_top && c->h_parts[p].w < 31) cand.push_back(p);
-    std::sort(cand.begin(), cand.end(), [&](size_t x, size_t y) { return m[x] > m[y]; });
-    if (cand.size() > c->refine_splits) cand.resize(c->refine_splits);
-    std::vector<char> cut(np, 0);
-    size_t n_new = np;
-    for (size_t p : cand) {
-        // the part's node record (copy 0 of the node array): children only under an inner node
-        float4 rec[2];
-        HIP_TRY(c, hipMemcpy(rec, c->dev.nodes + 2ull * static_cast<uint32_t>(c->h_parts[p].y), sizeof rec,
-                             hipMemcpyDeviceToHost));
-        uint32_t link, ntri;
-        std::memcpy(&link, &rec[1].z, 4);
-        std::memcpy(&ntri, &rec[1].w, 4);
-        if (ntri != 0 || n_new + 1 > static_cast<size_t>(kMaxParts)) continue;
-        cut[p] = 1;
-        ++n_new;
-        // (device layout: an inner node's link is its child pair's byte offset, 32 B a slot)
-        c->h_parts[p].y = static_cast<int>(link / 32u);   // the left child; the right one is inserted below
-    }
-    if (n_new == np) return RTX_OK;
-    std::vector<int4> fr;
-    fr.reserve(n_new);
-    for (size_t p = 0; p < np; ++p) {
-        const int4 e = c->h_parts[p];
-        if (!cut[p]) {
-            fr.push_back(e);
-            continue;
-        }
-        fr.push_back(make_int4(e.x, e.y, e.z, e.w + 1));
-        fr.push_back(make_int4(e.x, e.y + 1, e.z | (1 << e.w), e.w + 1));
-    }
-    c->h_parts.swap(fr);
-    if (const int rc = join_split(c); rc != RTX_OK) return rc;   // (the chain may still read the parts)
-    HIP_TRY(c, hipMemcpyAsync(c->parts_dev, c->h_parts.data(), c->h_parts.size() * sizeof(int4), hipMemcpyHostToDevice,
-                              c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));   // (the host copy is replaced by the next round)
-    c->dev.n_parts = static_cast<uint32_t>(c->h_parts.size());
-    if (c->tune_on) {   // a shorter chain: the split factor is balanced again from where it is
-        c->tune_done = false;
-        c->tune_steps = 0;
-        c->tune_dir = 0;
-        c->tune_step = 1.15f;
-        c->tune_best_span = 0.f;
-        c->tune_best_permille = 0;
-        c->win_state = 0;
-        c->win_frames = 0;
-        c->win_interval_ms = 0.f;
-    }
-    if (c->refine_round < c->refine_rounds) {
-        c->refine_state = 0;
-        c->refine_wait = 8;   // frames of the new frontier before it is measured
-    }
-    return RTX_OK;
-}
-
-// The heaviest tile's serialized one-piece time over the split frame's serialized span (the tuner's
-// best: main kernel or chain); 0 until both are known.
-float inflight_ratio(const rtx_ctx* c);
-
-// Whether a frame in flight (k frames of this device's contexts at once) renders one piece
-// (kInflightCritPermille): its heaviest tile is short next to the split frame's serialized span, or
-// the split frames in flight were measured not to overlap (their interval on this context's stream
-// ~ k x the serialized span: the chain's work fills the GPU, so the frames only queue).  Times the
-// interval over kInflightWindow split frames in flight first (rtx_ctx::win_*).
-bool inflight_onepiece(rtx_ctx* c, uint32_t k) {
-    c->win_rec = -1;
-    if (c->inflight_crit == 0) return false;
-    const float r = inflight_ratio(c);
-    if (r > 0.f && r * 1000.f < static_cast<float>(c->inflight_crit)) return true;
-    if (c->win_state == 4)   // measured: overlap = k x span / interval
-        return c->tune_best_span > 0.f && c->win_interval_ms > 0.f &&
-               static_cast<float>(k) * c->tune_best_span < kInflightOverlapMin * c->win_interval_ms;
-    if (c->win_state == 0 && ++c->win_frames >= kInflightWindowSkip) {
-        c->win_state = 2;
-        c->win_frames = 0;
-        c->win_rec = 0;
-    } else if (c->win_state == 2 && ++c->win_frames == kInflightWindow) {
-        c->win_state = 3;
-        c->win_rec = 1;
-    } else if (c->win_state == 3) {
-        const hipError_t q = hipEventQuery(c->ev_win[1]);
-        (void)hipGetLastError();   // (not-ready is no error for the caller's checks)
-        if (q == hipSuccess) {
-            float ms = 0.f;
-            if (hipEventElapsedTime(&ms, c->ev_win[0], c->ev_win[1]) == hipSuccess && ms > 0.f)
-                c->win_interval_ms = ms / static_cast<float>(kInflightWindow);
-            (void)hipGetLastError();
-            c->win_state = 4;
-        }
-    }
-    return false;
-}
-float inflight_ratio(const rtx_ctx* c) {
-    if (c->max_cost_serial == 0 || c->tune_best_span <= 0.f) return 0.f;
-    const float tile_ms = static_cast<float>(c->max_cost_serial) * static_cast<float>(kSplitMinUs) /
-                          static_cast<float>(kSplitMinCost) * 1e-3f;
-    return tile_ms / c->tune_best_span;
-}
 
 int prepare(rtx_ctx* c, const rtx_camera* cams, int n_views, const rtx_render_params* p, bool want_rgb, FrameArgs& F,
             dim3& grid) {
