@@ -57,7 +57,8 @@ def build_host(force: bool = False) -> Path:
 def build_hip(force: bool = False) -> Path:
     LIB.mkdir(exist_ok=True)
     out = LIB / "librtx_hip.so"
-    srcs = [CSRC / "rtx_hip.hip", CSRC / "rtx_policy.hip", CSRC / "rtx_anim.hip", CSRC / "rtx_group.cpp"]
+    srcs = [CSRC / "rtx_hip.hip", CSRC / "rtx_policy.hip", CSRC / "rtx_anim.hip", CSRC / "rtx_anim_host.hip",
+            CSRC / "rtx_group.cpp"]
     deps = srcs + list(CSRC.glob("*.h")) + [INC / "rtx.h", INC / "rtx_diag.h", Path(__file__)]   # flags live here
     if force or _stale(out, deps):
         # -fno-slp-vectorize: the SLP packer turns independent f32 ops into v_pk_* plus

@@ -257,6 +257,24 @@ inline int fail(rtx_ctx* c, int code, const std::string& msg) {
 uint32_t frames_concurrent(rtx_ctx* c);
 void frames_note(rtx_ctx* c);
 void frames_forget(rtx_ctx* c);
+// Layout of an upload whose meshes may reserve rebuild-sized regions (rtx_anim_*): a mesh
+// with reserve[i] set owns 2T node slots from its root (the most a rebuild can number) and
+// exactly `target` frontier entries (unused ones are {-1, ...}), so a device rebuild can
+// rewrite it in place without moving anything else.
+struct UploadLayout {
+    std::vector<uint8_t> reserve;                            // in, per mesh
+    std::vector<uint32_t> tri0, root, part0, part_cap;       // out, per mesh
+    std::vector<int> depth;
+    double max_ee = 0.0;
+    size_t total = 0;
+    uint32_t oct_bytes = 0;
+    size_t tri_off = 0, node_off = 0, part_off = 0, mesh_off = 0;   // section offsets in the image
+};
+
+// Upload a scene into the context's next image (rtx_hip.hip; rtx_upload_scene, and the device
+// Update's registration with `lay`).
+int upload_scene(rtx_ctx* c, const rtx_scene* s, UploadLayout* lay);
+
 // One step of the split-threshold tuner from a timed frame's main kernel and chain (ms).
 void split_tune(rtx_ctx* c, float main_ms, float chain_ms);
 // Join the last frame's deferred split chain into the frame stream (rtx_ctx::join_pending).

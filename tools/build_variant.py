@@ -23,7 +23,8 @@ def main() -> int:
            "-mllvm", "-structurizecfg-skip-uniform-regions=true",
            *([f for f in flags if not any(a.startswith(f.split("=")[0]) for a in args)]), "-fPIC", "-shared",
            "-Wall", f"-I{ROOT / 'include'}", f"-I{PKG / 'csrc'}", *args, str(src),
-           str(PKG / "csrc" / "rtx_policy.hip"), str(PKG / "csrc" / "rtx_anim.hip"), str(PKG / "csrc" / "rtx_group.cpp"), "-o", str(out)]
+           str(PKG / "csrc" / "rtx_policy.hip"), str(PKG / "csrc" / "rtx_anim.hip"),
+           str(PKG / "csrc" / "rtx_anim_host.hip"), str(PKG / "csrc" / "rtx_group.cpp"), "-o", str(out)]
     print(" ".join(cmd[-4:]), flush=True)
     return subprocess.call(cmd)
 
