@@ -239,13 +239,12 @@ struct FrameArgs {
     // split launches of a frame the frontier refinement measures (rtx_ctx::refine_*; else null): per
     // (phase 1/2, part, shard) the longest wave, 16-cycle units (atomicMax; shard = wave % kPartShards)
     uint32_t* __restrict__ part_max;
-    // Light-major frame (small shares): PHASE 4 writes each pixel's hit record, PHASE 5
-    // runs one (tile, light) shadow ray per wave (items in cost order, the light fastest), publishes
-    // the occluded lanes and the tile's last light wave shades every light in the reference's order.
+    // Light-major frame (opt-in): PHASE 4 writes each pixel's hit record, PHASE 5 runs
+    // persistent waves over the (tile, light) shadow rays (items in cost order, the light fastest) and
+    // publishes each light's occluded lanes, PHASE 6 shades every light in the reference's order.
     uint32_t lm_lights;                         // lights per tile (PHASE 5 items = n_tiles x lm_lights)
     float4* __restrict__ lm_rec;                // per tile pixel: {h, n.x}, {n.y, n.z, mat bits, did}
     unsigned long long* __restrict__ lm_mask;   // per (tile, light): the lanes whose shadow ray is occluded
-    uint32_t* __restrict__ lm_arrive;           // per tile: light waves done (0 between frames)
 };
 
 // Light-major frames (opt-in: RTX_LIGHT_MAJOR=1 always, =auto while a launch has at most kLmSlotsPercent /
