@@ -99,6 +99,8 @@ struct rtx_ctx {
     // else joins first (join_split).  join_*: that frame's identity.
     bool join_pending = false;
     bool join_off = false;                      // RTX_DEFER_JOIN=0
+    // frames in flight defer too, except while the in-flight overlap window is timed (RTX_DEFER_INFLIGHT=0: never)
+    bool defer_inflight = true;
     rtx_render_params join_p{};
     rtx_camera join_cams[kMaxViews]{};
     int join_views = 0;

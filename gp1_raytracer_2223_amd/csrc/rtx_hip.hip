@@ -2159,6 +2159,7 @@ extern "C" int rtx_create(rtx_ctx** out, int device_id) {
     if (const char* e = std::getenv("RTX_THROUGHPUT")) c->throughput_off = std::strcmp(e, "0") == 0;
     if (const char* e = std::getenv("RTX_REFINE")) c->refine_off = std::strcmp(e, "0") == 0;
     if (const char* e = std::getenv("RTX_DEFER_JOIN")) c->join_off = std::strcmp(e, "0") == 0;
+    if (const char* e = std::getenv("RTX_DEFER_INFLIGHT")) c->defer_inflight = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RTX_REFINE_ROUNDS")) c->refine_rounds = static_cast<uint32_t>(std::atoi(e));
     if (const char* e = std::getenv("RTX_REFINE_SPLITS")) c->refine_splits = static_cast<uint32_t>(std::atoi(e));
     if (const char* e = std::getenv("RTX_REFINE_TOP")) c->refine_top = static_cast<uint32_t>(std::atoi(e));
@@ -3264,7 +3265,8 @@ int ensure_hbm_stacks(rtx_ctx* c, uint32_t groups) {
 int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
     if (grid.x == 0 || grid.y == 0) return RTX_OK;
     // (prepare joined already unless this frame repeats the last one's parameters and cameras)
-    if (c->join_pending && (count || F.cost || F.part_max || F.lm_lights || c->concurrent || c->hbm_stack ||
+    const bool inflight_join = c->concurrent && (!c->defer_inflight || c->win_state == 2 || c->win_state == 3);
+    if (c->join_pending && (count || F.cost || F.part_max || F.lm_lights || inflight_join || c->hbm_stack ||
                             c->deep_stack || F.heavy_flag != c->join_heavy || F.heavy_n != c->join_heavy_n)) {
         const int rc = join_split(c);
         if (rc != RTX_OK) return rc;
@@ -3348,7 +3350,7 @@ int launch(rtx_ctx* c, const FrameArgs& F, dim3 grid, int count) {
     if (F.heavy_flag) {
         // a plain repeat of the frame defers the join to the next frame or reader (rtx_ctx::join_pending);
         // a measured, tuned, refined or in-flight one joins now
-        if (F.cost || F.part_max || c->concurrent || c->join_off || c->tune_rec || c->refine_rec) {
+        if (F.cost || F.part_max || inflight_join || c->join_off || c->tune_rec || c->refine_rec) {
             HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
         } else {
             c->join_pending = true;
